@@ -1,0 +1,56 @@
+/*
+ * lzma_oracle.h -- TEST INFRASTRUCTURE ONLY (parity checker, never shipped).
+ *
+ * Plain-C restatement of the reference LZMA SDK 9.20 decoder semantics
+ * (LzmaDec.c / Lzma2Dec.c).  Only tests/, __graft_entry__.smoke() and the
+ * cpu_baseline leg of bench.py may load liboracle.so; the product path in
+ * lzma-sdk-zliblike_amd/ never links it.
+ *
+ * Parity is pinned: tests/test_oracle.py checks every function here against
+ * the committed golden vectors in tests/golden/ (generated from the reference
+ * sources compiled in place, oracle/Makefile.ref + tests/golden/make_golden.py).
+ */
+#ifndef LZMA_ORACLE_H
+#define LZMA_ORACLE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* LzmaDecode (LzmaDec.c:972-1002).  *status preset to -1 ("untouched"). */
+int orc_lzma_decode(uint8_t *dst, size_t *dst_len, const uint8_t *src, size_t *src_len,
+                    const uint8_t *props, unsigned props_size, int finish_mode,
+                    int *status);
+
+/* LzmaUncompress (LzmaLib.c:41-46): LzmaDecode with LZMA_FINISH_ANY. */
+int orc_lzma_uncompress(uint8_t *dst, size_t *dst_len, const uint8_t *src,
+                        size_t *src_len, const uint8_t *props, size_t props_size);
+
+/* zlib-like loop over LzmaDec_DecodeToBuf (LzmaDec.c:840-878) with bounded
+ * in/out chunks -- same contract as ref_lzma_stream_decode in ref_shim.c. */
+int orc_lzma_stream_decode(const uint8_t *props, const uint8_t *src, size_t src_total,
+                           uint8_t *out, size_t out_total, size_t in_chunk,
+                           size_t out_chunk, int finish_mode, long long *trace,
+                           int max_calls, size_t *out_len, size_t *in_used);
+
+/* LZMA2 over a flat dictionary (Lzma2Dec.c:90-289, 7zDec.c:181-202 usage). */
+int orc_lzma2_decode(uint8_t *dst, size_t *dst_len, const uint8_t *src, size_t *src_len,
+                     uint8_t prop, int finish_mode, int *status);
+
+/* Batch helper for the CPU baseline: n independent LzmaDecode calls over a
+ * packed layout, spread over `threads` pthreads. Returns number of errors. */
+int orc_lzma_decode_batch(const uint8_t *src, const uint64_t *src_off,
+                          const uint64_t *src_len, const uint8_t *props5,
+                          uint8_t *dst, const uint64_t *dst_off, const uint64_t *dst_cap,
+                          int finish_mode, int32_t *res_out, int32_t *status_out,
+                          uint64_t *dest_len_out, uint64_t *src_len_out, size_t n,
+                          int threads);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

@@ -1,0 +1,156 @@
+"""ctypes handles for the native libraries the tests use.
+
+- ``oracle()``  -> oracle/liboracle.so  (CPU restatement; checker only)
+- ``ref()``     -> oracle/_ref/libref.so (reference sources compiled in place;
+                   present only in the build container, never on the GPU box)
+- ``synth()``   -> lzma-sdk-zliblike_amd/lib/liblzsynth.so (workload generator)
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg touch the
+oracle; the product (lzma-sdk-zliblike_amd/) never does.
+"""
+import ctypes
+import os
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_SO = os.path.join(ROOT, "oracle", "liboracle.so")
+REF_SO = os.path.join(ROOT, "oracle", "_ref", "libref.so")
+SYNTH_SO = os.path.join(ROOT, "lzma-sdk-zliblike_amd", "lib", "liblzsynth.so")
+
+_c = {}
+size_t_p = ctypes.POINTER(ctypes.c_size_t)
+int_p = ctypes.POINTER(ctypes.c_int)
+
+
+def _load(path):
+    if path not in _c:
+        _c[path] = ctypes.CDLL(path)
+    return _c[path]
+
+
+def _decl_decoder(lib, prefix):
+    f = getattr(lib, prefix + "_lzma_decode")
+    f.restype = ctypes.c_int
+    f.argtypes = [ctypes.c_char_p, size_t_p, ctypes.c_char_p, size_t_p, ctypes.c_char_p,
+                  ctypes.c_uint, ctypes.c_int, int_p]
+    f = getattr(lib, prefix + "_lzma_stream_decode")
+    f.restype = ctypes.c_int
+    f.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p,
+                  ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int,
+                  ctypes.POINTER(ctypes.c_longlong), ctypes.c_int, size_t_p, size_t_p]
+    f = getattr(lib, prefix + "_lzma2_decode")
+    f.restype = ctypes.c_int
+    f.argtypes = [ctypes.c_char_p, size_t_p, ctypes.c_char_p, size_t_p, ctypes.c_ubyte,
+                  ctypes.c_int, int_p]
+
+
+def oracle():
+    lib = _load(ORACLE_SO)
+    if not getattr(lib, "_declared", False):
+        _decl_decoder(lib, "orc")
+        f = lib.orc_lzma_decode_batch
+        f.restype = ctypes.c_int
+        f.argtypes = [ctypes.c_void_p] * 12 + [ctypes.c_size_t, ctypes.c_int]
+        lib._declared = True
+    return lib
+
+
+def ref():
+    lib = _load(REF_SO)
+    if not getattr(lib, "_declared", False):
+        _decl_decoder(lib, "ref")
+        f = lib.ref_lzma_encode
+        f.restype = ctypes.c_int
+        f.argtypes = [ctypes.c_char_p, size_t_p, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int,
+                      ctypes.c_uint, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                      ctypes.c_int, ctypes.c_char_p]
+        f = lib.ref_lzma2_encode
+        f.restype = ctypes.c_int
+        f.argtypes = [ctypes.c_char_p, size_t_p, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int,
+                      ctypes.c_uint, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_size_t,
+                      ctypes.POINTER(ctypes.c_ubyte)]
+        lib._declared = True
+    return lib
+
+
+def synth():
+    lib = _load(SYNTH_SO)
+    if not getattr(lib, "_declared", False):
+        for name in ("synth_text", "synth_random", "synth_runs"):
+            f = getattr(lib, name)
+            f.restype = None
+            f.argtypes = [ctypes.c_uint64, ctypes.c_void_p, ctypes.c_size_t]
+        lib.synth_batch.restype = None
+        lib.synth_batch.argtypes = [ctypes.c_int, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_size_t,
+                                    ctypes.c_size_t, ctypes.c_int]
+        lib._declared = True
+    return lib
+
+
+def gen(kind, seed, n):
+    """Synthetic plaintext: kind in {'text', 'random', 'runs'}."""
+    buf = ctypes.create_string_buffer(max(n, 1))
+    getattr(synth(), "synth_" + kind)(seed, buf, n)
+    return buf.raw[:n]
+
+
+# ---------------------------------------------------------------- decode wrappers
+
+def decode(lib, prefix, src, props, dest_cap, finish):
+    """One-call LzmaDecode through `lib` (prefix 'orc' or 'ref').
+
+    Returns (res, status, dest_len, src_len, out_bytes)."""
+    dst = ctypes.create_string_buffer(max(dest_cap, 1))
+    dl = ctypes.c_size_t(dest_cap)
+    sl = ctypes.c_size_t(len(src))
+    st = ctypes.c_int(-1)
+    res = getattr(lib, prefix + "_lzma_decode")(dst, ctypes.byref(dl), src, ctypes.byref(sl),
+                                                 props, len(props), finish, ctypes.byref(st))
+    return res, st.value, dl.value, sl.value, dst.raw[:dl.value]
+
+
+def stream_decode(lib, prefix, src, props, out_total, in_chunk, out_chunk, finish,
+                  max_calls=100000):
+    """zlib-like DecodeToBuf loop. Returns (calls, trace[list of 4-tuples], out, in_used)."""
+    out = ctypes.create_string_buffer(max(out_total, 1))
+    trace = (ctypes.c_longlong * (4 * max_calls))()
+    ol = ctypes.c_size_t(0)
+    iu = ctypes.c_size_t(0)
+    calls = getattr(lib, prefix + "_lzma_stream_decode")(
+        props, src, len(src), out, out_total, in_chunk, out_chunk, finish, trace, max_calls,
+        ctypes.byref(ol), ctypes.byref(iu))
+    tr = [tuple(trace[4 * i:4 * i + 4]) for i in range(max(calls, 0))]
+    return calls, tr, out.raw[:ol.value], iu.value
+
+
+def lzma2_decode(lib, prefix, src, prop, dest_cap, finish):
+    dst = ctypes.create_string_buffer(max(dest_cap, 1))
+    dl = ctypes.c_size_t(dest_cap)
+    sl = ctypes.c_size_t(len(src))
+    st = ctypes.c_int(-1)
+    res = getattr(lib, prefix + "_lzma2_decode")(dst, ctypes.byref(dl), src, ctypes.byref(sl),
+                                                  prop, finish, ctypes.byref(st))
+    return res, st.value, dl.value, sl.value, dst.raw[:dl.value]
+
+
+def ref_encode(data, level=5, dict_size=1 << 16, lc=3, lp=0, pb=2, fb=32, end_mark=False):
+    lib = ref()
+    cap = len(data) + len(data) // 2 + 1024
+    dst = ctypes.create_string_buffer(cap)
+    dl = ctypes.c_size_t(cap)
+    props = ctypes.create_string_buffer(5)
+    res = lib.ref_lzma_encode(dst, ctypes.byref(dl), data, len(data), level, dict_size, lc, lp,
+                              pb, fb, 1 if end_mark else 0, props)
+    assert res == 0, res
+    return props.raw, dst.raw[:dl.value]
+
+
+def ref_encode2(data, level=5, dict_size=1 << 16, lc=3, lp=0, pb=2, block_size=0):
+    lib = ref()
+    cap = len(data) + len(data) // 2 + 4096
+    dst = ctypes.create_string_buffer(cap)
+    dl = ctypes.c_size_t(cap)
+    prop = ctypes.c_ubyte(0)
+    res = lib.ref_lzma2_encode(dst, ctypes.byref(dl), data, len(data), level, dict_size, lc, lp,
+                               pb, block_size, ctypes.byref(prop))
+    assert res == 0, res
+    return prop.value, dst.raw[:dl.value]
