@@ -1,0 +1,245 @@
+/*
+ * lzma_gpu.h -- C ABI of liblzmagpu.so, the MI355X (gfx950) LZMA decoder.
+ *
+ * Two surfaces:
+ *
+ *  1. Drop-in symbols of the reference decoder (LZMA SDK 9.20, the
+ *     yurket/lzma-sdk-zlibLike fork).  Same names, argument meaning, enum
+ *     values, struct layouts and SRes codes, so a caller linking the
+ *     reference's LzmaDec.o / LzmaLib.o / Lzma2Dec.o can link this library
+ *     instead.  Decoding runs on the GPU; only property parsing and
+ *     allocation bookkeeping stay on the host.
+ *
+ *       LzmaProps_Decode        replaces LzmaDec.h:40  / LzmaDec.c:898-922
+ *       LzmaDec_AllocateProbs   replaces LzmaDec.h:134 / LzmaDec.c:938-948
+ *       LzmaDec_FreeProbs       replaces LzmaDec.h:135 / LzmaDec.c:880-884
+ *       LzmaDec_Allocate        replaces LzmaDec.h:137 / LzmaDec.c:950-970
+ *       LzmaDec_Free            replaces LzmaDec.h:138 / LzmaDec.c:892-896
+ *       LzmaDec_Init            replaces LzmaDec.h:73  / LzmaDec.c:701-705
+ *       LzmaDec_DecodeToDic     replaces LzmaDec.h:181-182 / LzmaDec.c:719-838
+ *       LzmaDec_DecodeToBuf     replaces LzmaDec.h:198-199 / LzmaDec.c:840-878
+ *       LzmaDecode              replaces LzmaDec.h:223-225 / LzmaDec.c:972-1002
+ *       LzmaUncompress          replaces LzmaLib.h:128-129 / LzmaLib.c:41-46
+ *       Lzma2Dec_AllocateProbs  replaces Lzma2Dec.h:31 / Lzma2Dec.c:73-78
+ *       Lzma2Dec_Allocate       replaces Lzma2Dec.h:32 / Lzma2Dec.c:80-85
+ *       Lzma2Dec_Init           replaces Lzma2Dec.h:33 / Lzma2Dec.c:87-94
+ *       Lzma2Dec_DecodeToDic    replaces Lzma2Dec.h:50-51 / Lzma2Dec.c:170-289
+ *       Lzma2Dec_DecodeToBuf    replaces Lzma2Dec.h:53-54 / Lzma2Dec.c:291-328
+ *       Lzma2Decode             replaces Lzma2Dec.h:76-77 / Lzma2Dec.c:330-356
+ *
+ *     Documented differences: no stdout print in LzmaDec_AllocateProbs (the
+ *     fork's LzmaDec.c:945 debug printf); Lzma2Decode initialises its state
+ *     (the reference one-call omits Lzma2Dec_Init, which is undefined
+ *     behaviour); a dicLimit beyond dicBufSize returns SZ_ERROR_PARAM instead
+ *     of writing out of bounds; without a usable HIP device every decode entry
+ *     returns SZ_ERROR_FAIL and LzmaGpu_LastError() says why (there is no CPU
+ *     fallback).
+ *
+ *  2. The batch extension (new): many independent streams per launch, all
+ *     buffers caller-owned device memory, no allocation inside the call.
+ */
+#ifndef LZMA_GPU_H
+#define LZMA_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---------------------------------------------------------------- base ABI (Types.h:25-97,227-234) */
+
+#ifndef SZ_OK
+#define SZ_OK 0
+#define SZ_ERROR_DATA 1
+#define SZ_ERROR_MEM 2
+#define SZ_ERROR_CRC 3
+#define SZ_ERROR_UNSUPPORTED 4
+#define SZ_ERROR_PARAM 5
+#define SZ_ERROR_INPUT_EOF 6
+#define SZ_ERROR_OUTPUT_EOF 7
+#define SZ_ERROR_READ 8
+#define SZ_ERROR_WRITE 9
+#define SZ_ERROR_PROGRESS 10
+#define SZ_ERROR_FAIL 11
+#define SZ_ERROR_THREAD 12
+#define SZ_ERROR_ARCHIVE 16
+#define SZ_ERROR_NO_ARCHIVE 17
+#endif
+
+#ifndef __7Z_TYPES_H
+typedef int SRes;
+typedef unsigned char Byte;
+typedef unsigned short UInt16;
+typedef unsigned int UInt32;
+typedef size_t SizeT;
+typedef int Bool;
+typedef struct {
+  void *(*Alloc)(void *p, size_t size);
+  void (*Free)(void *p, void *address);
+} ISzAlloc;
+#endif
+
+#define LZMA_PROPS_SIZE 5
+#define LZMA_REQUIRED_INPUT_MAX 20
+
+typedef UInt16 CLzmaProb; /* 16-bit probabilities (_LZMA_PROB32 not defined) */
+
+typedef struct _CLzmaProps {
+  unsigned lc, lp, pb;
+  UInt32 dicSize;
+} CLzmaProps;
+
+/* Field order and types are the public layout of LzmaDec.h:50-69: callers of
+ * the dictionary interface read dic/dicPos/dicBufSize directly. */
+typedef struct {
+  CLzmaProps prop;
+  CLzmaProb *probs;
+  Byte *dic;
+  const Byte *buf;
+  UInt32 range, code;
+  SizeT dicPos;
+  SizeT dicBufSize;
+  UInt32 processedPos;
+  UInt32 checkDicSize;
+  unsigned state;
+  UInt32 reps[4];
+  unsigned remainLen;
+  int needFlush;
+  int needInitState;
+  UInt32 numProbs;
+  unsigned tempBufSize;
+  Byte tempBuf[LZMA_REQUIRED_INPUT_MAX];
+} CLzmaDec;
+
+#define LzmaDec_Construct(p) { (p)->dic = 0; (p)->probs = 0; }
+
+typedef enum { LZMA_FINISH_ANY, LZMA_FINISH_END } ELzmaFinishMode;
+
+typedef enum {
+  LZMA_STATUS_NOT_SPECIFIED,
+  LZMA_STATUS_FINISHED_WITH_MARK,
+  LZMA_STATUS_NOT_FINISHED,
+  LZMA_STATUS_NEEDS_MORE_INPUT,
+  LZMA_STATUS_MAYBE_FINISHED_WITHOUT_MARK
+} ELzmaStatus;
+
+/* ---------------------------------------------------------------- drop-in LzmaDec.h */
+
+SRes LzmaProps_Decode(CLzmaProps *p, const Byte *data, unsigned size);
+SRes LzmaDec_AllocateProbs(CLzmaDec *p, const Byte *props, unsigned propsSize, ISzAlloc *alloc);
+void LzmaDec_FreeProbs(CLzmaDec *p, ISzAlloc *alloc);
+SRes LzmaDec_Allocate(CLzmaDec *state, const Byte *prop, unsigned propsSize, ISzAlloc *alloc);
+void LzmaDec_Free(CLzmaDec *state, ISzAlloc *alloc);
+void LzmaDec_Init(CLzmaDec *p);
+void LzmaDec_InitDicAndState(CLzmaDec *p, Bool initDic, Bool initState);
+SRes LzmaDec_DecodeToDic(CLzmaDec *p, SizeT dicLimit, const Byte *src, SizeT *srcLen,
+                         ELzmaFinishMode finishMode, ELzmaStatus *status);
+SRes LzmaDec_DecodeToBuf(CLzmaDec *p, Byte *dest, SizeT *destLen, const Byte *src,
+                         SizeT *srcLen, ELzmaFinishMode finishMode, ELzmaStatus *status);
+SRes LzmaDecode(Byte *dest, SizeT *destLen, const Byte *src, SizeT *srcLen,
+                const Byte *propData, unsigned propSize, ELzmaFinishMode finishMode,
+                ELzmaStatus *status, ISzAlloc *alloc);
+
+/* ---------------------------------------------------------------- drop-in LzmaLib.h */
+
+int LzmaUncompress(unsigned char *dest, size_t *destLen, const unsigned char *src,
+                   SizeT *srcLen, const unsigned char *props, size_t propsSize);
+
+/* ---------------------------------------------------------------- drop-in Lzma2Dec.h */
+
+typedef struct {
+  CLzmaDec decoder;
+  UInt32 packSize;
+  UInt32 unpackSize;
+  int state;
+  Byte control;
+  Bool needInitDic;
+  Bool needInitState;
+  Bool needInitProp;
+} CLzma2Dec;
+
+#define Lzma2Dec_Construct(p) LzmaDec_Construct(&(p)->decoder)
+#define Lzma2Dec_FreeProbs(p, alloc) LzmaDec_FreeProbs(&(p)->decoder, alloc);
+#define Lzma2Dec_Free(p, alloc) LzmaDec_Free(&(p)->decoder, alloc);
+
+SRes Lzma2Dec_AllocateProbs(CLzma2Dec *p, Byte prop, ISzAlloc *alloc);
+SRes Lzma2Dec_Allocate(CLzma2Dec *p, Byte prop, ISzAlloc *alloc);
+void Lzma2Dec_Init(CLzma2Dec *p);
+SRes Lzma2Dec_DecodeToDic(CLzma2Dec *p, SizeT dicLimit, const Byte *src, SizeT *srcLen,
+                          ELzmaFinishMode finishMode, ELzmaStatus *status);
+SRes Lzma2Dec_DecodeToBuf(CLzma2Dec *p, Byte *dest, SizeT *destLen, const Byte *src,
+                          SizeT *srcLen, ELzmaFinishMode finishMode, ELzmaStatus *status);
+SRes Lzma2Decode(Byte *dest, SizeT *destLen, const Byte *src, SizeT *srcLen, Byte prop,
+                 ELzmaFinishMode finishMode, ELzmaStatus *status, ISzAlloc *alloc);
+
+/* ---------------------------------------------------------------- batch extension */
+
+#define LZMA_GPU_KIND_LZMA 0  /* .lzma-style stream: props[0..5) = 5-byte header */
+#define LZMA_GPU_KIND_LZMA2 1 /* LZMA2 byte range: props[0] = dictionary prop byte */
+#define LZMA_GPU_NO_WORKSPACE (~(uint64_t)0)
+
+/* One stream of a batch (48 bytes).  Offsets index the caller's packed
+ * device buffers. probs_off is filled by LzmaGpu_PlanBatch. */
+typedef struct LzmaGpuStreamDesc {
+  uint64_t src_off;   /* compressed bytes start in d_src */
+  uint64_t src_len;   /* compressed bytes available (*srcLen in) */
+  uint64_t dst_off;   /* output window start in d_dst (window == dictionary) */
+  uint64_t dst_cap;   /* output capacity (*destLen in) */
+  uint64_t probs_off; /* in CLzmaProb cells, into the workspace */
+  uint8_t props[5];
+  uint8_t props_size;  /* propSize argument of LzmaDecode, normally 5 */
+  uint8_t finish_mode; /* ELzmaFinishMode */
+  uint8_t kind;        /* LZMA_GPU_KIND_* */
+} LzmaGpuStreamDesc;
+
+/* Per-stream outcome (24 bytes): exactly LzmaDecode's return value, *status
+ * (-1 where LzmaDecode leaves it untouched), *destLen and *srcLen. */
+typedef struct LzmaGpuResult {
+  int32_t res;
+  int32_t status;
+  uint64_t dest_len;
+  uint64_t src_len;
+} LzmaGpuResult;
+
+/* Host-side planner.  Fills descs[i].probs_off (16-byte aligned slices) and,
+ * if order != NULL, a lane->stream permutation that groups streams of equal
+ * table width and similar length into the same wavefront.  Returns the
+ * workspace size in bytes (0 for n == 0). */
+size_t LzmaGpu_PlanBatch(LzmaGpuStreamDesc *descs, size_t n, uint32_t *order);
+
+/* Decode n streams on the current HIP device.  All pointers are device
+ * memory owned by the caller; d_order may be NULL (identity).  Asynchronous
+ * on `stream` (a hipStream_t; NULL = default stream).  Returns SZ_OK if the
+ * launch was queued; per-stream outcomes land in d_results. */
+SRes LzmaGpu_DecodeBatch(const LzmaGpuStreamDesc *d_descs, const uint32_t *d_order, size_t n,
+                         const Byte *d_src, Byte *d_dst, void *d_workspace,
+                         size_t workspace_bytes, LzmaGpuResult *d_results, void *stream);
+
+/* Convenience: the same over host buffers (allocates, copies, decodes,
+ * copies back, frees).  descs need not be planned. */
+SRes LzmaGpu_DecodeBatchHost(const LzmaGpuStreamDesc *descs, size_t n, const Byte *src,
+                             size_t src_bytes, Byte *dst, size_t dst_bytes,
+                             LzmaGpuResult *results);
+
+/* Split an LZMA2 stream into its independently decodable blocks: a block
+ * starts at every chunk that resets the dictionary (control 0x01 or
+ * >= 0xE0, Lzma2Dec.c:14-26) and runs to the next one.  Walks chunk headers
+ * only (O(#chunks)).  For block i: src_off/src_len = its byte range
+ * (the final EOS byte belongs to no block), unpack = its decoded size.
+ * Returns the number of blocks (may exceed max_blocks: then only the first
+ * max_blocks are written) or (size_t)-1 on a malformed header sequence. */
+size_t Lzma2Gpu_SplitBlocks(const Byte *src, size_t src_len, uint64_t *src_off,
+                            uint64_t *block_src_len, uint64_t *unpack, size_t max_blocks);
+
+/* Device / diagnostics. */
+int LzmaGpu_DeviceCount(void);
+const char *LzmaGpu_LastError(void);
+const char *LzmaGpu_Version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* LZMA_GPU_H */

@@ -1,0 +1,774 @@
+// lzma_capi.hip -- host side of liblzmagpu.so: the drop-in LzmaDec / LzmaLib /
+// Lzma2Dec symbols and the batch extension (include/lzma_gpu.h).
+//
+// Every decode runs on the GPU.  What stays on the host is what the reference
+// keeps outside its decoder loop: property parsing (LzmaDec.c:898-922),
+// ISzAlloc bookkeeping (LzmaDec.c:880-970), the DecodeToBuf ring-to-caller
+// copy loop (LzmaDec.c:840-878) and the LZMA2 chunk-header walk of the
+// streaming interface (Lzma2Dec.c:170-328), whose LZMA chunks are decoded by
+// the GPU LzmaDec_DecodeToDic.  Without a HIP device every decode entry
+// returns SZ_ERROR_FAIL (no CPU fallback).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <numeric>
+#include <string>
+#include <vector>
+
+#include "lzma_device.h"
+#include "lzma_gpu_internal.h"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+void set_error(const std::string& s) { g_last_error = s; }
+
+bool hip_ok(hipError_t e, const char* what) {
+  if (e == hipSuccess) return true;
+  set_error(std::string(what) + ": " + hipGetErrorString(e));
+  return false;
+}
+
+int device_count() {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+bool ensure_device() {
+  static int count = -1;
+  if (count < 0) count = device_count();
+  if (count <= 0) {
+    set_error("liblzmagpu: no HIP device available (GPU decoder only, no CPU fallback)");
+    static bool warned = false;
+    if (!warned) {
+      warned = true;
+      fprintf(stderr, "liblzmagpu: no HIP device available -- decode calls return SZ_ERROR_FAIL\n");
+    }
+    return false;
+  }
+  return true;
+}
+
+// Grow-only device buffer, one set per host thread (the reference API is
+// re-entrant per decoder object; these buffers are per-call scratch).
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  int dev = -1;
+  void* get(size_t n) {
+    int d = 0;
+    (void)hipGetDevice(&d);
+    if (n == 0) n = 16;
+    if (p && cap >= n && dev == d) return p;
+    size_t want = std::max(n, cap * 2);
+    if (p && dev == d) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    if (hipMalloc(&p, want) != hipSuccess) {
+      p = nullptr;
+      if (hipMalloc(&p, n) != hipSuccess) { p = nullptr; return nullptr; }
+      want = n;
+    }
+    cap = want;
+    dev = d;
+    return p;
+  }
+};
+
+struct Scratch {
+  DevBuf probs, dic, src, sess, desc, res, dst;
+};
+
+Scratch& scratch() {
+  static thread_local Scratch* s = new Scratch();  // intentionally leaked at exit
+  return *s;
+}
+
+uint32_t probs_for(uint32_t lc, uint32_t lp) { return lzgpu::num_probs(lc, lp); }
+
+// Run one DecodeToDic on the GPU over a host-resident CLzmaDec.
+SRes gpu_decode_to_dic(CLzmaDec* p, SizeT dicLimit, const Byte* src, SizeT* srcLen,
+                       ELzmaFinishMode finishMode, ELzmaStatus* status) {
+  const SizeT in_size = *srcLen;
+  *srcLen = 0;
+  *status = LZMA_STATUS_NOT_SPECIFIED;
+  if (!ensure_device()) return SZ_ERROR_FAIL;
+  if (dicLimit > p->dicBufSize || (p->dic == nullptr && p->dicBufSize != 0)) {
+    set_error("LzmaDec_DecodeToDic: dicLimit beyond dicBufSize");
+    return SZ_ERROR_PARAM;
+  }
+  Scratch& sc = scratch();
+  const uint32_t nprobs = probs_for(p->prop.lc, p->prop.lp);
+  void* d_probs = sc.probs.get(size_t(nprobs) * 2);
+  void* d_dic = sc.dic.get(p->dicBufSize);
+  void* d_src = sc.src.get(in_size);
+  LzgpuSession* d_sess = static_cast<LzgpuSession*>(sc.sess.get(sizeof(LzgpuSession)));
+  if (!d_probs || !d_dic || !d_src || !d_sess) {
+    set_error("LzmaDec_DecodeToDic: device allocation failed");
+    return SZ_ERROR_MEM;
+  }
+  if (p->probs && !hip_ok(hipMemcpy(d_probs, p->probs, size_t(nprobs) * 2, hipMemcpyHostToDevice),
+                          "upload probs"))
+    return SZ_ERROR_FAIL;
+  if (p->dicBufSize &&
+      !hip_ok(hipMemcpy(d_dic, p->dic, p->dicBufSize, hipMemcpyHostToDevice), "upload dic"))
+    return SZ_ERROR_FAIL;
+  if (in_size && !hip_ok(hipMemcpy(d_src, src, in_size, hipMemcpyHostToDevice), "upload src"))
+    return SZ_ERROR_FAIL;
+
+  LzgpuSession q;
+  memset(&q, 0, sizeof q);
+  q.lc = p->prop.lc;
+  q.lp = p->prop.lp;
+  q.pb = p->prop.pb;
+  q.dict_size = p->prop.dicSize;
+  q.probs = static_cast<uint16_t*>(d_probs);
+  q.dic = static_cast<uint8_t*>(d_dic);
+  q.in = static_cast<const uint8_t*>(d_src);
+  q.cap = p->dicBufSize;
+  q.pos = p->dicPos;
+  q.dic_limit = dicLimit;
+  q.in_len = in_size;
+  q.range = p->range;
+  q.code = p->code;
+  q.total = p->processedPos;
+  q.full = p->checkDicSize;
+  q.st = p->state;
+  for (int i = 0; i < 4; ++i) q.rep[i] = p->reps[i];
+  q.pending = p->remainLen;
+  q.need_rc_init = p->needFlush ? 1 : 0;
+  q.need_state_init = p->needInitState ? 1 : 0;
+  q.tmp_n = p->tempBufSize;
+  memcpy(q.tmp, p->tempBuf, LZMA_REQUIRED_INPUT_MAX);
+  q.finish_mode = finishMode;
+  const SizeT pos0 = p->dicPos;
+
+  if (!hip_ok(hipMemcpy(d_sess, &q, sizeof q, hipMemcpyHostToDevice), "upload session"))
+    return SZ_ERROR_FAIL;
+  if (lzgpu_launch_session(d_sess, 1, nullptr) != 0) {
+    set_error("session kernel launch failed");
+    return SZ_ERROR_FAIL;
+  }
+  if (!hip_ok(hipMemcpy(&q, d_sess, sizeof q, hipMemcpyDeviceToHost), "download session"))
+    return SZ_ERROR_FAIL;
+  if (p->probs &&
+      !hip_ok(hipMemcpy(p->probs, d_probs, size_t(nprobs) * 2, hipMemcpyDeviceToHost),
+              "download probs"))
+    return SZ_ERROR_FAIL;
+  if (q.pos > pos0 &&
+      !hip_ok(hipMemcpy(p->dic + pos0, static_cast<uint8_t*>(d_dic) + pos0, q.pos - pos0,
+                        hipMemcpyDeviceToHost),
+              "download dic"))
+    return SZ_ERROR_FAIL;
+
+  p->dicPos = q.pos;
+  p->range = q.range;
+  p->code = q.code;
+  p->processedPos = q.total;
+  p->checkDicSize = q.full;
+  p->state = q.st;
+  for (int i = 0; i < 4; ++i) p->reps[i] = q.rep[i];
+  p->remainLen = q.pending;
+  p->needFlush = int(q.need_rc_init);
+  p->needInitState = int(q.need_state_init);
+  p->tempBufSize = q.tmp_n;
+  memcpy(p->tempBuf, q.tmp, LZMA_REQUIRED_INPUT_MAX);
+  p->buf = src + q.in_used;
+  *srcLen = q.in_used;
+  *status = ELzmaStatus(q.status);
+  return q.res;
+}
+
+// LzmaDecode-style one-call over host buffers, as a 1-stream GPU batch.
+SRes gpu_one_call(uint8_t kind, Byte* dest, SizeT* destLen, const Byte* src, SizeT* srcLen,
+                  const Byte* props, unsigned propSize, ELzmaFinishMode finishMode,
+                  int* status_out) {
+  const SizeT in_size = *srcLen, out_size = *destLen;
+  *srcLen = 0;
+  *destLen = 0;
+  if (!ensure_device()) return SZ_ERROR_FAIL;
+  LzmaGpuStreamDesc d;
+  memset(&d, 0, sizeof d);
+  d.src_len = in_size;
+  d.dst_cap = out_size;
+  memcpy(d.props, props, std::min<unsigned>(propSize, 5));
+  d.props_size = uint8_t(std::min<unsigned>(propSize, 255));
+  d.finish_mode = uint8_t(finishMode);
+  d.kind = kind;
+  size_t ws = LzmaGpu_PlanBatch(&d, 1, nullptr);
+  Scratch& sc = scratch();
+  void* d_src = sc.src.get(in_size);
+  void* d_dst = sc.dst.get(out_size);
+  void* d_ws = sc.probs.get(ws);
+  void* d_desc = sc.desc.get(sizeof d);
+  void* d_res = sc.res.get(sizeof(LzmaGpuResult));
+  if (!d_src || !d_dst || !d_ws || !d_desc || !d_res) {
+    set_error("device allocation failed");
+    return SZ_ERROR_MEM;
+  }
+  if (in_size && !hip_ok(hipMemcpy(d_src, src, in_size, hipMemcpyHostToDevice), "upload src"))
+    return SZ_ERROR_FAIL;
+  if (!hip_ok(hipMemcpy(d_desc, &d, sizeof d, hipMemcpyHostToDevice), "upload desc"))
+    return SZ_ERROR_FAIL;
+  if (lzgpu_launch_decode_batch(static_cast<LzmaGpuStreamDesc*>(d_desc), nullptr, 1,
+                                static_cast<uint8_t*>(d_src), static_cast<uint8_t*>(d_dst),
+                                static_cast<uint16_t*>(d_ws), static_cast<LzmaGpuResult*>(d_res),
+                                nullptr) != 0) {
+    set_error("decode kernel launch failed");
+    return SZ_ERROR_FAIL;
+  }
+  LzmaGpuResult r;
+  if (!hip_ok(hipMemcpy(&r, d_res, sizeof r, hipMemcpyDeviceToHost), "download result"))
+    return SZ_ERROR_FAIL;
+  if (r.dest_len &&
+      !hip_ok(hipMemcpy(dest, d_dst, r.dest_len, hipMemcpyDeviceToHost), "download output"))
+    return SZ_ERROR_FAIL;
+  *destLen = r.dest_len;
+  *srcLen = r.src_len;
+  *status_out = r.status;
+  return r.res;
+}
+
+}  // namespace
+
+extern "C" {
+
+// ------------------------------------------------------------------ props + allocation
+
+SRes LzmaProps_Decode(CLzmaProps* p, const Byte* data, unsigned size) {
+  uint32_t lc, lp, pb, dict;
+  if (size < LZMA_PROPS_SIZE) return SZ_ERROR_UNSUPPORTED;
+  int r = lzgpu::lz_props_parse(data, size, lc, lp, pb, dict);
+  // the reference stores dicSize before rejecting a bad lc/lp/pb byte
+  p->dicSize = dict;
+  if (r != SZ_OK) return r;
+  p->lc = lc;
+  p->lp = lp;
+  p->pb = pb;
+  return SZ_OK;
+}
+
+void LzmaDec_FreeProbs(CLzmaDec* p, ISzAlloc* alloc) {
+  alloc->Free(alloc, p->probs);
+  p->probs = nullptr;
+}
+
+static void free_dict(CLzmaDec* p, ISzAlloc* alloc) {
+  alloc->Free(alloc, p->dic);
+  p->dic = nullptr;
+}
+
+void LzmaDec_Free(CLzmaDec* p, ISzAlloc* alloc) {
+  LzmaDec_FreeProbs(p, alloc);
+  free_dict(p, alloc);
+}
+
+static SRes alloc_probs(CLzmaDec* p, const CLzmaProps* np, ISzAlloc* alloc) {
+  const uint32_t n = probs_for(np->lc, np->lp);
+  if (p->probs == nullptr || n != p->numProbs) {
+    LzmaDec_FreeProbs(p, alloc);
+    p->probs = static_cast<CLzmaProb*>(alloc->Alloc(alloc, size_t(n) * sizeof(CLzmaProb)));
+    p->numProbs = n;
+    if (p->probs == nullptr) return SZ_ERROR_MEM;
+  }
+  return SZ_OK;
+}
+
+SRes LzmaDec_AllocateProbs(CLzmaDec* p, const Byte* props, unsigned propsSize, ISzAlloc* alloc) {
+  CLzmaProps np;
+  SRes r = LzmaProps_Decode(&np, props, propsSize);
+  if (r != SZ_OK) return r;
+  r = alloc_probs(p, &np, alloc);
+  if (r != SZ_OK) return r;
+  p->prop = np;
+  return SZ_OK;
+}
+
+SRes LzmaDec_Allocate(CLzmaDec* p, const Byte* props, unsigned propsSize, ISzAlloc* alloc) {
+  CLzmaProps np;
+  SRes r = LzmaProps_Decode(&np, props, propsSize);
+  if (r != SZ_OK) return r;
+  r = alloc_probs(p, &np, alloc);
+  if (r != SZ_OK) return r;
+  const SizeT dsz = np.dicSize;
+  if (p->dic == nullptr || dsz != p->dicBufSize) {
+    free_dict(p, alloc);
+    p->dic = static_cast<Byte*>(alloc->Alloc(alloc, dsz));
+    if (p->dic == nullptr) {
+      LzmaDec_FreeProbs(p, alloc);
+      return SZ_ERROR_MEM;
+    }
+  }
+  p->dicBufSize = dsz;
+  p->prop = np;
+  return SZ_OK;
+}
+
+void LzmaDec_InitDicAndState(CLzmaDec* p, Bool initDic, Bool initState) {
+  p->needFlush = 1;
+  p->remainLen = 0;
+  p->tempBufSize = 0;
+  if (initDic) {
+    p->processedPos = 0;
+    p->checkDicSize = 0;
+    p->needInitState = 1;
+  }
+  if (initState) p->needInitState = 1;
+}
+
+void LzmaDec_Init(CLzmaDec* p) {
+  p->dicPos = 0;
+  LzmaDec_InitDicAndState(p, 1, 1);
+}
+
+// ------------------------------------------------------------------ decode entry points
+
+SRes LzmaDec_DecodeToDic(CLzmaDec* p, SizeT dicLimit, const Byte* src, SizeT* srcLen,
+                         ELzmaFinishMode finishMode, ELzmaStatus* status) {
+  return gpu_decode_to_dic(p, dicLimit, src, srcLen, finishMode, status);
+}
+
+SRes LzmaDec_DecodeToBuf(CLzmaDec* p, Byte* dest, SizeT* destLen, const Byte* src, SizeT* srcLen,
+                         ELzmaFinishMode finishMode, ELzmaStatus* status) {
+  SizeT out_left = *destLen, in_left = *srcLen;
+  *srcLen = 0;
+  *destLen = 0;
+  for (;;) {
+    SizeT in_cur = in_left, lim, start;
+    ELzmaFinishMode fin_cur;
+    if (p->dicPos == p->dicBufSize) p->dicPos = 0;
+    start = p->dicPos;
+    if (out_left > p->dicBufSize - start) {
+      lim = p->dicBufSize;
+      fin_cur = LZMA_FINISH_ANY;
+    } else {
+      lim = start + out_left;
+      fin_cur = finishMode;
+    }
+    SRes r = LzmaDec_DecodeToDic(p, lim, src, &in_cur, fin_cur, status);
+    src += in_cur;
+    in_left -= in_cur;
+    *srcLen += in_cur;
+    const SizeT produced = p->dicPos - start;
+    memcpy(dest, p->dic + start, produced);
+    dest += produced;
+    out_left -= produced;
+    *destLen += produced;
+    if (r != SZ_OK) return r;
+    if (produced == 0 || out_left == 0) return SZ_OK;
+  }
+}
+
+SRes LzmaDecode(Byte* dest, SizeT* destLen, const Byte* src, SizeT* srcLen, const Byte* propData,
+                unsigned propSize, ELzmaFinishMode finishMode, ELzmaStatus* status,
+                ISzAlloc* alloc) {
+  const SizeT in_size = *srcLen;
+  *srcLen = 0;
+  *destLen = 0;
+  if (in_size < 5) return SZ_ERROR_INPUT_EOF;
+  CLzmaProps np;
+  SRes r = LzmaProps_Decode(&np, propData, propSize);
+  if (r != SZ_OK) return r;
+  // honour the caller's allocator contract: the reference allocates the
+  // probability table through it and reports SZ_ERROR_MEM when that fails
+  void* host_probs = alloc->Alloc(alloc, size_t(probs_for(np.lc, np.lp)) * sizeof(CLzmaProb));
+  if (host_probs == nullptr) return SZ_ERROR_MEM;
+  SizeT sl = in_size;
+  int st = -1;
+  r = gpu_one_call(LZMA_GPU_KIND_LZMA, dest, destLen, src, &sl, propData, propSize, finishMode,
+                   &st);
+  alloc->Free(alloc, host_probs);
+  *srcLen = sl;
+  if (st >= 0) *status = ELzmaStatus(st);
+  return r;
+}
+
+static void* lib_alloc(void*, size_t n) { return malloc(n ? n : 1); }
+static void lib_free(void*, void* a) { free(a); }
+static ISzAlloc g_lib_alloc = {lib_alloc, lib_free};
+
+int LzmaUncompress(unsigned char* dest, size_t* destLen, const unsigned char* src, SizeT* srcLen,
+                   const unsigned char* props, size_t propsSize) {
+  ELzmaStatus status;
+  return LzmaDecode(dest, destLen, src, srcLen, props, unsigned(propsSize), LZMA_FINISH_ANY,
+                    &status, &g_lib_alloc);
+}
+
+// ------------------------------------------------------------------ LZMA2
+
+enum {
+  S2_CONTROL, S2_UNPACK0, S2_UNPACK1, S2_PACK0, S2_PACK1, S2_PROP, S2_DATA, S2_DATA_CONT,
+  S2_FINISHED, S2_ERROR
+};
+
+static SRes lzma2_props(Byte prop, Byte* props) {
+  if (prop > 40) return SZ_ERROR_UNSUPPORTED;
+  const UInt32 dict = (prop == 40) ? 0xFFFFFFFFu : ((2u | (prop & 1u)) << (prop / 2 + 11));
+  props[0] = 4;  // lc+lp budget of LZMA2 (Lzma2Dec.c:36,67)
+  props[1] = Byte(dict);
+  props[2] = Byte(dict >> 8);
+  props[3] = Byte(dict >> 16);
+  props[4] = Byte(dict >> 24);
+  return SZ_OK;
+}
+
+SRes Lzma2Dec_AllocateProbs(CLzma2Dec* p, Byte prop, ISzAlloc* alloc) {
+  Byte props[LZMA_PROPS_SIZE];
+  SRes r = lzma2_props(prop, props);
+  if (r != SZ_OK) return r;
+  return LzmaDec_AllocateProbs(&p->decoder, props, LZMA_PROPS_SIZE, alloc);
+}
+
+SRes Lzma2Dec_Allocate(CLzma2Dec* p, Byte prop, ISzAlloc* alloc) {
+  Byte props[LZMA_PROPS_SIZE];
+  SRes r = lzma2_props(prop, props);
+  if (r != SZ_OK) return r;
+  return LzmaDec_Allocate(&p->decoder, props, LZMA_PROPS_SIZE, alloc);
+}
+
+void Lzma2Dec_Init(CLzma2Dec* p) {
+  p->state = S2_CONTROL;
+  p->needInitDic = 1;
+  p->needInitState = 1;
+  p->needInitProp = 1;
+  LzmaDec_Init(&p->decoder);
+}
+
+static int lzma2_header(CLzma2Dec* p, Byte b) {
+  const bool copy = (p->control & 0x80) == 0;
+  switch (p->state) {
+    case S2_CONTROL:
+      p->control = b;
+      if (b == 0) return S2_FINISHED;
+      if ((b & 0x80) == 0) {
+        if ((b & 0x7F) > 2) return S2_ERROR;
+        p->unpackSize = 0;
+      } else {
+        p->unpackSize = UInt32(b & 0x1F) << 16;
+      }
+      return S2_UNPACK0;
+    case S2_UNPACK0:
+      p->unpackSize |= UInt32(b) << 8;
+      return S2_UNPACK1;
+    case S2_UNPACK1:
+      p->unpackSize |= b;
+      p->unpackSize++;
+      return copy ? S2_DATA : S2_PACK0;
+    case S2_PACK0:
+      p->packSize = UInt32(b) << 8;
+      return S2_PACK1;
+    case S2_PACK1:
+      p->packSize |= b;
+      p->packSize++;
+      if (((p->control >> 5) & 3) >= 2) return S2_PROP;
+      return p->needInitProp ? S2_ERROR : S2_DATA;
+    case S2_PROP: {
+      if (b >= 225) return S2_ERROR;
+      unsigned lc = b % 9;
+      b /= 9;
+      unsigned pb = b / 5, lp = b % 5;
+      if (lc + lp > 4) return S2_ERROR;
+      p->decoder.prop.lc = lc;
+      p->decoder.prop.lp = lp;
+      p->decoder.prop.pb = pb;
+      p->needInitProp = 0;
+      return S2_DATA;
+    }
+  }
+  return S2_ERROR;
+}
+
+SRes Lzma2Dec_DecodeToDic(CLzma2Dec* p, SizeT dicLimit, const Byte* src, SizeT* srcLen,
+                          ELzmaFinishMode finishMode, ELzmaStatus* status) {
+  const SizeT in_size = *srcLen;
+  *srcLen = 0;
+  *status = LZMA_STATUS_NOT_SPECIFIED;
+  if (!ensure_device()) return SZ_ERROR_FAIL;
+  while (p->state != S2_FINISHED) {
+    const SizeT pos0 = p->decoder.dicPos;
+    if (p->state == S2_ERROR) return SZ_ERROR_DATA;
+    if (pos0 == dicLimit && finishMode == LZMA_FINISH_ANY) {
+      *status = LZMA_STATUS_NOT_FINISHED;
+      return SZ_OK;
+    }
+    if (p->state != S2_DATA && p->state != S2_DATA_CONT) {
+      if (*srcLen == in_size) {
+        *status = LZMA_STATUS_NEEDS_MORE_INPUT;
+        return SZ_OK;
+      }
+      (*srcLen)++;
+      p->state = lzma2_header(p, *src++);
+      continue;
+    }
+    SizeT out_cur = dicLimit - pos0, in_cur = in_size - *srcLen;
+    ELzmaFinishMode fin_cur = LZMA_FINISH_ANY;
+    if (p->unpackSize <= out_cur) {
+      out_cur = p->unpackSize;
+      fin_cur = LZMA_FINISH_END;
+    }
+    if ((p->control & 0x80) == 0) {
+      if (*srcLen == in_size) {
+        *status = LZMA_STATUS_NEEDS_MORE_INPUT;
+        return SZ_OK;
+      }
+      if (p->state == S2_DATA) {
+        const bool reset = (p->control == 1);
+        if (reset)
+          p->needInitProp = p->needInitState = 1;
+        else if (p->needInitDic)
+          return SZ_ERROR_DATA;
+        p->needInitDic = 0;
+        LzmaDec_InitDicAndState(&p->decoder, reset, 0);
+      }
+      if (in_cur > out_cur) in_cur = out_cur;
+      if (in_cur == 0) return SZ_ERROR_DATA;
+      // stored chunk: a plain copy into the dictionary (Lzma2Dec.c:159-166)
+      CLzmaDec* d = &p->decoder;
+      memcpy(d->dic + d->dicPos, src, in_cur);
+      d->dicPos += in_cur;
+      if (d->checkDicSize == 0 && d->prop.dicSize - d->processedPos <= in_cur)
+        d->checkDicSize = d->prop.dicSize;
+      d->processedPos += UInt32(in_cur);
+      src += in_cur;
+      *srcLen += in_cur;
+      p->unpackSize -= UInt32(in_cur);
+      p->state = (p->unpackSize == 0) ? S2_CONTROL : S2_DATA_CONT;
+    } else {
+      if (p->state == S2_DATA) {
+        const int mode = (p->control >> 5) & 3;
+        const bool init_dic = (mode == 3), init_state = (mode > 0);
+        if ((!init_dic && p->needInitDic) || (!init_state && p->needInitState))
+          return SZ_ERROR_DATA;
+        LzmaDec_InitDicAndState(&p->decoder, init_dic, init_state);
+        p->needInitDic = 0;
+        p->needInitState = 0;
+        p->state = S2_DATA_CONT;
+      }
+      if (in_cur > p->packSize) in_cur = p->packSize;
+      SRes r = LzmaDec_DecodeToDic(&p->decoder, pos0 + out_cur, src, &in_cur, fin_cur, status);
+      src += in_cur;
+      *srcLen += in_cur;
+      p->packSize -= UInt32(in_cur);
+      const SizeT produced = p->decoder.dicPos - pos0;
+      p->unpackSize -= UInt32(produced);
+      if (r != SZ_OK) return r;
+      if (*status == LZMA_STATUS_NEEDS_MORE_INPUT) return r;
+      if (in_cur == 0 && produced == 0) {
+        if (*status != LZMA_STATUS_MAYBE_FINISHED_WITHOUT_MARK || p->unpackSize != 0 ||
+            p->packSize != 0)
+          return SZ_ERROR_DATA;
+        p->state = S2_CONTROL;
+      }
+      if (*status == LZMA_STATUS_MAYBE_FINISHED_WITHOUT_MARK) *status = LZMA_STATUS_NOT_FINISHED;
+    }
+  }
+  *status = LZMA_STATUS_FINISHED_WITH_MARK;
+  return SZ_OK;
+}
+
+SRes Lzma2Dec_DecodeToBuf(CLzma2Dec* p, Byte* dest, SizeT* destLen, const Byte* src,
+                          SizeT* srcLen, ELzmaFinishMode finishMode, ELzmaStatus* status) {
+  SizeT out_left = *destLen, in_left = *srcLen;
+  *srcLen = 0;
+  *destLen = 0;
+  for (;;) {
+    SizeT in_cur = in_left, lim, start;
+    ELzmaFinishMode fin_cur;
+    CLzmaDec* d = &p->decoder;
+    if (d->dicPos == d->dicBufSize) d->dicPos = 0;
+    start = d->dicPos;
+    if (out_left > d->dicBufSize - start) {
+      lim = d->dicBufSize;
+      fin_cur = LZMA_FINISH_ANY;
+    } else {
+      lim = start + out_left;
+      fin_cur = finishMode;
+    }
+    SRes r = Lzma2Dec_DecodeToDic(p, lim, src, &in_cur, fin_cur, status);
+    src += in_cur;
+    in_left -= in_cur;
+    *srcLen += in_cur;
+    const SizeT produced = d->dicPos - start;
+    memcpy(dest, d->dic + start, produced);
+    dest += produced;
+    out_left -= produced;
+    *destLen += produced;
+    if (r != SZ_OK) return r;
+    if (produced == 0 || out_left == 0) return SZ_OK;
+  }
+}
+
+SRes Lzma2Decode(Byte* dest, SizeT* destLen, const Byte* src, SizeT* srcLen, Byte prop,
+                 ELzmaFinishMode finishMode, ELzmaStatus* status, ISzAlloc* alloc) {
+  const SizeT in_size = *srcLen;
+  *destLen = 0;
+  *srcLen = 0;
+  *status = LZMA_STATUS_NOT_SPECIFIED;
+  Byte props[LZMA_PROPS_SIZE];
+  SRes r = lzma2_props(prop, props);
+  if (r != SZ_OK) return r;
+  void* host_probs = alloc->Alloc(alloc, size_t(probs_for(4, 0)) * sizeof(CLzmaProb));
+  if (host_probs == nullptr) return SZ_ERROR_MEM;
+  SizeT sl = in_size;
+  int st = -1;
+  r = gpu_one_call(LZMA_GPU_KIND_LZMA2, dest, destLen, src, &sl, &prop, 1, finishMode, &st);
+  alloc->Free(alloc, host_probs);
+  *srcLen = sl;
+  if (st >= 0) *status = ELzmaStatus(st);
+  return r;
+}
+
+// ------------------------------------------------------------------ batch extension
+
+size_t LzmaGpu_PlanBatch(LzmaGpuStreamDesc* descs, size_t n, uint32_t* order) {
+  uint64_t off = 0;
+  std::vector<uint32_t> width(n);
+  for (size_t i = 0; i < n; ++i) {
+    LzmaGpuStreamDesc& d = descs[i];
+    uint32_t np = 0;
+    if (d.kind == LZMA_GPU_KIND_LZMA2) {
+      np = probs_for(4, 0);
+    } else {
+      uint32_t lc, lp, pb, dict;
+      if (lzgpu::lz_props_parse(d.props, d.props_size, lc, lp, pb, dict) == SZ_OK)
+        np = probs_for(lc, lp);
+    }
+    width[i] = np;
+    d.probs_off = off;
+    off += (uint64_t(np) + 7) & ~uint64_t(7);
+  }
+  if (order) {
+    std::vector<uint32_t> idx(n);
+    std::iota(idx.begin(), idx.end(), 0u);
+    std::stable_sort(idx.begin(), idx.end(), [&](uint32_t a, uint32_t b) {
+      if (descs[a].dst_cap != descs[b].dst_cap) return descs[a].dst_cap > descs[b].dst_cap;
+      return width[a] > width[b];
+    });
+    for (size_t i = 0; i < n; ++i) order[i] = idx[i];
+  }
+  return size_t(off) * 2;
+}
+
+SRes LzmaGpu_DecodeBatch(const LzmaGpuStreamDesc* d_descs, const uint32_t* d_order, size_t n,
+                         const Byte* d_src, Byte* d_dst, void* d_workspace, size_t workspace_bytes,
+                         LzmaGpuResult* d_results, void* stream) {
+  (void)workspace_bytes;
+  if (!ensure_device()) return SZ_ERROR_FAIL;
+  if (n > 0xFFFFFFFFull) return SZ_ERROR_PARAM;
+  if (lzgpu_launch_decode_batch(d_descs, d_order, uint32_t(n), d_src, d_dst,
+                                static_cast<uint16_t*>(d_workspace), d_results,
+                                static_cast<hipStream_t>(stream)) != 0) {
+    set_error("batch kernel launch failed");
+    return SZ_ERROR_FAIL;
+  }
+  return SZ_OK;
+}
+
+SRes LzmaGpu_DecodeBatchHost(const LzmaGpuStreamDesc* descs, size_t n, const Byte* src,
+                             size_t src_bytes, Byte* dst, size_t dst_bytes,
+                             LzmaGpuResult* results) {
+  if (!ensure_device()) return SZ_ERROR_FAIL;
+  if (n == 0) return SZ_OK;
+  std::vector<LzmaGpuStreamDesc> d(descs, descs + n);
+  std::vector<uint32_t> order(n);
+  const size_t ws = LzmaGpu_PlanBatch(d.data(), n, order.data());
+  void *d_src = nullptr, *d_dst = nullptr, *d_ws = nullptr, *d_desc = nullptr, *d_order = nullptr,
+       *d_res = nullptr;
+  SRes r = SZ_ERROR_MEM;
+  do {
+    if (!hip_ok(hipMalloc(&d_src, std::max<size_t>(src_bytes, 16)), "alloc src")) break;
+    if (!hip_ok(hipMalloc(&d_dst, std::max<size_t>(dst_bytes, 16)), "alloc dst")) break;
+    if (!hip_ok(hipMalloc(&d_ws, std::max<size_t>(ws, 16)), "alloc workspace")) break;
+    if (!hip_ok(hipMalloc(&d_desc, n * sizeof(LzmaGpuStreamDesc)), "alloc desc")) break;
+    if (!hip_ok(hipMalloc(&d_order, n * sizeof(uint32_t)), "alloc order")) break;
+    if (!hip_ok(hipMalloc(&d_res, n * sizeof(LzmaGpuResult)), "alloc results")) break;
+    r = SZ_ERROR_FAIL;
+    if (src_bytes && !hip_ok(hipMemcpy(d_src, src, src_bytes, hipMemcpyHostToDevice), "H2D src"))
+      break;
+    if (!hip_ok(hipMemcpy(d_desc, d.data(), n * sizeof(LzmaGpuStreamDesc), hipMemcpyHostToDevice),
+                "H2D desc"))
+      break;
+    if (!hip_ok(hipMemcpy(d_order, order.data(), n * sizeof(uint32_t), hipMemcpyHostToDevice),
+                "H2D order"))
+      break;
+    if (LzmaGpu_DecodeBatch(static_cast<LzmaGpuStreamDesc*>(d_desc),
+                            static_cast<uint32_t*>(d_order), n, static_cast<Byte*>(d_src),
+                            static_cast<Byte*>(d_dst), d_ws, ws,
+                            static_cast<LzmaGpuResult*>(d_res), nullptr) != SZ_OK)
+      break;
+    if (!hip_ok(hipDeviceSynchronize(), "decode kernel")) break;
+    if (!hip_ok(hipMemcpy(results, d_res, n * sizeof(LzmaGpuResult), hipMemcpyDeviceToHost),
+                "D2H results"))
+      break;
+    if (dst_bytes && !hip_ok(hipMemcpy(dst, d_dst, dst_bytes, hipMemcpyDeviceToHost), "D2H dst"))
+      break;
+    r = SZ_OK;
+  } while (0);
+  (void)hipFree(d_src);
+  (void)hipFree(d_dst);
+  (void)hipFree(d_ws);
+  (void)hipFree(d_desc);
+  (void)hipFree(d_order);
+  (void)hipFree(d_res);
+  return r;
+}
+
+size_t Lzma2Gpu_SplitBlocks(const Byte* src, size_t src_len, uint64_t* src_off,
+                            uint64_t* block_src_len, uint64_t* unpack, size_t max_blocks) {
+  size_t pos = 0, nb = 0;
+  uint64_t cur_unpack = 0;
+  bool open = false;
+  auto close_block = [&](size_t end) {
+    if (open && nb - 1 < max_blocks) {
+      block_src_len[nb - 1] = end - src_off[nb - 1];
+      unpack[nb - 1] = cur_unpack;
+    }
+  };
+  while (pos < src_len) {
+    const Byte c = src[pos];
+    if (c == 0) {
+      close_block(pos);
+      return nb;
+    }
+    const bool is_lzma = (c & 0x80) != 0;
+    if (!is_lzma && c > 2) return size_t(-1);
+    const bool reset = (c == 1) || (c >= 0xE0);
+    if (reset) {
+      close_block(pos);
+      if (nb < max_blocks) src_off[nb] = pos;
+      nb++;
+      open = true;
+      cur_unpack = 0;
+    } else if (!open) {
+      return size_t(-1);  // stream must start with a dictionary reset
+    }
+    if (is_lzma) {
+      if (pos + 5 > src_len) return size_t(-1);
+      const uint64_t u = (uint64_t(c & 0x1F) << 16) + (uint64_t(src[pos + 1]) << 8) + src[pos + 2] + 1;
+      const uint64_t pk = (uint64_t(src[pos + 3]) << 8) + src[pos + 4] + 1;
+      const size_t hdr = (((c >> 5) & 3) >= 2) ? 6 : 5;
+      cur_unpack += u;
+      pos += hdr + pk;
+    } else {
+      if (pos + 3 > src_len) return size_t(-1);
+      const uint64_t u = (uint64_t(src[pos + 1]) << 8) + src[pos + 2] + 1;
+      cur_unpack += u;
+      pos += 3 + u;
+    }
+  }
+  if (pos > src_len) return size_t(-1);
+  close_block(src_len);  // no EOS byte: the last block runs to the end
+  return nb;
+}
+
+int LzmaGpu_DeviceCount(void) { return device_count(); }
+
+const char* LzmaGpu_LastError(void) { return g_last_error.c_str(); }
+
+const char* LzmaGpu_Version(void) { return "liblzmagpu 0.1 (gfx950, LZMA SDK 9.20 decoder contract)"; }
+
+}  // extern "C"

@@ -1,0 +1,650 @@
+// lzma_device.h -- per-lane LZMA decoder for CDNA4 (gfx950).
+//
+// One independent LZMA stream per lane.  Every lane runs the complete
+// LzmaDec_DecodeToDic contract (LzmaDec.c:719-838) on its own state, so the
+// observable results {res, status, destLen, srcLen} -- which depend on the
+// reference's call segmentation: bulk pass bounded at inSize-20, one-symbol
+// tail passes behind a dry-run look-ahead, the dictionary-size split -- are
+// reproduced exactly, including truncated and corrupt streams.
+//
+// Memory layout per lane (all device memory):
+//   probs  : CLzmaProb[1846 + 0x300 << (lc+lp)] in the LZMA-format order
+//            (offsets below), 16-bit cells;
+//   dic    : the caller's output window, which IS the dictionary (as in
+//            LzmaDecode, LzmaDec.c:988-989) or a ring of dicBufSize bytes;
+//   input  : the compressed bytes, read through a register window refilled
+//            with aligned 4-byte loads one word ahead, so NORMALIZE does not
+//            wait on memory.
+//
+// Reference map: bit/tree/direct-bit primitives LzmaDec.c:8-45,323-344;
+// symbol loop :131-426 (lz_run); pending flush :428-452; dictionary split
+// :454-477 (lz_run_split); look-ahead :487-675 (lz_probe); driver :719-838
+// (lz_decode_to_dic); LZMA2 chunk walker Lzma2Dec.c:98-289 (lz2_*).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace lzgpu {
+
+enum : int { kOk = 0, kErrData = 1, kErrMem = 2, kErrUnsupported = 4, kErrInputEof = 6 };
+enum : int { kStNone = 0, kStDoneMark = 1, kStNotDone = 2, kStMoreInput = 3, kStMaybeDone = 4 };
+enum : int { kFinAny = 0, kFinEnd = 1 };
+
+constexpr uint32_t kTop = 1u << 24;
+constexpr uint32_t kProbOne = 2048u;
+constexpr uint32_t kProbInit = 1024u;
+constexpr uint32_t kLookahead = 20u;  // LZMA_REQUIRED_INPUT_MAX
+constexpr uint32_t kLenDone = 274u;   // kMatchSpecLenStart
+
+// LZMA-format probability layout (16-bit cells).
+enum : uint32_t {
+  P_IS_MATCH = 0, P_IS_REP = 192, P_IS_REP_G0 = 204, P_IS_REP_G1 = 216, P_IS_REP_G2 = 228,
+  P_IS_REP0_LONG = 240, P_POS_SLOT = 432, P_SPEC_POS = 688, P_ALIGN = 802, P_LEN = 818,
+  P_REP_LEN = 1332, P_LITERAL = 1846
+};
+enum : uint32_t { L_CHOICE = 0, L_CHOICE2 = 1, L_LOW = 2, L_MID = 130, L_HIGH = 258 };
+
+__host__ __device__ inline uint32_t num_probs(uint32_t lc, uint32_t lp) {
+  return 1846u + (768u << (lc + lp));
+}
+
+// Per-lane decoder state (CLzmaDec fields, LzmaDec.h:50-69).
+struct LzState {
+  uint32_t lc, lp, pb, dict_size;
+  uint16_t* probs;
+  uint8_t* dic;
+  uint64_t cap;   // dicBufSize
+  uint64_t pos;   // dicPos
+  uint32_t range, code;
+  uint32_t total;  // processedPos
+  uint32_t full;   // checkDicSize
+  uint32_t st;
+  uint32_t rep0, rep1, rep2, rep3;
+  uint32_t pending;  // remainLen
+  uint32_t need_rc_init, need_state_init;
+  uint32_t tmp_n;
+  uint8_t tmp[kLookahead];
+};
+
+__device__ __forceinline__ uint64_t ring_back(uint64_t pos, uint32_t dist, uint64_t cap) {
+  return pos - dist + (pos < dist ? cap : 0);
+}
+
+// ------------------------------------------------------------------ input readers
+
+// Prefetching reader over a lane's compressed bytes in global memory.  Holds up
+// to 7 bytes in `win` plus one prefetched aligned word in `pend`; the word is
+// merged only when fewer than 4 bytes remain, one full word after its load
+// was issued.  Never loads an aligned word that lies wholly outside
+// [base, base+avail) (so it cannot fault past the end of an allocation).
+struct GlobalReader {
+  const uint32_t* wp;    // next aligned word to prefetch
+  const uint32_t* wend;  // one past the last word that holds a valid byte
+  uint64_t win;
+  uint32_t nb;
+  uint32_t pend;
+  uint32_t idx;  // bytes consumed since init
+
+  __device__ __forceinline__ void init(const uint8_t* p, uint64_t avail) {
+    uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    uintptr_t a0 = a & ~uintptr_t(3);
+    uint32_t skip = uint32_t(a & 3);
+    wend = reinterpret_cast<const uint32_t*>((a + avail + 3) & ~uintptr_t(3));
+    const uint32_t* w = reinterpret_cast<const uint32_t*>(a0);
+    idx = 0;
+    if (avail == 0) {
+      win = 0; nb = 0; pend = 0; wp = w; return;
+    }
+    win = uint64_t(__builtin_nontemporal_load(w) >> (8 * skip));
+    nb = 4 - skip;
+    wp = w + 1;
+    pend = (wp < wend) ? *wp : 0u;
+    ++wp;
+  }
+  __device__ __forceinline__ uint32_t next() {
+    uint32_t b = uint32_t(win) & 0xFFu;
+    win >>= 8;
+    --nb;
+    ++idx;
+    if (nb < 4) {
+      win |= uint64_t(pend) << (8 * nb);
+      nb += 4;
+      pend = (wp < wend) ? *wp : 0u;
+      ++wp;
+    }
+    return b;
+  }
+};
+
+// Reader over a lane-private byte array (the tempBuf path).
+struct LocalReader {
+  const uint8_t* p;
+  uint32_t idx;
+  __device__ __forceinline__ void init(const uint8_t* q) { p = q; idx = 0; }
+  __device__ __forceinline__ uint32_t next() { return p[idx++]; }
+};
+
+// ------------------------------------------------------------------ symbol loop
+
+template <class Rd>
+struct Rc {
+  uint32_t range, code;
+  Rd* rd;
+  __device__ __forceinline__ void norm() {
+    if (range < kTop) {
+      range <<= 8;
+      code = (code << 8) | rd->next();
+    }
+  }
+  __device__ __forceinline__ uint32_t bit(uint16_t* prob) {
+    uint32_t p = *prob;
+    norm();
+    uint32_t bound = (range >> 11) * p;
+    if (code < bound) {
+      range = bound;
+      *prob = uint16_t(p + ((kProbOne - p) >> 5));
+      return 0;
+    }
+    range -= bound;
+    code -= bound;
+    *prob = uint16_t(p - (p >> 5));
+    return 1;
+  }
+  __device__ __forceinline__ uint32_t tree(uint16_t* probs, uint32_t bits) {
+    uint32_t m = 1, lim = 1u << bits;
+    while (m < lim) m = (m << 1) | bit(probs + m);
+    return m - lim;
+  }
+  __device__ __forceinline__ void direct(uint32_t& v) {
+    norm();
+    range >>= 1;
+    code -= range;
+    uint32_t t = 0u - (code >> 31);
+    v = (v << 1) + (t + 1u);
+    code += range & t;
+  }
+};
+
+// Copy n bytes of an LZ match: dic[pos..pos+n) = dic[from..], byte-serial
+// overlap semantics (rep0 < n replicates the period), ring wrap at cap.
+// Non-overlapping, non-wrapping spans go 8 bytes per round trip.
+__device__ __forceinline__ uint32_t lz_copy(uint8_t* dic, uint64_t pos, uint64_t from, uint32_t n,
+                                            uint32_t dist, uint64_t cap) {
+  uint32_t last = 0;
+  if (from + n <= cap) {
+    uint8_t* d = dic + pos;
+    const uint8_t* s = dic + from;
+    uint32_t i = 0;
+    if (dist >= 8) {
+      for (; i + 8 <= n; i += 8) {
+        uint8_t b0 = s[i], b1 = s[i + 1], b2 = s[i + 2], b3 = s[i + 3];
+        uint8_t b4 = s[i + 4], b5 = s[i + 5], b6 = s[i + 6], b7 = s[i + 7];
+        d[i] = b0; d[i + 1] = b1; d[i + 2] = b2; d[i + 3] = b3;
+        d[i + 4] = b4; d[i + 5] = b5; d[i + 6] = b6; d[i + 7] = b7;
+        last = b7;
+      }
+    }
+    for (; i < n; ++i) {
+      uint8_t b = s[i];
+      d[i] = b;
+      last = b;
+    }
+  } else {
+    do {
+      uint8_t b = dic[from];
+      dic[pos++] = b;
+      last = b;
+      if (++from == cap) from = 0;
+    } while (--n != 0);
+  }
+  return last;
+}
+
+// Decode symbols until pos reaches `limit` or the reader index reaches
+// `in_limit` (checked after each whole symbol; the first is always decoded).
+// State is written back only on success, as LzmaDec_DecodeReal does.
+template <class Rd>
+__device__ int lz_run(LzState& s, uint64_t limit, Rd& rd, uint32_t in_limit) {
+  uint16_t* __restrict__ pr = s.probs;
+  uint32_t st = s.st;
+  uint32_t r0 = s.rep0, r1 = s.rep1, r2 = s.rep2, r3 = s.rep3;
+  const uint32_t pb_mask = (1u << s.pb) - 1, lp_mask = (1u << s.lp) - 1;
+  const uint32_t lc = s.lc;
+  uint8_t* __restrict__ dic = s.dic;
+  const uint64_t cap = s.cap;
+  uint64_t pos = s.pos;
+  uint32_t total = s.total;
+  const uint32_t full = s.full;
+  uint32_t len = 0;
+  Rc<Rd> rc{s.range, s.code, &rd};
+  // previous byte (literal context), kept in a register
+  uint32_t prev = 0;
+  if (full != 0 || total != 0) prev = dic[(pos == 0 ? cap : pos) - 1];
+
+  do {
+    const uint32_t ps = total & pb_mask;
+    uint32_t lcoder;
+    if (!rc.bit(pr + P_IS_MATCH + (st << 4) + ps)) {
+      uint16_t* lit = pr + P_LITERAL;
+      uint32_t sym = 1;
+      if (full != 0 || total != 0)
+        lit += 768u * (((total & lp_mask) << lc) + (prev >> (8 - lc)));
+      if (st < 7) {
+        st = (st < 4) ? 0 : st - 3;
+        do sym = (sym << 1) | rc.bit(lit + sym); while (sym < 0x100);
+      } else {
+        uint32_t mbyte = dic[ring_back(pos, r0, cap)];
+        uint32_t offs = 0x100;
+        st = (st < 10) ? st - 3 : st - 6;
+        do {
+          mbyte <<= 1;
+          uint32_t mbit = mbyte & offs;
+          uint32_t b = rc.bit(lit + offs + mbit + sym);
+          sym = (sym << 1) | b;
+          offs = b ? (offs & mbit) : (offs & ~mbit);
+        } while (sym < 0x100);
+      }
+      prev = sym & 0xFFu;
+      dic[pos++] = uint8_t(prev);
+      total++;
+      continue;
+    }
+    if (!rc.bit(pr + P_IS_REP + st)) {
+      st += 12;
+      lcoder = P_LEN;
+    } else {
+      if (full == 0 && total == 0) return kErrData;
+      if (!rc.bit(pr + P_IS_REP_G0 + st)) {
+        if (!rc.bit(pr + P_IS_REP0_LONG + (st << 4) + ps)) {
+          prev = dic[ring_back(pos, r0, cap)];
+          dic[pos++] = uint8_t(prev);
+          total++;
+          st = (st < 7) ? 9 : 11;
+          continue;
+        }
+      } else {
+        uint32_t dist;
+        if (!rc.bit(pr + P_IS_REP_G1 + st)) {
+          dist = r1;
+        } else {
+          if (!rc.bit(pr + P_IS_REP_G2 + st)) {
+            dist = r2;
+          } else {
+            dist = r3;
+            r3 = r2;
+          }
+          r2 = r1;
+        }
+        r1 = r0;
+        r0 = dist;
+      }
+      st = (st < 7) ? 8 : 11;
+      lcoder = P_REP_LEN;
+    }
+    if (!rc.bit(pr + lcoder + L_CHOICE))
+      len = rc.tree(pr + lcoder + L_LOW + (ps << 3), 3);
+    else if (!rc.bit(pr + lcoder + L_CHOICE2))
+      len = 8 + rc.tree(pr + lcoder + L_MID + (ps << 3), 3);
+    else
+      len = 16 + rc.tree(pr + lcoder + L_HIGH, 8);
+
+    if (st >= 12) {
+      const uint32_t lstate = len < 4 ? len : 3;
+      uint32_t dist = rc.tree(pr + P_POS_SLOT + (lstate << 6), 6);
+      if (dist >= 4) {
+        const uint32_t slot = dist;
+        uint32_t nbits = (slot >> 1) - 1;
+        dist = 2 | (slot & 1);
+        if (slot < 14) {
+          dist <<= nbits;
+          uint16_t* sp = pr + P_SPEC_POS + dist - slot - 1;
+          uint32_t mask = 1, node = 1;
+          do {
+            uint32_t b = rc.bit(sp + node);
+            node = (node << 1) | b;
+            dist |= b ? mask : 0u;
+            mask <<= 1;
+          } while (--nbits != 0);
+        } else {
+          nbits -= 4;
+          do rc.direct(dist); while (--nbits != 0);
+          dist <<= 4;
+          uint32_t node = 1;
+#pragma unroll
+          for (uint32_t k = 0; k < 4; ++k) {
+            uint32_t b = rc.bit(pr + P_ALIGN + node);
+            node = (node << 1) | b;
+            dist |= b << k;
+          }
+          if (dist == 0xFFFFFFFFu) {
+            len += kLenDone;
+            st -= 12;
+            break;
+          }
+        }
+      }
+      r3 = r2;
+      r2 = r1;
+      r1 = r0;
+      r0 = dist + 1;
+      if (full == 0) {
+        if (dist >= total) return kErrData;
+      } else if (dist >= full) {
+        return kErrData;
+      }
+      st = (st < 19) ? 7 : 10;
+    }
+    len += 2;
+    if (limit == pos) return kErrData;
+    {
+      const uint64_t room = limit - pos;
+      const uint32_t n = (room < len) ? uint32_t(room) : len;
+      const uint64_t from = ring_back(pos, r0, cap);
+      total += n;
+      len -= n;
+      prev = lz_copy(dic, pos, from, n, r0, cap);
+      pos += n;
+    }
+  } while (pos < limit && rd.idx < in_limit);
+
+  rc.norm();
+  s.range = rc.range;
+  s.code = rc.code;
+  s.pending = len;
+  s.pos = pos;
+  s.total = total;
+  s.rep0 = r0;
+  s.rep1 = r1;
+  s.rep2 = r2;
+  s.rep3 = r3;
+  s.st = st;
+  return kOk;
+}
+
+__device__ inline void lz_flush_pending(LzState& s, uint64_t limit) {
+  if (s.pending == 0 || s.pending >= kLenDone) return;
+  uint32_t n = s.pending;
+  if (limit - s.pos < n) n = uint32_t(limit - s.pos);
+  if (s.full == 0 && s.dict_size - s.total <= n) s.full = s.dict_size;
+  s.total += n;
+  s.pending -= n;
+  while (n-- != 0) {
+    s.dic[s.pos] = s.dic[ring_back(s.pos, s.rep0, s.cap)];
+    s.pos++;
+  }
+}
+
+template <class Rd>
+__device__ int lz_run_split(LzState& s, uint64_t limit, Rd& rd, uint32_t in_limit) {
+  do {
+    uint64_t lim = limit;
+    if (s.full == 0) {
+      uint32_t left = s.dict_size - s.total;
+      if (limit - s.pos > left) lim = s.pos + left;
+    }
+    if (lz_run(s, lim, rd, in_limit) != kOk) return kErrData;
+    if (s.total >= s.dict_size) s.full = s.dict_size;
+    lz_flush_pending(s, limit);
+  } while (s.pos < limit && rd.idx < in_limit && s.pending < kLenDone);
+  if (s.pending > kLenDone) s.pending = kLenDone;
+  return kOk;
+}
+
+// ------------------------------------------------------------------ look-ahead dry run
+
+enum : int { PROBE_SHORT = 0, PROBE_LIT = 1, PROBE_MATCH = 2, PROBE_REP = 3 };
+
+struct Probe {
+  uint32_t range, code;
+  const uint8_t* in;
+  const uint8_t* end;
+  __device__ __forceinline__ bool norm() {
+    if (range < kTop) {
+      if (in >= end) return false;
+      range <<= 8;
+      code = (code << 8) | *in++;
+    }
+    return true;
+  }
+  // 0/1, or -1 when the input ran out
+  __device__ __forceinline__ int bit(const uint16_t* prob) {
+    if (!norm()) return -1;
+    uint32_t bound = (range >> 11) * uint32_t(*prob);
+    if (code < bound) { range = bound; return 0; }
+    range -= bound;
+    code -= bound;
+    return 1;
+  }
+  __device__ __forceinline__ bool tree(const uint16_t* probs, uint32_t bits, uint32_t& out) {
+    uint32_t m = 1, lim = 1u << bits;
+    while (m < lim) {
+      int b = bit(probs + m);
+      if (b < 0) return false;
+      m = (m << 1) | uint32_t(b);
+    }
+    out = m - lim;
+    return true;
+  }
+};
+
+// Would one more symbol decode from [in, in+n)?  (LzmaDec_TryDummy)
+__device__ int lz_probe(const LzState& s, const uint8_t* in, uint64_t n) {
+  const uint16_t* pr = s.probs;
+  const uint32_t ps = s.total & ((1u << s.pb) - 1);
+  uint32_t st = s.st, lcoder, len = 0;
+  int kind, b;
+  Probe t{s.range, s.code, in, in + n};
+#define LZ_PB(p) do { b = t.bit(p); if (b < 0) return PROBE_SHORT; } while (0)
+  LZ_PB(pr + P_IS_MATCH + (st << 4) + ps);
+  if (b == 0) {
+    const uint16_t* lit = pr + P_LITERAL;
+    uint32_t sym = 1;
+    if (s.full != 0 || s.total != 0) {
+      uint32_t prev = s.dic[(s.pos == 0 ? s.cap : s.pos) - 1];
+      lit += 768u * (((s.total & ((1u << s.lp) - 1)) << s.lc) + (prev >> (8 - s.lc)));
+    }
+    if (st < 7) {
+      while (sym < 0x100) {
+        LZ_PB(lit + sym);
+        sym = (sym << 1) | uint32_t(b);
+      }
+    } else {
+      uint32_t mbyte = s.dic[ring_back(s.pos, s.rep0, s.cap)];
+      uint32_t offs = 0x100;
+      while (sym < 0x100) {
+        mbyte <<= 1;
+        uint32_t mbit = mbyte & offs;
+        LZ_PB(lit + offs + mbit + sym);
+        sym = (sym << 1) | uint32_t(b);
+        offs = b ? (offs & mbit) : (offs & ~mbit);
+      }
+    }
+    kind = PROBE_LIT;
+  } else {
+    LZ_PB(pr + P_IS_REP + st);
+    if (b == 0) {
+      st = 0;
+      lcoder = P_LEN;
+      kind = PROBE_MATCH;
+    } else {
+      kind = PROBE_REP;
+      LZ_PB(pr + P_IS_REP_G0 + st);
+      if (b == 0) {
+        LZ_PB(pr + P_IS_REP0_LONG + (st << 4) + ps);
+        if (b == 0) return t.norm() ? PROBE_REP : PROBE_SHORT;
+      } else {
+        LZ_PB(pr + P_IS_REP_G1 + st);
+        if (b != 0) LZ_PB(pr + P_IS_REP_G2 + st);
+      }
+      st = 12;
+      lcoder = P_REP_LEN;
+    }
+    LZ_PB(pr + lcoder + L_CHOICE);
+    if (b == 0) {
+      if (!t.tree(pr + lcoder + L_LOW + (ps << 3), 3, len)) return PROBE_SHORT;
+    } else {
+      LZ_PB(pr + lcoder + L_CHOICE2);
+      if (b == 0) {
+        if (!t.tree(pr + lcoder + L_MID + (ps << 3), 3, len)) return PROBE_SHORT;
+        len += 8;
+      } else {
+        if (!t.tree(pr + lcoder + L_HIGH, 8, len)) return PROBE_SHORT;
+        len += 16;
+      }
+    }
+    if (st < 4) {
+      uint32_t slot;
+      if (!t.tree(pr + P_POS_SLOT + ((len < 4 ? len : 3) << 6), 6, slot)) return PROBE_SHORT;
+      if (slot >= 4) {
+        uint32_t nbits = (slot >> 1) - 1, node = 1;
+        const uint16_t* base;
+        if (slot < 14) {
+          base = pr + P_SPEC_POS + ((2u | (slot & 1)) << nbits) - slot - 1;
+        } else {
+          nbits -= 4;
+          do {
+            if (!t.norm()) return PROBE_SHORT;
+            t.range >>= 1;
+            t.code -= t.range & (((t.code - t.range) >> 31) - 1);
+          } while (--nbits != 0);
+          base = pr + P_ALIGN;
+          nbits = 4;
+        }
+        do {
+          LZ_PB(base + node);
+          node = (node << 1) | uint32_t(b);
+        } while (--nbits != 0);
+      }
+    }
+  }
+#undef LZ_PB
+  return t.norm() ? kind : PROBE_SHORT;
+}
+
+// ------------------------------------------------------------------ init + driver
+
+__device__ inline void lz_init_state_real(LzState& s) {
+  const uint32_t n = num_probs(s.lc, s.lp);
+  // 8-byte stores where possible (the table starts 8-byte aligned)
+  uint64_t* p8 = reinterpret_cast<uint64_t*>(s.probs);
+  const uint64_t v = 0x0400040004000400ull;
+  uint32_t i = 0;
+  for (; i + 4 <= n; i += 4) p8[i >> 2] = v;
+  for (; i < n; ++i) s.probs[i] = uint16_t(kProbInit);
+  s.rep0 = s.rep1 = s.rep2 = s.rep3 = 1;
+  s.st = 0;
+  s.need_state_init = 0;
+}
+
+__device__ inline void lz_init_dic_state(LzState& s, bool init_dic, bool init_state) {
+  s.need_rc_init = 1;
+  s.pending = 0;
+  s.tmp_n = 0;
+  if (init_dic) {
+    s.total = 0;
+    s.full = 0;
+    s.need_state_init = 1;
+  }
+  if (init_state) s.need_state_init = 1;
+}
+
+// LzmaDec_DecodeToDic for one lane.  src is global memory.
+__device__ int lz_decode_to_dic(LzState& s, uint64_t dic_limit, const uint8_t* src,
+                                uint64_t& src_len, int fin, int& status) {
+  uint64_t avail = src_len;
+  src_len = 0;
+  lz_flush_pending(s, dic_limit);
+  status = kStNone;
+
+  while (s.pending != kLenDone) {
+    bool at_end_check = false;
+    if (s.need_rc_init) {
+      while (avail > 0 && s.tmp_n < 5) {
+        s.tmp[s.tmp_n++] = *src++;
+        src_len++;
+        avail--;
+      }
+      if (s.tmp_n < 5) { status = kStMoreInput; return kOk; }
+      if (s.tmp[0] != 0) return kErrData;
+      s.code = (uint32_t(s.tmp[1]) << 24) | (uint32_t(s.tmp[2]) << 16) |
+               (uint32_t(s.tmp[3]) << 8) | uint32_t(s.tmp[4]);
+      s.range = 0xFFFFFFFFu;
+      s.need_rc_init = 0;
+      s.tmp_n = 0;
+    }
+    if (s.pos >= dic_limit) {
+      if (s.pending == 0 && s.code == 0) { status = kStMaybeDone; return kOk; }
+      if (fin == kFinAny) { status = kStNotDone; return kOk; }
+      if (s.pending != 0) { status = kStNotDone; return kErrData; }
+      at_end_check = true;
+    }
+    if (s.need_state_init) lz_init_state_real(s);
+
+    if (s.tmp_n == 0) {
+      uint32_t in_limit;
+      if (avail < kLookahead || at_end_check) {
+        int k = lz_probe(s, src, avail);
+        if (k == PROBE_SHORT) {
+          for (uint32_t i = 0; i < uint32_t(avail); ++i) s.tmp[i] = src[i];
+          s.tmp_n = uint32_t(avail);
+          src_len += avail;
+          status = kStMoreInput;
+          return kOk;
+        }
+        if (at_end_check && k != PROBE_MATCH) { status = kStNotDone; return kErrData; }
+        in_limit = 0;
+      } else {
+        uint64_t lim = avail - kLookahead;
+        in_limit = lim > 0xFFFFFFF0ull ? 0xFFFFFFF0u : uint32_t(lim);
+      }
+      GlobalReader rd;
+      rd.init(src, avail);
+      if (lz_run_split(s, dic_limit, rd, in_limit) != kOk) return kErrData;
+      const uint32_t used = rd.idx;
+      src_len += used;
+      src += used;
+      avail -= used;
+    } else {
+      uint32_t have = s.tmp_n, taken = 0;
+      while (have < kLookahead && taken < avail) s.tmp[have++] = src[taken++];
+      s.tmp_n = have;
+      if (have < kLookahead || at_end_check) {
+        int k = lz_probe(s, s.tmp, have);
+        if (k == PROBE_SHORT) {
+          src_len += taken;
+          status = kStMoreInput;
+          return kOk;
+        }
+        if (at_end_check && k != PROBE_MATCH) { status = kStNotDone; return kErrData; }
+      }
+      LocalReader rd;
+      rd.init(s.tmp);
+      if (lz_run_split(s, dic_limit, rd, 0) != kOk) return kErrData;
+      taken -= (have - rd.idx);
+      src_len += taken;
+      src += taken;
+      avail -= taken;
+      s.tmp_n = 0;
+    }
+  }
+  if (s.code == 0) status = kStDoneMark;
+  return s.code == 0 ? kOk : kErrData;
+}
+
+// ------------------------------------------------------------------ props
+
+__device__ __host__ inline int lz_props_parse(const uint8_t* b, uint32_t n, uint32_t& lc,
+                                              uint32_t& lp, uint32_t& pb, uint32_t& dict) {
+  if (n < 5) return kErrUnsupported;
+  dict = uint32_t(b[1]) | (uint32_t(b[2]) << 8) | (uint32_t(b[3]) << 16) | (uint32_t(b[4]) << 24);
+  if (dict < 4096) dict = 4096;
+  uint32_t d = b[0];
+  if (d >= 225) return kErrUnsupported;
+  lc = d % 9;
+  lp = (d / 9) % 5;
+  pb = d / 45;
+  return kOk;
+}
+
+}  // namespace lzgpu

@@ -1,0 +1,271 @@
+"""lzmagpu -- Python mirror of liblzmagpu.so (include/lzma_gpu.h) over ctypes.
+
+The product is the C ABI; this module only binds it for the test-suite and
+bench.py.  Function names and argument meaning follow the reference C API
+(LzmaDec.h / LzmaLib.h / Lzma2Dec.h): ``LzmaDecode`` returns the same
+``(res, status, destLen, srcLen)`` the reference returns through its
+out-parameters, plus the output bytes.
+
+There is no fallback: if lib/liblzmagpu.so is missing this module raises at
+import time, and on a machine without a HIP device every decode returns
+SZ_ERROR_FAIL (``LzmaGpu_LastError`` says why).
+"""
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "liblzmagpu.so")
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(f"liblzmagpu.so not built ({LIB_PATH}); run __graft_entry__.build()")
+
+SZ_OK, SZ_ERROR_DATA, SZ_ERROR_MEM, SZ_ERROR_UNSUPPORTED = 0, 1, 2, 4
+SZ_ERROR_PARAM, SZ_ERROR_INPUT_EOF, SZ_ERROR_FAIL = 5, 6, 11
+LZMA_FINISH_ANY, LZMA_FINISH_END = 0, 1
+KIND_LZMA, KIND_LZMA2 = 0, 1
+
+_lib = ctypes.CDLL(LIB_PATH)
+_sp = ctypes.POINTER(ctypes.c_size_t)
+_ip = ctypes.POINTER(ctypes.c_int)
+
+
+class ISzAlloc(ctypes.Structure):
+    _fields_ = [("Alloc", ctypes.CFUNCTYPE(ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t)),
+                ("Free", ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_void_p))]
+
+
+class CLzmaProps(ctypes.Structure):
+    _fields_ = [("lc", ctypes.c_uint), ("lp", ctypes.c_uint), ("pb", ctypes.c_uint),
+                ("dicSize", ctypes.c_uint32)]
+
+
+class CLzmaDec(ctypes.Structure):
+    """Public layout of LzmaDec.h:50-69."""
+    _fields_ = [("prop", CLzmaProps), ("probs", ctypes.c_void_p), ("dic", ctypes.c_void_p),
+                ("buf", ctypes.c_void_p), ("range", ctypes.c_uint32), ("code", ctypes.c_uint32),
+                ("dicPos", ctypes.c_size_t), ("dicBufSize", ctypes.c_size_t),
+                ("processedPos", ctypes.c_uint32), ("checkDicSize", ctypes.c_uint32),
+                ("state", ctypes.c_uint), ("reps", ctypes.c_uint32 * 4),
+                ("remainLen", ctypes.c_uint), ("needFlush", ctypes.c_int),
+                ("needInitState", ctypes.c_int), ("numProbs", ctypes.c_uint32),
+                ("tempBufSize", ctypes.c_uint), ("tempBuf", ctypes.c_ubyte * 20)]
+
+
+class CLzma2Dec(ctypes.Structure):
+    _fields_ = [("decoder", CLzmaDec), ("packSize", ctypes.c_uint32),
+                ("unpackSize", ctypes.c_uint32), ("state", ctypes.c_int),
+                ("control", ctypes.c_ubyte), ("needInitDic", ctypes.c_int),
+                ("needInitState", ctypes.c_int), ("needInitProp", ctypes.c_int)]
+
+
+class StreamDesc(ctypes.Structure):
+    _fields_ = [("src_off", ctypes.c_uint64), ("src_len", ctypes.c_uint64),
+                ("dst_off", ctypes.c_uint64), ("dst_cap", ctypes.c_uint64),
+                ("probs_off", ctypes.c_uint64), ("props", ctypes.c_ubyte * 5),
+                ("props_size", ctypes.c_ubyte), ("finish_mode", ctypes.c_ubyte),
+                ("kind", ctypes.c_ubyte)]
+
+
+class Result(ctypes.Structure):
+    _fields_ = [("res", ctypes.c_int32), ("status", ctypes.c_int32),
+                ("dest_len", ctypes.c_uint64), ("src_len", ctypes.c_uint64)]
+
+
+assert ctypes.sizeof(StreamDesc) == 48 and ctypes.sizeof(Result) == 24
+assert ctypes.sizeof(CLzmaDec) == 136
+
+_P = ctypes.c_void_p
+_sig = {
+    "LzmaProps_Decode": (ctypes.c_int, [ctypes.POINTER(CLzmaProps), ctypes.c_char_p, ctypes.c_uint]),
+    "LzmaDec_AllocateProbs": (ctypes.c_int, [ctypes.POINTER(CLzmaDec), ctypes.c_char_p, ctypes.c_uint, ctypes.POINTER(ISzAlloc)]),
+    "LzmaDec_FreeProbs": (None, [ctypes.POINTER(CLzmaDec), ctypes.POINTER(ISzAlloc)]),
+    "LzmaDec_Allocate": (ctypes.c_int, [ctypes.POINTER(CLzmaDec), ctypes.c_char_p, ctypes.c_uint, ctypes.POINTER(ISzAlloc)]),
+    "LzmaDec_Free": (None, [ctypes.POINTER(CLzmaDec), ctypes.POINTER(ISzAlloc)]),
+    "LzmaDec_Init": (None, [ctypes.POINTER(CLzmaDec)]),
+    "LzmaDec_InitDicAndState": (None, [ctypes.POINTER(CLzmaDec), ctypes.c_int, ctypes.c_int]),
+    "LzmaDec_DecodeToDic": (ctypes.c_int, [ctypes.POINTER(CLzmaDec), ctypes.c_size_t, _P, _sp, ctypes.c_int, _ip]),
+    "LzmaDec_DecodeToBuf": (ctypes.c_int, [ctypes.POINTER(CLzmaDec), _P, _sp, _P, _sp, ctypes.c_int, _ip]),
+    "LzmaDecode": (ctypes.c_int, [_P, _sp, _P, _sp, ctypes.c_char_p, ctypes.c_uint, ctypes.c_int, _ip, ctypes.POINTER(ISzAlloc)]),
+    "LzmaUncompress": (ctypes.c_int, [_P, _sp, _P, _sp, ctypes.c_char_p, ctypes.c_size_t]),
+    "Lzma2Dec_AllocateProbs": (ctypes.c_int, [ctypes.POINTER(CLzma2Dec), ctypes.c_ubyte, ctypes.POINTER(ISzAlloc)]),
+    "Lzma2Dec_Allocate": (ctypes.c_int, [ctypes.POINTER(CLzma2Dec), ctypes.c_ubyte, ctypes.POINTER(ISzAlloc)]),
+    "Lzma2Dec_Init": (None, [ctypes.POINTER(CLzma2Dec)]),
+    "Lzma2Dec_DecodeToDic": (ctypes.c_int, [ctypes.POINTER(CLzma2Dec), ctypes.c_size_t, _P, _sp, ctypes.c_int, _ip]),
+    "Lzma2Dec_DecodeToBuf": (ctypes.c_int, [ctypes.POINTER(CLzma2Dec), _P, _sp, _P, _sp, ctypes.c_int, _ip]),
+    "Lzma2Decode": (ctypes.c_int, [_P, _sp, _P, _sp, ctypes.c_ubyte, ctypes.c_int, _ip, ctypes.POINTER(ISzAlloc)]),
+    "LzmaGpu_PlanBatch": (ctypes.c_size_t, [ctypes.POINTER(StreamDesc), ctypes.c_size_t, _P]),
+    "LzmaGpu_DecodeBatch": (ctypes.c_int, [_P, _P, ctypes.c_size_t, _P, _P, _P, ctypes.c_size_t, _P, _P]),
+    "LzmaGpu_DecodeBatchHost": (ctypes.c_int, [ctypes.POINTER(StreamDesc), ctypes.c_size_t, _P, ctypes.c_size_t, _P, ctypes.c_size_t, ctypes.POINTER(Result)]),
+    "Lzma2Gpu_SplitBlocks": (ctypes.c_size_t, [_P, ctypes.c_size_t, _P, _P, _P, ctypes.c_size_t]),
+    "LzmaGpu_DeviceCount": (ctypes.c_int, []),
+    "LzmaGpu_LastError": (ctypes.c_char_p, []),
+    "LzmaGpu_Version": (ctypes.c_char_p, []),
+}
+for _name, (_rt, _at) in _sig.items():
+    _f = getattr(_lib, _name)
+    _f.restype = _rt
+    _f.argtypes = _at
+
+EXPORTED = tuple(_sig)
+lib = _lib
+
+_libc = ctypes.CDLL(None)
+_libc.malloc.restype = ctypes.c_void_p
+_libc.malloc.argtypes = [ctypes.c_size_t]
+_libc.free.argtypes = [ctypes.c_void_p]
+
+
+@ctypes.CFUNCTYPE(ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t)
+def _py_alloc(_p, n):
+    return _libc.malloc(n if n else 1)
+
+
+@ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_void_p)
+def _py_free(_p, a):
+    _libc.free(a)
+
+
+g_alloc = ISzAlloc(_py_alloc, _py_free)
+
+
+def last_error():
+    return _lib.LzmaGpu_LastError().decode()
+
+
+def device_count():
+    return _lib.LzmaGpu_DeviceCount()
+
+
+def _buf(data):
+    return ctypes.create_string_buffer(bytes(data), max(len(data), 1))
+
+
+# ---------------------------------------------------------------- one-call API
+
+def LzmaDecode(src, props, dest_cap, finish=LZMA_FINISH_END):
+    """LzmaDecode (LzmaDec.c:972). Returns (res, status, destLen, srcLen, out)."""
+    s = _buf(src)
+    d = ctypes.create_string_buffer(max(dest_cap, 1))
+    dl = ctypes.c_size_t(dest_cap)
+    sl = ctypes.c_size_t(len(src))
+    st = ctypes.c_int(-1)
+    res = _lib.LzmaDecode(d, ctypes.byref(dl), s, ctypes.byref(sl), bytes(props), len(props),
+                          finish, ctypes.byref(st), ctypes.byref(g_alloc))
+    return res, st.value, dl.value, sl.value, d.raw[:dl.value]
+
+
+def LzmaUncompress(src, props, dest_cap):
+    """LzmaUncompress (LzmaLib.c:41). Returns (res, destLen, srcLen, out)."""
+    s = _buf(src)
+    d = ctypes.create_string_buffer(max(dest_cap, 1))
+    dl = ctypes.c_size_t(dest_cap)
+    sl = ctypes.c_size_t(len(src))
+    res = _lib.LzmaUncompress(d, ctypes.byref(dl), s, ctypes.byref(sl), bytes(props), len(props))
+    return res, dl.value, sl.value, d.raw[:dl.value]
+
+
+def Lzma2Decode(src, prop, dest_cap, finish=LZMA_FINISH_END):
+    s = _buf(src)
+    d = ctypes.create_string_buffer(max(dest_cap, 1))
+    dl = ctypes.c_size_t(dest_cap)
+    sl = ctypes.c_size_t(len(src))
+    st = ctypes.c_int(-1)
+    res = _lib.Lzma2Decode(d, ctypes.byref(dl), s, ctypes.byref(sl), prop, finish,
+                           ctypes.byref(st), ctypes.byref(g_alloc))
+    return res, st.value, dl.value, sl.value, d.raw[:dl.value]
+
+
+# ---------------------------------------------------------------- streaming API
+
+def stream_decode(src, props, out_total, in_chunk, out_chunk, finish, max_calls=100000):
+    """zlib-like loop over LzmaDec_DecodeToBuf with bounded chunks -- the same
+    contract as the oracle's orc_lzma_stream_decode / the fork's
+    SzDecodeLzmaToFileWithBuf (7zDec.c:567-648).
+    Returns (calls, trace[(res, status, srcLen, destLen)], out, in_used)."""
+    dec = CLzmaDec()
+    dec.dic = None
+    dec.probs = None
+    r = _lib.LzmaDec_Allocate(ctypes.byref(dec), bytes(props), 5, ctypes.byref(g_alloc))
+    if r != SZ_OK:
+        return -r, [], b"", 0
+    _lib.LzmaDec_Init(ctypes.byref(dec))
+    sbuf = _buf(src)
+    out = ctypes.create_string_buffer(max(out_total, 1))
+    base_s = ctypes.addressof(sbuf)
+    base_o = ctypes.addressof(out)
+    in_pos = out_pos = 0
+    trace = []
+    try:
+        while len(trace) < max_calls:
+            sl = ctypes.c_size_t(min(len(src) - in_pos, in_chunk))
+            dl = ctypes.c_size_t(min(out_total - out_pos, out_chunk))
+            st = ctypes.c_int(-1)
+            res = _lib.LzmaDec_DecodeToBuf(ctypes.byref(dec), base_o + out_pos, ctypes.byref(dl),
+                                           base_s + in_pos, ctypes.byref(sl), finish,
+                                           ctypes.byref(st))
+            trace.append((res, st.value, sl.value, dl.value))
+            in_pos += sl.value
+            out_pos += dl.value
+            if res != SZ_OK or st.value == 1 or out_pos == out_total:
+                break
+            if sl.value == 0 and dl.value == 0:
+                break
+    finally:
+        _lib.LzmaDec_Free(ctypes.byref(dec), ctypes.byref(g_alloc))
+    return len(trace), trace, out.raw[:out_pos], in_pos
+
+
+# ---------------------------------------------------------------- batch API
+
+def make_descs(items):
+    """items: list of dicts with src_off, src_len, dst_off, dst_cap, props(bytes),
+    finish, kind.  Returns a ctypes StreamDesc array."""
+    arr = (StreamDesc * len(items))()
+    for i, it in enumerate(items):
+        d = arr[i]
+        d.src_off, d.src_len = it["src_off"], it["src_len"]
+        d.dst_off, d.dst_cap = it["dst_off"], it["dst_cap"]
+        p = bytes(it["props"])
+        for k in range(min(len(p), 5)):
+            d.props[k] = p[k]
+        d.props_size = it.get("props_size", len(p))
+        d.finish_mode = it.get("finish", LZMA_FINISH_END)
+        d.kind = it.get("kind", KIND_LZMA)
+    return arr
+
+
+def decode_batch_host(descs, src, dst_bytes):
+    """Decode a batch from host buffers.  Returns (res, results[ctypes], dst bytes)."""
+    n = len(descs)
+    res = (Result * max(n, 1))()
+    s = _buf(src)
+    d = ctypes.create_string_buffer(max(dst_bytes, 1))
+    r = _lib.LzmaGpu_DecodeBatchHost(descs, n, s, len(src), d, dst_bytes, res)
+    return r, res, d.raw[:dst_bytes]
+
+
+def plan(descs, order=None):
+    """Fill probs_off (and the lane order, a ctypes uint32 array). Returns workspace bytes."""
+    return _lib.LzmaGpu_PlanBatch(descs, len(descs), order)
+
+
+def decode_batch_device(d_descs, d_order, n, d_src, d_dst, d_ws, ws_bytes, d_results, stream=0):
+    """All arguments are raw device pointers (ints); stream is a hipStream_t (int)."""
+    return _lib.LzmaGpu_DecodeBatch(d_descs, d_order, n, d_src, d_dst, d_ws, ws_bytes, d_results,
+                                    stream or None)
+
+
+def split_lzma2_blocks(src):
+    """Lzma2Gpu_SplitBlocks: list of (src_off, src_len, unpack) per dict-reset block."""
+    cap = max(16, len(src) // 16)
+    s = _buf(src)
+    while True:
+        o = (ctypes.c_uint64 * cap)()
+        ln = (ctypes.c_uint64 * cap)()
+        u = (ctypes.c_uint64 * cap)()
+        nb = _lib.Lzma2Gpu_SplitBlocks(s, len(src), o, ln, u, cap)
+        if nb == ctypes.c_size_t(-1).value:
+            raise ValueError("malformed LZMA2 chunk headers")
+        if nb <= cap:
+            return [(o[i], ln[i], u[i]) for i in range(nb)]
+        cap = nb

@@ -1,0 +1,118 @@
+"""CPU-side checks of the C-ABI library (no GPU needed).
+
+- liblzmagpu.so loads and exports every function include/lzma_gpu.h declares;
+- struct sizes match the reference layouts (CLzmaDec is public ABI);
+- without a device, decode entry points fail loudly (SZ_ERROR_FAIL), never
+  silently fall back to a CPU path;
+- the host-side LZMA2 block splitter and batch planner (pure host logic).
+"""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+import native
+
+ROOT = native.ROOT
+HEADER = os.path.join(ROOT, "include", "lzma_gpu.h")
+LIB = os.path.join(ROOT, "lzma-sdk-zliblike_amd", "lib", "liblzmagpu.so")
+
+
+def header_functions():
+    txt = open(HEADER).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    names = re.findall(r"^\s*(?:SRes|void|int|size_t|const char \*)\s*\*?\s*(\w+)\s*\(", txt,
+                       flags=re.M)
+    return sorted(set(names))
+
+
+def test_header_declares_reference_surface():
+    names = header_functions()
+    for ref_name in ("LzmaProps_Decode", "LzmaDec_AllocateProbs", "LzmaDec_FreeProbs",
+                     "LzmaDec_Allocate", "LzmaDec_Free", "LzmaDec_Init", "LzmaDec_DecodeToDic",
+                     "LzmaDec_DecodeToBuf", "LzmaDecode", "LzmaUncompress",
+                     "Lzma2Dec_AllocateProbs", "Lzma2Dec_Allocate", "Lzma2Dec_Init",
+                     "Lzma2Dec_DecodeToDic", "Lzma2Dec_DecodeToBuf", "Lzma2Decode"):
+        assert ref_name in names
+
+
+def test_library_exports_every_declared_symbol():
+    out = subprocess.run(["nm", "-D", "--defined-only", LIB], capture_output=True, text=True,
+                         check=True).stdout
+    exported = {line.split()[-1] for line in out.splitlines() if " T " in line}
+    missing = [n for n in header_functions() if n not in exported]
+    assert not missing, missing
+    lib = ctypes.CDLL(LIB)
+    for n in header_functions():
+        assert hasattr(lib, n)
+
+
+def test_struct_layouts():
+    import lzmagpu as L
+    assert ctypes.sizeof(L.CLzmaDec) == 136
+    assert L.CLzmaDec.dicPos.offset == 48 and L.CLzmaDec.tempBuf.offset == 112
+    assert ctypes.sizeof(L.StreamDesc) == 48
+    assert ctypes.sizeof(L.Result) == 24
+
+
+def test_props_decode_host():
+    import lzmagpu as L
+    p = L.CLzmaProps()
+    assert L.lib.LzmaProps_Decode(ctypes.byref(p), b"\x5d\x00\x00\x01\x00", 5) == 0
+    assert (p.lc, p.lp, p.pb, p.dicSize) == (3, 0, 2, 65536)
+    assert L.lib.LzmaProps_Decode(ctypes.byref(p), b"\x00\x00\x01\x00\x00", 5) == 0
+    assert (p.lc, p.lp, p.pb, p.dicSize) == (0, 0, 0, 4096)
+    assert L.lib.LzmaProps_Decode(ctypes.byref(p), b"\xe1\x00\x00\x01\x00", 5) == 4
+    assert L.lib.LzmaProps_Decode(ctypes.byref(p), b"\x5d\x00\x00\x01", 4) == 4
+
+
+def test_no_device_fails_loudly():
+    import lzmagpu as L
+    if L.device_count() > 0:
+        pytest.skip("a HIP device is present")
+    res, st, dl, sl, out = L.LzmaDecode(b"\x00" * 32, b"\x5d\x00\x00\x01\x00", 100)
+    assert res == L.SZ_ERROR_FAIL and dl == 0
+    assert "no HIP device" in L.last_error()
+
+
+def test_lzma2_split_blocks_matches_reference_layout():
+    import lzmagpu as L
+    if not os.path.exists(native.REF_SO):
+        pytest.skip("reference build absent (fixture generation only)")
+    import importlib.util
+    spec = importlib.util.spec_from_file_location(
+        "mg", os.path.join(ROOT, "tests", "golden", "make_golden.py"))
+    mg = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mg)
+    data = native.gen("text", 5, 300000) + native.gen("random", 6, 70000)
+    prop, comp = mg.lzma2_multiblock(data, 100000, 1 << 16)
+    blocks = L.split_lzma2_blocks(comp)
+    assert len(blocks) == 4
+    assert [b[2] for b in blocks] == [100000, 100000, 100000, 70000]
+    assert blocks[0][0] == 0
+    for a, b in zip(blocks, blocks[1:]):
+        assert a[0] + a[1] == b[0]
+    assert blocks[-1][0] + blocks[-1][1] == len(comp) - 1  # trailing EOS byte
+    # each block decodes standalone with the reference to its slice
+    off = 0
+    for so, sl, u in blocks:
+        r = native.lzma2_decode(native.ref(), "ref", comp[so:so + sl], prop, u, 0)
+        assert r[0] == 0 and r[2] == u and r[3] == sl
+        assert r[4] == data[off:off + u]
+        off += u
+
+
+def test_plan_batch_workspace_and_order():
+    import lzmagpu as L
+    items = [dict(src_off=0, src_len=10, dst_off=0, dst_cap=c, props=p)
+             for c, p in ((100, b"\x5d\x00\x00\x01\x00"), (5000, b"\x00\x00\x10\x00\x00"),
+                          (300, b"\xe1\x00\x00\x01\x00"))]
+    descs = L.make_descs(items)
+    order = (ctypes.c_uint32 * 3)()
+    ws = L.plan(descs, order)
+    assert descs[0].probs_off == 0
+    assert descs[1].probs_off == (1846 + 768 * 8 + 7) // 8 * 8
+    assert ws == 2 * (descs[1].probs_off + (1846 + 768 + 7) // 8 * 8)
+    assert list(order) == [1, 2, 0]
