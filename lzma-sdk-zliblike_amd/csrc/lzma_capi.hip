@@ -366,7 +366,7 @@ SRes LzmaDec_DecodeToBuf(CLzmaDec* p, Byte* dest, SizeT* destLen, const Byte* sr
 SRes LzmaDecode(Byte* dest, SizeT* destLen, const Byte* src, SizeT* srcLen, const Byte* propData,
                 unsigned propSize, ELzmaFinishMode finishMode, ELzmaStatus* status,
                 ISzAlloc* alloc) {
-  const SizeT in_size = *srcLen;
+  const SizeT in_size = *srcLen, out_size = *destLen;
   *srcLen = 0;
   *destLen = 0;
   if (in_size < 5) return SZ_ERROR_INPUT_EOF;
@@ -377,12 +377,12 @@ SRes LzmaDecode(Byte* dest, SizeT* destLen, const Byte* src, SizeT* srcLen, cons
   // probability table through it and reports SZ_ERROR_MEM when that fails
   void* host_probs = alloc->Alloc(alloc, size_t(probs_for(np.lc, np.lp)) * sizeof(CLzmaProb));
   if (host_probs == nullptr) return SZ_ERROR_MEM;
-  SizeT sl = in_size;
+  SizeT sl = in_size, dl = out_size;
   int st = -1;
-  r = gpu_one_call(LZMA_GPU_KIND_LZMA, dest, destLen, src, &sl, propData, propSize, finishMode,
-                   &st);
+  r = gpu_one_call(LZMA_GPU_KIND_LZMA, dest, &dl, src, &sl, propData, propSize, finishMode, &st);
   alloc->Free(alloc, host_probs);
   *srcLen = sl;
+  *destLen = dl;
   if (st >= 0) *status = ELzmaStatus(st);
   return r;
 }
@@ -604,7 +604,7 @@ SRes Lzma2Dec_DecodeToBuf(CLzma2Dec* p, Byte* dest, SizeT* destLen, const Byte* 
 
 SRes Lzma2Decode(Byte* dest, SizeT* destLen, const Byte* src, SizeT* srcLen, Byte prop,
                  ELzmaFinishMode finishMode, ELzmaStatus* status, ISzAlloc* alloc) {
-  const SizeT in_size = *srcLen;
+  const SizeT in_size = *srcLen, out_size = *destLen;
   *destLen = 0;
   *srcLen = 0;
   *status = LZMA_STATUS_NOT_SPECIFIED;
@@ -613,11 +613,13 @@ SRes Lzma2Decode(Byte* dest, SizeT* destLen, const Byte* src, SizeT* srcLen, Byt
   if (r != SZ_OK) return r;
   void* host_probs = alloc->Alloc(alloc, size_t(probs_for(4, 0)) * sizeof(CLzmaProb));
   if (host_probs == nullptr) return SZ_ERROR_MEM;
-  SizeT sl = in_size;
+  SizeT sl = in_size, dl = out_size;
   int st = -1;
-  r = gpu_one_call(LZMA_GPU_KIND_LZMA2, dest, destLen, src, &sl, &prop, 1, finishMode, &st);
+  r = gpu_one_call(LZMA_GPU_KIND_LZMA2, dest, &dl, src, &sl, &prop, 1, finishMode, &st);
+  if (r == SZ_OK && st == LZMA_STATUS_NEEDS_MORE_INPUT) r = SZ_ERROR_INPUT_EOF;  // Lzma2Dec.c:350
   alloc->Free(alloc, host_probs);
   *srcLen = sl;
+  *destLen = dl;
   if (st >= 0) *status = ELzmaStatus(st);
   return r;
 }

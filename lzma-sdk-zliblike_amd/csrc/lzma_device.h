@@ -22,8 +22,19 @@
 // (lz_decode_to_dic); LZMA2 chunk walker Lzma2Dec.c:98-289 (lz2_*).
 #pragma once
 
-#include <hip/hip_runtime.h>
 #include <stdint.h>
+
+#ifdef LZGPU_HOST_EMU
+// Test-only host build of the per-lane logic (tests/emu): lets the CPU test
+// suite exercise exactly this code before it runs on the GPU.  Never part
+// of liblzmagpu.so.
+#include <stddef.h>
+#define __device__
+#define __host__
+#define __forceinline__ inline
+#else
+#include <hip/hip_runtime.h>
+#endif
 
 namespace lzgpu {
 
@@ -96,7 +107,7 @@ struct GlobalReader {
     if (avail == 0) {
       win = 0; nb = 0; pend = 0; wp = w; return;
     }
-    win = uint64_t(__builtin_nontemporal_load(w) >> (8 * skip));
+    win = uint64_t(*w >> (8 * skip));
     nb = 4 - skip;
     wp = w + 1;
     pend = (wp < wend) ? *wp : 0u;

@@ -1,0 +1,80 @@
+// lane_emu.cpp -- TEST INFRASTRUCTURE ONLY.
+//
+// Host build (-DLZGPU_HOST_EMU) of the exact per-lane code the HIP kernels run
+// (lzma-sdk-zliblike_amd/csrc/lzma_lane.h), so the CPU test-suite can check the
+// kernel logic against the golden vectors before any GPU run.  Not linked into
+// the product library; the product has no CPU decode path.
+#include <stdlib.h>
+#include <string.h>
+
+#include "../../lzma-sdk-zliblike_amd/csrc/lzma_lane.h"
+
+using namespace lzgpu;
+
+extern "C" {
+
+// Batch: the kernel body applied lane by lane (descs already planned).
+void emu_decode_batch(const LzmaGpuStreamDesc* descs, size_t n, const uint8_t* src, uint8_t* dst,
+                      uint16_t* ws, LzmaGpuResult* results) {
+  for (size_t i = 0; i < n; ++i) results[i] = lane_decode(descs[i], src, dst, ws);
+}
+
+// zlib-like DecodeToBuf loop driven through lane_session (the session
+// kernel's body), same contract as orc_lzma_stream_decode.
+int emu_stream_decode(const uint8_t* props, const uint8_t* src, size_t src_total, uint8_t* out,
+                      size_t out_total, size_t in_chunk, size_t out_chunk, int finish_mode,
+                      long long* trace, int max_calls, size_t* out_len, size_t* in_used) {
+  uint32_t lc, lp, pb, dict;
+  int r = lz_props_parse(props, 5, lc, lp, pb, dict);
+  if (r != kOk) { *out_len = 0; *in_used = 0; return -r; }
+  LzgpuSession q;
+  memset(&q, 0, sizeof q);
+  q.lc = lc; q.lp = lp; q.pb = pb; q.dict_size = dict;
+  q.probs = (uint16_t*)malloc(size_t(num_probs(lc, lp)) * 2);
+  q.dic = (uint8_t*)malloc(dict);
+  q.cap = dict;
+  q.pos = 0;
+  q.need_rc_init = 1; q.need_state_init = 1; q.pending = 0; q.tmp_n = 0;
+  size_t in_pos = 0, out_pos = 0;
+  int calls = 0;
+  while (calls < max_calls) {
+    size_t sl = src_total - in_pos, dl = out_total - out_pos;
+    if (sl > in_chunk) sl = in_chunk;
+    if (dl > out_chunk) dl = out_chunk;
+    // ---- LzmaDec_DecodeToBuf (LzmaDec.c:840-878) over lane_session
+    size_t out_left = dl, in_left = sl, got_in = 0, got_out = 0;
+    const uint8_t* s = src + in_pos;
+    uint8_t* d = out + out_pos;
+    int res = 0, st = -1;
+    for (;;) {
+      if (q.pos == q.cap) q.pos = 0;
+      uint64_t start = q.pos, lim;
+      int fin;
+      if (out_left > q.cap - start) { lim = q.cap; fin = 0; } else { lim = start + out_left; fin = finish_mode; }
+      q.in = s; q.in_len = in_left; q.dic_limit = lim; q.finish_mode = fin;
+      lane_session(q);
+      res = q.res; st = q.status;
+      s += q.in_used; in_left -= q.in_used; got_in += q.in_used;
+      size_t produced = q.pos - start;
+      memcpy(d, q.dic + start, produced);
+      d += produced; out_left -= produced; got_out += produced;
+      if (res != 0) break;
+      if (produced == 0 || out_left == 0) break;
+    }
+    trace[4 * calls + 0] = res;
+    trace[4 * calls + 1] = st;
+    trace[4 * calls + 2] = (long long)got_in;
+    trace[4 * calls + 3] = (long long)got_out;
+    calls++;
+    in_pos += got_in;
+    out_pos += got_out;
+    if (res != 0 || st == 1 || out_pos == out_total || (got_in == 0 && got_out == 0)) break;
+  }
+  free(q.probs);
+  free(q.dic);
+  *out_len = out_pos;
+  *in_used = in_pos;
+  return calls;
+}
+
+}  // extern "C"

@@ -108,7 +108,9 @@ def test_golden_lzma2_one_call(L):
         # Lzma2Decode reports NOT_SPECIFIED (0) where the 7zDec-pattern oracle
         # leaves status untouched (-1) on an unsupported prop byte.
         exp_st = 0 if e["status"] == -1 else e["status"]
-        if (res, st, dl, sl) != (e["res"], exp_st, e["dest_len"], e["src_len"]) or \
+        # ... and maps an OK/NEEDS_MORE_INPUT ending to SZ_ERROR_INPUT_EOF (Lzma2Dec.c:350-351)
+        exp_res = 6 if (e["res"] == 0 and e["status"] == 3) else e["res"]
+        if (res, st, dl, sl) != (exp_res, exp_st, e["dest_len"], e["src_len"]) or \
                 G.sha(out) != e["sha256"]:
             bad.append((i, c["note"], (res, st, dl, sl), _expect(c)))
     assert not bad, bad[:10]
