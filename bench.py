@@ -153,19 +153,20 @@ def main():
     cpus = os.cpu_count() or 8
     workers = max(1, min(16, cpus // max(1, world)))
 
+    count, n, lc, lp, pb, dsz, desc_txt = CONFIGS[args.config]
+    # workload first: the compression pool forks before this process touches the GPU
+    plain, comp, lens, props = build_workload(args.config, rank, workers)
+
     import torch
     import torch.distributed as dist
     torch.cuda.set_device(local_rank)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     import lzmagpu as L  # after torch: shares torch's HIP runtime
-
-    count, n, lc, lp, pb, dsz, desc_txt = CONFIGS[args.config]
-    plain, comp, lens, props = build_workload(args.config, rank, workers)
     descs, order, ws_bytes, offs = make_descs(lens, n, props)
     comp_bytes = int(lens.sum())
     dev = torch.device("cuda", local_rank)
-    d_src = torch.from_numpy(comp).to(dev)
+    d_src = torch.from_numpy(np.ascontiguousarray(comp).copy()).to(dev)
     d_dst = torch.empty(count * n, dtype=torch.uint8, device=dev)
     d_ws = torch.empty(max(ws_bytes, 16), dtype=torch.uint8, device=dev)
     d_desc = torch.frombuffer(bytearray(descs), dtype=torch.uint8).to(dev)

@@ -20,12 +20,13 @@
  *       LzmaDec_DecodeToBuf     replaces LzmaDec.h:198-199 / LzmaDec.c:840-878
  *       LzmaDecode              replaces LzmaDec.h:223-225 / LzmaDec.c:972-1002
  *       LzmaUncompress          replaces LzmaLib.h:128-129 / LzmaLib.c:41-46
- *       Lzma2Dec_AllocateProbs  replaces Lzma2Dec.h:31 / Lzma2Dec.c:73-78
- *       Lzma2Dec_Allocate       replaces Lzma2Dec.h:32 / Lzma2Dec.c:80-85
- *       Lzma2Dec_Init           replaces Lzma2Dec.h:33 / Lzma2Dec.c:87-94
- *       Lzma2Dec_DecodeToDic    replaces Lzma2Dec.h:50-51 / Lzma2Dec.c:170-289
- *       Lzma2Dec_DecodeToBuf    replaces Lzma2Dec.h:53-54 / Lzma2Dec.c:291-328
- *       Lzma2Decode             replaces Lzma2Dec.h:76-77 / Lzma2Dec.c:330-356
+ *       Lzma2Dec_AllocateProbs  replaces Lzma2Dec.h:31 / Lzma2Dec.c:75-80
+ *       Lzma2Dec_Allocate       replaces Lzma2Dec.h:32 / Lzma2Dec.c:82-87
+ *       Lzma2Dec_Init           replaces Lzma2Dec.h:33 / Lzma2Dec.c:89-96
+ *       Lzma2Dec_DecodeToDic    replaces Lzma2Dec.h:51-52 / Lzma2Dec.c:170-289
+ *       Lzma2Dec_DecodeToBuf    replaces Lzma2Dec.h:54-55 / Lzma2Dec.c:291-328
+ *       Lzma2Decode             replaces Lzma2Dec.h:77-78 / Lzma2Dec.c:330-356
+ *       LzmaDec_InitDicAndState exported like LzmaDec.c:685 (declared by Lzma2Dec.c:168)
  *
  *     Documented differences: no stdout print in LzmaDec_AllocateProbs (the
  *     fork's LzmaDec.c:945 debug printf); Lzma2Decode initialises its state
