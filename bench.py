@@ -112,9 +112,8 @@ def make_descs(lens, n, props, finish=1):
     arr[:, 45] = 5
     arr[:, 46] = finish
     arr[:, 47] = L.KIND_LZMA
-    order = (ctypes.c_uint32 * count)()
-    ws = L.plan(descs, order)
-    return descs, order, ws, offs
+    plan, order = L.plan_ex(descs)
+    return descs, order, plan, offs
 
 
 def cpu_baseline(comp, lens, offs, n, props, threads, sample_streams):
@@ -163,7 +162,8 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     import lzmagpu as L  # after torch: shares torch's HIP runtime
-    descs, order, ws_bytes, offs = make_descs(lens, n, props)
+    descs, order, plan, offs = make_descs(lens, n, props)
+    ws_bytes = int(plan.workspace_bytes)
     comp_bytes = int(lens.sum())
     dev = torch.device("cuda", local_rank)
     d_src = torch.from_numpy(np.ascontiguousarray(comp).copy()).to(dev)
@@ -176,8 +176,8 @@ def main():
     sh = stream.cuda_stream
 
     def step():
-        r = L.decode_batch_device(d_desc.data_ptr(), d_order.data_ptr(), count, d_src.data_ptr(),
-                                  d_dst.data_ptr(), d_ws.data_ptr(), ws_bytes, d_res.data_ptr(), sh)
+        r = L.decode_batch_device_ex(plan, d_desc.data_ptr(), d_order.data_ptr(), d_src.data_ptr(),
+                                     d_dst.data_ptr(), d_ws.data_ptr(), d_res.data_ptr(), sh)
         if r != 0:
             raise RuntimeError("LzmaGpu_DecodeBatch failed: " + L.last_error())
 
@@ -255,10 +255,16 @@ def main():
             "config": {"workload": desc_txt, "streams_per_gpu": count, "stream_bytes": n,
                        "props": props.hex(), "compressed_bytes_per_gpu": comp_bytes,
                        "ratio": round(comp_bytes / (count * n), 4),
-                       "parallelism": f"{world} rank(s), streams sharded, no data-path collective"},
+                       "parallelism": f"{world} rank(s), streams sharded, no data-path collective",
+                       "kernel_plan": {"lds_streams": int(plan.n_lds),
+                                       "streams_per_workgroup": int(plan.lanes_per_group),
+                                       "lds_bytes_per_stream": int(plan.lds_cells_per_lane) * 2,
+                                       "workgroups_per_cu": int(plan.groups_per_cu)}},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
-                         "traffic": traffic, "kernel": "lzgpu_decode_batch_kernel",
+                         "traffic": traffic,
+                         "kernel": "lzgpu_decode_lds_kernel" if plan.n_lds else
+                                   "lzgpu_decode_batch_kernel",
                          "kernel_avg_ms": round(avg_kern_ms, 4),
                          "alg_bytes_per_launch": alg_bytes},
             "cpu_baseline": cpu,

@@ -210,7 +210,31 @@ typedef struct LzmaGpuResult {
  * workspace size in bytes (0 for n == 0). */
 size_t LzmaGpu_PlanBatch(LzmaGpuStreamDesc *descs, size_t n, uint32_t *order);
 
-/* Decode n streams on the current HIP device.  All pointers are device
+/* Launch plan for LzmaGpu_DecodeBatchEx (filled by LzmaGpu_PlanBatchEx).
+ * The lane order is partitioned: order[0, n_lds) runs on the LDS kernel
+ * (per-stream probability tables in LDS, lanes_per_group streams per
+ * workgroup, lds_cells_per_lane cells each); order[n_lds, n) runs on the
+ * generic kernel (tables in the global workspace: LZMA2 ranges, lc+lp too
+ * wide for LDS).  Environment overrides for experiments:
+ * LZGPU_KERNEL=global|lds, LZGPU_LANES=<streams per workgroup>. */
+typedef struct LzmaGpuPlan {
+  uint64_t workspace_bytes;
+  uint64_t n;
+  uint64_t n_lds;
+  uint32_t lanes_per_group;
+  uint32_t lds_cells_per_lane;
+  uint32_t groups_per_cu;
+  uint32_t reserved[9];
+} LzmaGpuPlan;
+
+SRes LzmaGpu_PlanBatchEx(LzmaGpuStreamDesc *descs, size_t n, uint32_t *order, LzmaGpuPlan *plan);
+
+/* Decode a planned batch (order is required: the plan's lane partition). */
+SRes LzmaGpu_DecodeBatchEx(const LzmaGpuPlan *plan, const LzmaGpuStreamDesc *d_descs,
+                           const uint32_t *d_order, const Byte *d_src, Byte *d_dst,
+                           void *d_workspace, LzmaGpuResult *d_results, void *stream);
+
+/* Decode n streams on the current HIP device (generic kernel, any plan).  All pointers are device
  * memory owned by the caller; d_order may be NULL (identity).  Asynchronous
  * on `stream` (a hipStream_t; NULL = default stream).  Returns SZ_OK if the
  * launch was queued; per-stream outcomes land in d_results. */

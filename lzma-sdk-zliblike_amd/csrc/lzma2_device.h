@@ -16,8 +16,9 @@ enum : int {
   C2_FINISHED, C2_ERROR
 };
 
-struct Lz2State {
-  LzState dec;
+template <class Lo>
+struct Lz2StateT {
+  LzStateT<Lo> dec;
   uint32_t pack_left, unpack_left;
   int phase;
   uint32_t control;
@@ -27,7 +28,8 @@ struct Lz2State {
 __device__ __forceinline__ bool c2_is_copy(uint32_t c) { return (c & 0x80u) == 0; }
 __device__ __forceinline__ uint32_t c2_mode(uint32_t c) { return (c >> 5) & 3u; }
 
-__device__ inline int lz2_header_byte(Lz2State& p, uint32_t b) {
+template <class Lo>
+__device__ inline int lz2_header_byte(Lz2StateT<Lo>& p, uint32_t b) {
   switch (p.phase) {
     case C2_CONTROL:
       p.control = b;
@@ -71,7 +73,8 @@ __device__ inline int lz2_header_byte(Lz2State& p, uint32_t b) {
 }
 
 // Lzma2Dec_DecodeToDic for one lane (src in global memory).
-__device__ __forceinline__ int lz2_decode_to_dic(Lz2State& p, uint64_t dic_limit,
+template <class Lo>
+__device__ __forceinline__ int lz2_decode_to_dic(Lz2StateT<Lo>& p, uint64_t dic_limit,
                                                  const uint8_t* src, uint64_t& src_len, int fin,
                                                  int& status) {
   const uint64_t in_size = src_len;
@@ -129,7 +132,9 @@ __device__ __forceinline__ int lz2_decode_to_dic(Lz2State& p, uint64_t dic_limit
         p.phase = C2_DATA_CONT;
       }
       if (in_cur > p.pack_left) in_cur = p.pack_left;
-      int res = lz_decode_to_dic(p.dec, pos0 + out_cur, src, in_cur, cur_fin, status);
+      // each chunk is one DecodeToDic call over all of its bytes: the
+      // tempBuf continuation path is never taken (as in a one-call decode)
+      int res = lz_decode_to_dic<false>(p.dec, pos0 + out_cur, src, in_cur, cur_fin, status);
       src += in_cur;
       src_len += in_cur;
       p.pack_left -= uint32_t(in_cur);
@@ -150,15 +155,18 @@ __device__ __forceinline__ int lz2_decode_to_dic(Lz2State& p, uint64_t dic_limit
 
 // Lzma2Dec_Init (Lzma2Dec.c:90-97) after Lzma2Dec_AllocateProbs(prop):
 // lc = 4, lp = 0, pb = 0 for the allocation; dictionary size from the prop.
-__device__ __forceinline__ int lz2_init(Lz2State& p, uint32_t prop, uint16_t* probs, uint8_t* dic,
-                                        uint64_t cap) {
+// lo must hold lo_cells(4, 0, 4) cells (the largest an LZMA2 chunk can ask for).
+template <class Lo>
+__device__ __forceinline__ int lz2_init(Lz2StateT<Lo>& p, uint32_t prop, Lo lo, uint16_t* hi,
+                                        uint8_t* dic, uint64_t cap) {
   if (prop > 40) return kErrUnsupported;
   uint32_t dict = (prop == 40) ? 0xFFFFFFFFu : ((2u | (prop & 1u)) << (prop / 2 + 11));
   p.dec.lc = 4;
   p.dec.lp = 0;
   p.dec.pb = 0;
   p.dec.dict_size = dict < 4096 ? 4096 : dict;
-  p.dec.probs = probs;
+  p.dec.lo = lo;
+  p.dec.hi = hi;
   p.dec.dic = dic;
   p.dec.cap = cap;
   p.dec.pos = 0;

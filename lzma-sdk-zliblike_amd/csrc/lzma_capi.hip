@@ -12,6 +12,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <numeric>
 #include <string>
@@ -90,6 +91,11 @@ Scratch& scratch() {
 
 uint32_t probs_for(uint32_t lc, uint32_t lp) { return lzgpu::num_probs(lc, lp); }
 
+int env_int(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return (v && *v) ? atoi(v) : dflt;
+}
+
 // Run one DecodeToDic on the GPU over a host-resident CLzmaDec.
 SRes gpu_decode_to_dic(CLzmaDec* p, SizeT dicLimit, const Byte* src, SizeT* srcLen,
                        ELzmaFinishMode finishMode, ELzmaStatus* status) {
@@ -102,7 +108,9 @@ SRes gpu_decode_to_dic(CLzmaDec* p, SizeT dicLimit, const Byte* src, SizeT* srcL
     return SZ_ERROR_PARAM;
   }
   Scratch& sc = scratch();
-  const uint32_t nprobs = probs_for(p->prop.lc, p->prop.lp);
+  // compact device layout (lzma_device.h): lo + hi for the current lc/lp/pb,
+  // never more than the numProbs cells LzmaDec_AllocateProbs allocated
+  const uint32_t nprobs = lzgpu::table_cells(p->prop.lc, p->prop.lp, p->prop.pb);
   void* d_probs = sc.probs.get(size_t(nprobs) * 2);
   void* d_dic = sc.dic.get(p->dicBufSize);
   void* d_src = sc.src.get(in_size);
@@ -626,33 +634,112 @@ SRes Lzma2Decode(Byte* dest, SizeT* destLen, const Byte* src, SizeT* srcLen, Byt
 
 // ------------------------------------------------------------------ batch extension
 
-size_t LzmaGpu_PlanBatch(LzmaGpuStreamDesc* descs, size_t n, uint32_t* order) {
+// Workspace: each item gets a 16-byte aligned slice of table_cells() cells
+// (LZMA2 ranges: the lc+lp=4, pb=4 maximum).  Returns per-item lo-table
+// widths (0 = not LDS-eligible) through lo_w when given.
+static uint64_t plan_workspace(LzmaGpuStreamDesc* descs, size_t n, std::vector<uint32_t>* lo_w) {
   uint64_t off = 0;
-  std::vector<uint32_t> width(n);
+  if (lo_w) lo_w->assign(n, 0);
   for (size_t i = 0; i < n; ++i) {
     LzmaGpuStreamDesc& d = descs[i];
     uint32_t np = 0;
     if (d.kind == LZMA_GPU_KIND_LZMA2) {
-      np = probs_for(4, 0);
+      np = lzgpu::table_cells(4, 0, 4);
     } else {
       uint32_t lc, lp, pb, dict;
-      if (lzgpu::lz_props_parse(d.props, d.props_size, lc, lp, pb, dict) == SZ_OK)
-        np = probs_for(lc, lp);
+      if (lzgpu::lz_props_parse(d.props, d.props_size, lc, lp, pb, dict) == SZ_OK) {
+        np = lzgpu::table_cells(lc, lp, pb);
+        if (lo_w) (*lo_w)[i] = lzgpu::lo_cells(lc, lp, pb);
+      }
     }
-    width[i] = np;
     d.probs_off = off;
     off += (uint64_t(np) + 7) & ~uint64_t(7);
   }
+  return off * 2;
+}
+
+size_t LzmaGpu_PlanBatch(LzmaGpuStreamDesc* descs, size_t n, uint32_t* order) {
+  std::vector<uint32_t> w;
+  const uint64_t bytes = plan_workspace(descs, n, &w);
   if (order) {
     std::vector<uint32_t> idx(n);
     std::iota(idx.begin(), idx.end(), 0u);
     std::stable_sort(idx.begin(), idx.end(), [&](uint32_t a, uint32_t b) {
       if (descs[a].dst_cap != descs[b].dst_cap) return descs[a].dst_cap > descs[b].dst_cap;
-      return width[a] > width[b];
+      return w[a] > w[b];
     });
     for (size_t i = 0; i < n; ++i) order[i] = idx[i];
   }
-  return size_t(off) * 2;
+  return size_t(bytes);
+}
+
+SRes LzmaGpu_PlanBatchEx(LzmaGpuStreamDesc* descs, size_t n, uint32_t* order,
+                         LzmaGpuPlan* plan) {
+  if (!order || !plan) return SZ_ERROR_PARAM;
+  memset(plan, 0, sizeof *plan);
+  std::vector<uint32_t> w;
+  plan->workspace_bytes = plan_workspace(descs, n, &w);
+  plan->n = n;
+  // LDS-eligible: lo table <= 16384 cells (32 KiB, >= 5 streams per CU)
+  const uint32_t kMaxLdsCells = 16384;
+  const int force = env_int("LZGPU_KERNEL_GLOBAL", 0);
+  const char* kv = getenv("LZGPU_KERNEL");
+  const bool global_only = force || (kv && strcmp(kv, "global") == 0);
+  uint32_t stride = 0;
+  std::vector<uint32_t> lds_idx, glob_idx;
+  for (size_t i = 0; i < n; ++i) {
+    if (!global_only && w[i] != 0 && w[i] <= kMaxLdsCells) {
+      lds_idx.push_back(uint32_t(i));
+      stride = std::max(stride, w[i]);
+    } else {
+      glob_idx.push_back(uint32_t(i));
+    }
+  }
+  auto by_len = [&](uint32_t a, uint32_t b) {
+    if (descs[a].dst_cap != descs[b].dst_cap) return descs[a].dst_cap > descs[b].dst_cap;
+    return w[a] > w[b];
+  };
+  std::stable_sort(lds_idx.begin(), lds_idx.end(), by_len);
+  std::stable_sort(glob_idx.begin(), glob_idx.end(), by_len);
+  size_t k = 0;
+  for (uint32_t i : lds_idx) order[k++] = i;
+  for (uint32_t i : glob_idx) order[k++] = i;
+  plan->n_lds = lds_idx.size();
+  if (plan->n_lds) {
+    stride = (stride + 3) & ~3u;  // 8-byte aligned per-lane slices
+    const uint32_t lds_per_cu = 160 * 1024;
+    const uint32_t per_cu = std::max<uint32_t>(1, lds_per_cu / (stride * 2));
+    uint32_t lanes = 1;
+    while (lanes * 2 <= 64 && lanes * 2 * 4 <= per_cu) lanes *= 2;  // ~4 groups per CU
+    const int over = env_int("LZGPU_LANES", 0);
+    if (over > 0 && over <= 64 && uint32_t(over) * stride * 2 <= lds_per_cu) lanes = uint32_t(over);
+    plan->lanes_per_group = lanes;
+    plan->lds_cells_per_lane = stride;
+    plan->groups_per_cu = lds_per_cu / (lanes * stride * 2);
+  }
+  return SZ_OK;
+}
+
+SRes LzmaGpu_DecodeBatchEx(const LzmaGpuPlan* plan, const LzmaGpuStreamDesc* d_descs,
+                           const uint32_t* d_order, const Byte* d_src, Byte* d_dst,
+                           void* d_workspace, LzmaGpuResult* d_results, void* stream) {
+  if (!ensure_device()) return SZ_ERROR_FAIL;
+  if (!plan || !d_order || plan->n > 0xFFFFFFFFull || plan->n_lds > plan->n) return SZ_ERROR_PARAM;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  uint16_t* ws = static_cast<uint16_t*>(d_workspace);
+  const uint32_t n_lds = uint32_t(plan->n_lds), n_glob = uint32_t(plan->n - plan->n_lds);
+  if (n_lds && lzgpu_launch_decode_lds(d_descs, d_order, n_lds, d_src, d_dst, ws, d_results,
+                                       plan->lanes_per_group, plan->lds_cells_per_lane,
+                                       st) != 0) {
+    set_error("LDS decode kernel launch failed");
+    return SZ_ERROR_FAIL;
+  }
+  if (n_glob && lzgpu_launch_decode_batch(d_descs, d_order + n_lds, n_glob, d_src, d_dst, ws,
+                                          d_results, st) != 0) {
+    set_error("generic decode kernel launch failed");
+    return SZ_ERROR_FAIL;
+  }
+  return SZ_OK;
 }
 
 SRes LzmaGpu_DecodeBatch(const LzmaGpuStreamDesc* d_descs, const uint32_t* d_order, size_t n,
@@ -677,7 +764,9 @@ SRes LzmaGpu_DecodeBatchHost(const LzmaGpuStreamDesc* descs, size_t n, const Byt
   if (n == 0) return SZ_OK;
   std::vector<LzmaGpuStreamDesc> d(descs, descs + n);
   std::vector<uint32_t> order(n);
-  const size_t ws = LzmaGpu_PlanBatch(d.data(), n, order.data());
+  LzmaGpuPlan plan;
+  LzmaGpu_PlanBatchEx(d.data(), n, order.data(), &plan);
+  const size_t ws = size_t(plan.workspace_bytes);
   void *d_src = nullptr, *d_dst = nullptr, *d_ws = nullptr, *d_desc = nullptr, *d_order = nullptr,
        *d_res = nullptr;
   SRes r = SZ_ERROR_MEM;
@@ -697,10 +786,10 @@ SRes LzmaGpu_DecodeBatchHost(const LzmaGpuStreamDesc* descs, size_t n, const Byt
     if (!hip_ok(hipMemcpy(d_order, order.data(), n * sizeof(uint32_t), hipMemcpyHostToDevice),
                 "H2D order"))
       break;
-    if (LzmaGpu_DecodeBatch(static_cast<LzmaGpuStreamDesc*>(d_desc),
-                            static_cast<uint32_t*>(d_order), n, static_cast<Byte*>(d_src),
-                            static_cast<Byte*>(d_dst), d_ws, ws,
-                            static_cast<LzmaGpuResult*>(d_res), nullptr) != SZ_OK)
+    if (LzmaGpu_DecodeBatchEx(&plan, static_cast<LzmaGpuStreamDesc*>(d_desc),
+                              static_cast<uint32_t*>(d_order), static_cast<Byte*>(d_src),
+                              static_cast<Byte*>(d_dst), d_ws, static_cast<LzmaGpuResult*>(d_res),
+                              nullptr) != SZ_OK)
       break;
     if (!hip_ok(hipDeviceSynchronize(), "decode kernel")) break;
     if (!hip_ok(hipMemcpy(results, d_res, n * sizeof(LzmaGpuResult), hipMemcpyDeviceToHost),

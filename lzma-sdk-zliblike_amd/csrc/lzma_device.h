@@ -7,19 +7,26 @@
 // tail passes behind a dry-run look-ahead, the dictionary-size split -- are
 // reproduced exactly, including truncated and corrupt streams.
 //
-// Memory layout per lane (all device memory):
-//   probs  : CLzmaProb[1846 + 0x300 << (lc+lp)] in the LZMA-format order
-//            (offsets below), 16-bit cells;
-//   dic    : the caller's output window, which IS the dictionary (as in
-//            LzmaDecode, LzmaDec.c:988-989) or a ring of dicBufSize bytes;
-//   input  : the compressed bytes, read through a register window refilled
-//            with aligned 4-byte loads one word ahead, so NORMALIZE does not
-//            wait on memory.
+// Probability tables use a compact, pb-dependent layout (the reference's
+// layout is not observable): IsMatch / IsRep0Long / LenLow / LenMid are sized
+// by the posStates actually reachable (1 << pb) instead of always 16.  The
+// table splits into
+//   lo : everything except the two 256-entry LenHigh trees -- the hot part,
+//        kept in LDS by the fast kernel (ProbLo = LDS pointer) or in global
+//        memory by the generic kernels (ProbLo = global pointer);
+//   hi : the LenHigh trees (lengths >= 18, rare), always in global memory.
+// lc=0/lp=0/pb=0: lo = 1262 cells (2,524 B), so 16 streams share a 40 KiB
+// LDS slab and four such workgroups fill a CU.
+//
+// Other per-lane memory: dic = the caller's output window, which IS the
+// dictionary (LzmaDecode, LzmaDec.c:988-989) or a ring of dicBufSize bytes;
+// input = the compressed bytes, read through a register window refilled with
+// aligned 4-byte loads one word ahead so NORMALIZE does not wait on memory.
 //
 // Reference map: bit/tree/direct-bit primitives LzmaDec.c:8-45,323-344;
 // symbol loop :131-426 (lz_run); pending flush :428-452; dictionary split
 // :454-477 (lz_run_split); look-ahead :487-675 (lz_probe); driver :719-838
-// (lz_decode_to_dic); LZMA2 chunk walker Lzma2Dec.c:98-289 (lz2_*).
+// (lz_decode_to_dic); LZMA2 chunk walker Lzma2Dec.c:98-289 (lzma2_device.h).
 #pragma once
 
 #include <stdint.h>
@@ -48,22 +55,54 @@ constexpr uint32_t kProbInit = 1024u;
 constexpr uint32_t kLookahead = 20u;  // LZMA_REQUIRED_INPUT_MAX
 constexpr uint32_t kLenDone = 274u;   // kMatchSpecLenStart
 
-// LZMA-format probability layout (16-bit cells).
-enum : uint32_t {
-  P_IS_MATCH = 0, P_IS_REP = 192, P_IS_REP_G0 = 204, P_IS_REP_G1 = 216, P_IS_REP_G2 = 228,
-  P_IS_REP0_LONG = 240, P_POS_SLOT = 432, P_SPEC_POS = 688, P_ALIGN = 802, P_LEN = 818,
-  P_REP_LEN = 1332, P_LITERAL = 1846
-};
-enum : uint32_t { L_CHOICE = 0, L_CHOICE2 = 1, L_LOW = 2, L_MID = 130, L_HIGH = 258 };
+// ------------------------------------------------------------------ compact layout
 
+// Section offsets (in 16-bit cells) of the lo table for posState count P = 1 << pb:
+//   IsMatch[12P] | IsRep0Long[12P] | IsRep[12] IsRepG0[12] IsRepG1[12] IsRepG2[12] |
+//   PosSlot[4][64] | SpecPos[114] | Align[16] | Len{choice,choice2,low[P][8],mid[P][8]} |
+//   RepLen{same} | Literal[0x300 << (lc+lp)]
+// hi table: LenHigh[256] | RepLenHigh[256].
+__host__ __device__ __forceinline__ uint32_t off_rep0long(uint32_t pb) { return 12u << pb; }
+__host__ __device__ __forceinline__ uint32_t off_is_rep(uint32_t pb) { return 24u << pb; }
+__host__ __device__ __forceinline__ uint32_t off_slot(uint32_t pb) { return (24u << pb) + 48u; }
+__host__ __device__ __forceinline__ uint32_t off_spec(uint32_t pb) { return (24u << pb) + 304u; }
+__host__ __device__ __forceinline__ uint32_t off_align(uint32_t pb) { return (24u << pb) + 418u; }
+__host__ __device__ __forceinline__ uint32_t off_len(uint32_t pb) { return (24u << pb) + 434u; }
+__host__ __device__ __forceinline__ uint32_t len_coder_cells(uint32_t pb) { return 2u + (16u << pb); }
+__host__ __device__ __forceinline__ uint32_t off_replen(uint32_t pb) {
+  return off_len(pb) + len_coder_cells(pb);
+}
+__host__ __device__ __forceinline__ uint32_t off_lit(uint32_t pb) {
+  return off_len(pb) + 2u * len_coder_cells(pb);
+}
+__host__ __device__ __forceinline__ uint32_t lo_cells(uint32_t lc, uint32_t lp, uint32_t pb) {
+  return off_lit(pb) + (768u << (lc + lp));
+}
+constexpr uint32_t kHiCells = 512u;
+__host__ __device__ __forceinline__ uint32_t table_cells(uint32_t lc, uint32_t lp, uint32_t pb) {
+  return lo_cells(lc, lp, pb) + kHiCells;
+}
+// reference numProbs (LzmaDec.c:110): what LzmaDec_AllocateProbs allocates;
+// table_cells() <= num_probs() for every pb <= 4.
 __host__ __device__ inline uint32_t num_probs(uint32_t lc, uint32_t lp) {
   return 1846u + (768u << (lc + lp));
 }
 
-// Per-lane decoder state (CLzmaDec fields, LzmaDec.h:50-69).
-struct LzState {
+#ifdef LZGPU_HOST_EMU
+typedef uint16_t lds_u16;
+typedef uint32_t lds_u32;
+#else
+typedef __attribute__((address_space(3))) uint16_t lds_u16;
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+#endif
+
+// Per-lane decoder state (CLzmaDec fields, LzmaDec.h:50-69).  Lo = pointer type
+// of the lo table (uint16_t* global, or lds_u16* for LDS).
+template <class Lo>
+struct LzStateT {
   uint32_t lc, lp, pb, dict_size;
-  uint16_t* probs;
+  Lo lo;
+  uint16_t* hi;
   uint8_t* dic;
   uint64_t cap;   // dicBufSize
   uint64_t pos;   // dicPos
@@ -136,7 +175,7 @@ struct LocalReader {
   __device__ __forceinline__ uint32_t next() { return p[idx++]; }
 };
 
-// ------------------------------------------------------------------ symbol loop
+// ------------------------------------------------------------------ range decoder
 
 template <class Rd>
 struct Rc {
@@ -148,7 +187,9 @@ struct Rc {
       code = (code << 8) | rd->next();
     }
   }
-  __device__ __forceinline__ uint32_t bit(uint16_t* prob) {
+  // one adaptive decision on *prob (any address space)
+  template <class P>
+  __device__ __forceinline__ uint32_t bit(P prob) {
     uint32_t p = *prob;
     norm();
     uint32_t bound = (range >> 11) * p;
@@ -162,7 +203,8 @@ struct Rc {
     *prob = uint16_t(p - (p >> 5));
     return 1;
   }
-  __device__ __forceinline__ uint32_t tree(uint16_t* probs, uint32_t bits) {
+  template <class P>
+  __device__ __forceinline__ uint32_t tree(P probs, uint32_t bits) {
     uint32_t m = 1, lim = 1u << bits;
     while (m < lim) m = (m << 1) | bit(probs + m);
     return m - lim;
@@ -212,16 +254,24 @@ __device__ __forceinline__ uint32_t lz_copy(uint8_t* dic, uint64_t pos, uint64_t
   return last;
 }
 
+// ------------------------------------------------------------------ symbol loop
+
 // Decode symbols until pos reaches `limit` or the reader index reaches
 // `in_limit` (checked after each whole symbol; the first is always decoded).
 // State is written back only on success, as LzmaDec_DecodeReal does.
-template <class Rd>
-__device__ int lz_run(LzState& s, uint64_t limit, Rd& rd, uint32_t in_limit) {
-  uint16_t* __restrict__ pr = s.probs;
+template <class Lo, class Rd>
+__device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
+                                      uint32_t in_limit) {
+  const Lo pr = s.lo;
+  uint16_t* const hi = s.hi;
+  const uint32_t pb = s.pb;
   uint32_t st = s.st;
   uint32_t r0 = s.rep0, r1 = s.rep1, r2 = s.rep2, r3 = s.rep3;
-  const uint32_t pb_mask = (1u << s.pb) - 1, lp_mask = (1u << s.lp) - 1;
+  const uint32_t pb_mask = (1u << pb) - 1, lp_mask = (1u << s.lp) - 1;
   const uint32_t lc = s.lc;
+  const uint32_t o_rep0long = off_rep0long(pb), o_is_rep = off_is_rep(pb);
+  const uint32_t o_slot = off_slot(pb), o_spec = off_spec(pb), o_align = off_align(pb);
+  const uint32_t o_len = off_len(pb), o_replen = off_replen(pb), o_lit = off_lit(pb);
   uint8_t* __restrict__ dic = s.dic;
   const uint64_t cap = s.cap;
   uint64_t pos = s.pos;
@@ -235,9 +285,9 @@ __device__ int lz_run(LzState& s, uint64_t limit, Rd& rd, uint32_t in_limit) {
 
   do {
     const uint32_t ps = total & pb_mask;
-    uint32_t lcoder;
-    if (!rc.bit(pr + P_IS_MATCH + (st << 4) + ps)) {
-      uint16_t* lit = pr + P_LITERAL;
+    uint32_t lcoder, hcoder;
+    if (!rc.bit(pr + (st << pb) + ps)) {
+      Lo lit = pr + o_lit;
       uint32_t sym = 1;
       if (full != 0 || total != 0)
         lit += 768u * (((total & lp_mask) << lc) + (prev >> (8 - lc)));
@@ -261,13 +311,14 @@ __device__ int lz_run(LzState& s, uint64_t limit, Rd& rd, uint32_t in_limit) {
       total++;
       continue;
     }
-    if (!rc.bit(pr + P_IS_REP + st)) {
+    if (!rc.bit(pr + o_is_rep + st)) {
       st += 12;
-      lcoder = P_LEN;
+      lcoder = o_len;
+      hcoder = 0;
     } else {
       if (full == 0 && total == 0) return kErrData;
-      if (!rc.bit(pr + P_IS_REP_G0 + st)) {
-        if (!rc.bit(pr + P_IS_REP0_LONG + (st << 4) + ps)) {
+      if (!rc.bit(pr + o_is_rep + 12 + st)) {
+        if (!rc.bit(pr + o_rep0long + (st << pb) + ps)) {
           prev = dic[ring_back(pos, r0, cap)];
           dic[pos++] = uint8_t(prev);
           total++;
@@ -276,10 +327,10 @@ __device__ int lz_run(LzState& s, uint64_t limit, Rd& rd, uint32_t in_limit) {
         }
       } else {
         uint32_t dist;
-        if (!rc.bit(pr + P_IS_REP_G1 + st)) {
+        if (!rc.bit(pr + o_is_rep + 24 + st)) {
           dist = r1;
         } else {
-          if (!rc.bit(pr + P_IS_REP_G2 + st)) {
+          if (!rc.bit(pr + o_is_rep + 36 + st)) {
             dist = r2;
           } else {
             dist = r3;
@@ -291,25 +342,26 @@ __device__ int lz_run(LzState& s, uint64_t limit, Rd& rd, uint32_t in_limit) {
         r0 = dist;
       }
       st = (st < 7) ? 8 : 11;
-      lcoder = P_REP_LEN;
+      lcoder = o_replen;
+      hcoder = 256;
     }
-    if (!rc.bit(pr + lcoder + L_CHOICE))
-      len = rc.tree(pr + lcoder + L_LOW + (ps << 3), 3);
-    else if (!rc.bit(pr + lcoder + L_CHOICE2))
-      len = 8 + rc.tree(pr + lcoder + L_MID + (ps << 3), 3);
+    if (!rc.bit(pr + lcoder))
+      len = rc.tree(pr + lcoder + 2 + (ps << 3), 3);
+    else if (!rc.bit(pr + lcoder + 1))
+      len = 8 + rc.tree(pr + lcoder + 2 + (8u << pb) + (ps << 3), 3);
     else
-      len = 16 + rc.tree(pr + lcoder + L_HIGH, 8);
+      len = 16 + rc.tree(hi + hcoder, 8);
 
     if (st >= 12) {
       const uint32_t lstate = len < 4 ? len : 3;
-      uint32_t dist = rc.tree(pr + P_POS_SLOT + (lstate << 6), 6);
+      uint32_t dist = rc.tree(pr + o_slot + (lstate << 6), 6);
       if (dist >= 4) {
         const uint32_t slot = dist;
         uint32_t nbits = (slot >> 1) - 1;
         dist = 2 | (slot & 1);
         if (slot < 14) {
           dist <<= nbits;
-          uint16_t* sp = pr + P_SPEC_POS + dist - slot - 1;
+          Lo sp = pr + o_spec + dist - slot - 1;
           uint32_t mask = 1, node = 1;
           do {
             uint32_t b = rc.bit(sp + node);
@@ -324,7 +376,7 @@ __device__ int lz_run(LzState& s, uint64_t limit, Rd& rd, uint32_t in_limit) {
           uint32_t node = 1;
 #pragma unroll
           for (uint32_t k = 0; k < 4; ++k) {
-            uint32_t b = rc.bit(pr + P_ALIGN + node);
+            uint32_t b = rc.bit(pr + o_align + node);
             node = (node << 1) | b;
             dist |= b << k;
           }
@@ -373,7 +425,8 @@ __device__ int lz_run(LzState& s, uint64_t limit, Rd& rd, uint32_t in_limit) {
   return kOk;
 }
 
-__device__ inline void lz_flush_pending(LzState& s, uint64_t limit) {
+template <class Lo>
+__device__ __forceinline__ void lz_flush_pending(LzStateT<Lo>& s, uint64_t limit) {
   if (s.pending == 0 || s.pending >= kLenDone) return;
   uint32_t n = s.pending;
   if (limit - s.pos < n) n = uint32_t(limit - s.pos);
@@ -386,8 +439,9 @@ __device__ inline void lz_flush_pending(LzState& s, uint64_t limit) {
   }
 }
 
-template <class Rd>
-__device__ int lz_run_split(LzState& s, uint64_t limit, Rd& rd, uint32_t in_limit) {
+template <class Lo, class Rd>
+__device__ __forceinline__ int lz_run_split(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
+                                            uint32_t in_limit) {
   do {
     uint64_t lim = limit;
     if (s.full == 0) {
@@ -419,7 +473,8 @@ struct Probe {
     return true;
   }
   // 0/1, or -1 when the input ran out
-  __device__ __forceinline__ int bit(const uint16_t* prob) {
+  template <class P>
+  __device__ __forceinline__ int bit(P prob) {
     if (!norm()) return -1;
     uint32_t bound = (range >> 11) * uint32_t(*prob);
     if (code < bound) { range = bound; return 0; }
@@ -427,7 +482,8 @@ struct Probe {
     code -= bound;
     return 1;
   }
-  __device__ __forceinline__ bool tree(const uint16_t* probs, uint32_t bits, uint32_t& out) {
+  template <class P>
+  __device__ __forceinline__ bool tree(P probs, uint32_t bits, uint32_t& out) {
     uint32_t m = 1, lim = 1u << bits;
     while (m < lim) {
       int b = bit(probs + m);
@@ -440,16 +496,18 @@ struct Probe {
 };
 
 // Would one more symbol decode from [in, in+n)?  (LzmaDec_TryDummy)
-__device__ int lz_probe(const LzState& s, const uint8_t* in, uint64_t n) {
-  const uint16_t* pr = s.probs;
-  const uint32_t ps = s.total & ((1u << s.pb) - 1);
-  uint32_t st = s.st, lcoder, len = 0;
+template <class Lo>
+__device__ int lz_probe(const LzStateT<Lo>& s, const uint8_t* in, uint64_t n) {
+  const Lo pr = s.lo;
+  const uint32_t pb = s.pb;
+  const uint32_t ps = s.total & ((1u << pb) - 1);
+  uint32_t st = s.st, lcoder, hcoder, len = 0;
   int kind, b;
   Probe t{s.range, s.code, in, in + n};
 #define LZ_PB(p) do { b = t.bit(p); if (b < 0) return PROBE_SHORT; } while (0)
-  LZ_PB(pr + P_IS_MATCH + (st << 4) + ps);
+  LZ_PB(pr + (st << pb) + ps);
   if (b == 0) {
-    const uint16_t* lit = pr + P_LITERAL;
+    Lo lit = pr + off_lit(pb);
     uint32_t sym = 1;
     if (s.full != 0 || s.total != 0) {
       uint32_t prev = s.dic[(s.pos == 0 ? s.cap : s.pos) - 1];
@@ -473,45 +531,47 @@ __device__ int lz_probe(const LzState& s, const uint8_t* in, uint64_t n) {
     }
     kind = PROBE_LIT;
   } else {
-    LZ_PB(pr + P_IS_REP + st);
+    LZ_PB(pr + off_is_rep(pb) + st);
     if (b == 0) {
       st = 0;
-      lcoder = P_LEN;
+      lcoder = off_len(pb);
+      hcoder = 0;
       kind = PROBE_MATCH;
     } else {
       kind = PROBE_REP;
-      LZ_PB(pr + P_IS_REP_G0 + st);
+      LZ_PB(pr + off_is_rep(pb) + 12 + st);
       if (b == 0) {
-        LZ_PB(pr + P_IS_REP0_LONG + (st << 4) + ps);
+        LZ_PB(pr + off_rep0long(pb) + (st << pb) + ps);
         if (b == 0) return t.norm() ? PROBE_REP : PROBE_SHORT;
       } else {
-        LZ_PB(pr + P_IS_REP_G1 + st);
-        if (b != 0) LZ_PB(pr + P_IS_REP_G2 + st);
+        LZ_PB(pr + off_is_rep(pb) + 24 + st);
+        if (b != 0) LZ_PB(pr + off_is_rep(pb) + 36 + st);
       }
       st = 12;
-      lcoder = P_REP_LEN;
+      lcoder = off_replen(pb);
+      hcoder = 256;
     }
-    LZ_PB(pr + lcoder + L_CHOICE);
+    LZ_PB(pr + lcoder);
     if (b == 0) {
-      if (!t.tree(pr + lcoder + L_LOW + (ps << 3), 3, len)) return PROBE_SHORT;
+      if (!t.tree(pr + lcoder + 2 + (ps << 3), 3, len)) return PROBE_SHORT;
     } else {
-      LZ_PB(pr + lcoder + L_CHOICE2);
+      LZ_PB(pr + lcoder + 1);
       if (b == 0) {
-        if (!t.tree(pr + lcoder + L_MID + (ps << 3), 3, len)) return PROBE_SHORT;
+        if (!t.tree(pr + lcoder + 2 + (8u << pb) + (ps << 3), 3, len)) return PROBE_SHORT;
         len += 8;
       } else {
-        if (!t.tree(pr + lcoder + L_HIGH, 8, len)) return PROBE_SHORT;
+        if (!t.tree(s.hi + hcoder, 8, len)) return PROBE_SHORT;
         len += 16;
       }
     }
     if (st < 4) {
       uint32_t slot;
-      if (!t.tree(pr + P_POS_SLOT + ((len < 4 ? len : 3) << 6), 6, slot)) return PROBE_SHORT;
+      if (!t.tree(pr + off_slot(pb) + ((len < 4 ? len : 3) << 6), 6, slot)) return PROBE_SHORT;
       if (slot >= 4) {
         uint32_t nbits = (slot >> 1) - 1, node = 1;
-        const uint16_t* base;
+        Lo base;
         if (slot < 14) {
-          base = pr + P_SPEC_POS + ((2u | (slot & 1)) << nbits) - slot - 1;
+          base = pr + off_spec(pb) + ((2u | (slot & 1)) << nbits) - slot - 1;
         } else {
           nbits -= 4;
           do {
@@ -519,7 +579,7 @@ __device__ int lz_probe(const LzState& s, const uint8_t* in, uint64_t n) {
             t.range >>= 1;
             t.code -= t.range & (((t.code - t.range) >> 31) - 1);
           } while (--nbits != 0);
-          base = pr + P_ALIGN;
+          base = pr + off_align(pb);
           nbits = 4;
         }
         do {
@@ -535,20 +595,30 @@ __device__ int lz_probe(const LzState& s, const uint8_t* in, uint64_t n) {
 
 // ------------------------------------------------------------------ init + driver
 
-__device__ inline void lz_init_state_real(LzState& s) {
-  const uint32_t n = num_probs(s.lc, s.lp);
-  // 8-byte stores where possible (the table starts 8-byte aligned)
-  uint64_t* p8 = reinterpret_cast<uint64_t*>(s.probs);
-  const uint64_t v = 0x0400040004000400ull;
+// All cells to 1024 (LzmaDec_InitStateReal, LzmaDec.c:707-717).  lo and hi
+// start 4-byte aligned; stores go two cells at a time.
+template <class Lo>
+__device__ __forceinline__ void fill_prob_init(Lo p, uint32_t n) {
   uint32_t i = 0;
-  for (; i + 4 <= n; i += 4) p8[i >> 2] = v;
-  for (; i < n; ++i) s.probs[i] = uint16_t(kProbInit);
+  for (; i + 2 <= n; i += 2) {
+    p[i] = uint16_t(kProbInit);
+    p[i + 1] = uint16_t(kProbInit);
+  }
+  if (i < n) p[i] = uint16_t(kProbInit);
+}
+
+template <class Lo>
+__device__ __forceinline__ void lz_init_state_real(LzStateT<Lo>& s) {
+  fill_prob_init(s.lo, lo_cells(s.lc, s.lp, s.pb));
+  fill_prob_init(s.hi, kHiCells);
   s.rep0 = s.rep1 = s.rep2 = s.rep3 = 1;
   s.st = 0;
   s.need_state_init = 0;
 }
 
-__device__ inline void lz_init_dic_state(LzState& s, bool init_dic, bool init_state) {
+template <class Lo>
+__device__ __forceinline__ void lz_init_dic_state(LzStateT<Lo>& s, bool init_dic,
+                                                  bool init_state) {
   s.need_rc_init = 1;
   s.pending = 0;
   s.tmp_n = 0;
@@ -560,9 +630,13 @@ __device__ inline void lz_init_dic_state(LzState& s, bool init_dic, bool init_st
   if (init_state) s.need_state_init = 1;
 }
 
-// LzmaDec_DecodeToDic for one lane.  src is global memory.
-__device__ int lz_decode_to_dic(LzState& s, uint64_t dic_limit, const uint8_t* src,
-                                uint64_t& src_len, int fin, int& status) {
+// LzmaDec_DecodeToDic for one lane.  src is global memory.  WithTemp = false
+// drops the tempBuf continuation path, which a one-call decode (all input
+// present) never takes: its first need is a NEEDS_MORE_INPUT return.
+template <bool WithTemp, class Lo>
+__device__ __forceinline__ int lz_decode_to_dic(LzStateT<Lo>& s, uint64_t dic_limit,
+                                                const uint8_t* src, uint64_t& src_len, int fin,
+                                                int& status) {
   uint64_t avail = src_len;
   src_len = 0;
   lz_flush_pending(s, dic_limit);
@@ -592,7 +666,7 @@ __device__ int lz_decode_to_dic(LzState& s, uint64_t dic_limit, const uint8_t* s
     }
     if (s.need_state_init) lz_init_state_real(s);
 
-    if (s.tmp_n == 0) {
+    if (!WithTemp || s.tmp_n == 0) {
       uint32_t in_limit;
       if (avail < kLookahead || at_end_check) {
         int k = lz_probe(s, src, avail);

@@ -11,3 +11,7 @@ extern "C" int lzgpu_launch_decode_batch(const LzmaGpuStreamDesc* d_descs, const
                                          uint16_t* d_ws, LzmaGpuResult* d_results,
                                          hipStream_t stream);
 extern "C" int lzgpu_launch_session(LzgpuSession* d_sess, uint32_t n, hipStream_t stream);
+extern "C" int lzgpu_launch_decode_lds(const LzmaGpuStreamDesc* d_descs, const uint32_t* d_order,
+                                       uint32_t n, const uint8_t* d_src, uint8_t* d_dst,
+                                       uint16_t* d_ws, LzmaGpuResult* d_results, uint32_t lanes,
+                                       uint32_t stride, hipStream_t stream);

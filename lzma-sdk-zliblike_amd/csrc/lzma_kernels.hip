@@ -1,9 +1,19 @@
 // lzma_kernels.hip -- batch LZMA / LZMA2 decode kernels for gfx950.
 //
-// Grid mapping: one stream per lane, 64-lane workgroups (one wave each).
-// `order` (optional) maps lane -> descriptor so the host planner can group
-// streams of similar size and table width into the same wave (a wave runs
-// until its slowest lane finishes).  The per-lane work is in lzma_lane.h.
+// lzgpu_decode_lds_kernel (fast path, LZMA items whose lo table fits LDS):
+//   one stream per lane, L lanes per workgroup (one wave with L active
+//   lanes), each lane's lo probability table in its own LDS slice of
+//   `stride` cells; the planner picks L so that about four workgroups share a
+//   CU's 160 KiB.  The hardware dispatcher starts a new workgroup whenever
+//   one retires, so a 64K-stream batch streams through the chip in waves of
+//   resident workgroups with no host round trips.
+// lzgpu_decode_batch_kernel (generic: any lc/lp/pb, LZMA2 ranges): 64 lanes
+//   per workgroup, whole table in the item's global workspace slice.
+// lzgpu_session_kernel: one LzmaDec_DecodeToDic call per lane on a
+//   device-resident decoder state (dictionary / buffer interfaces).
+// `order` (optional) maps lane -> descriptor so the planner can put streams of
+// similar length into the same wave (a wave runs until its slowest lane ends).
+// The per-lane work is in lzma_lane.h.
 #include <hip/hip_runtime.h>
 
 #include "lzma_gpu_internal.h"
@@ -19,6 +29,20 @@ __global__ void __launch_bounds__(64) lzgpu_decode_batch_kernel(
   const uint32_t id = order ? order[lane] : lane;
   const LzmaGpuStreamDesc d = descs[id];
   results[id] = lane_decode(d, src, dst, ws);
+}
+
+__global__ void __launch_bounds__(64) lzgpu_decode_lds_kernel(
+    const LzmaGpuStreamDesc* __restrict__ descs, const uint32_t* __restrict__ order, uint32_t n,
+    const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, uint16_t* __restrict__ ws,
+    LzmaGpuResult* __restrict__ results, uint32_t stride) {
+  extern __shared__ uint32_t lz_smem[];
+  const uint32_t lane = blockIdx.x * blockDim.x + threadIdx.x;
+  if (lane >= n) return;
+  const uint32_t id = order ? order[lane] : lane;
+  const LzmaGpuStreamDesc d = descs[id];
+  lds_u16* lo = (lds_u16*)((uint16_t*)lz_smem) +
+                threadIdx.x * stride;
+  results[id] = lane_decode_lds(d, src, dst, ws, lo, stride);
 }
 
 // One DecodeToDic call per lane on a device-resident decoder state.
@@ -38,6 +62,24 @@ extern "C" int lzgpu_launch_decode_batch(const LzmaGpuStreamDesc* d_descs, const
   const uint32_t grid = (n + block - 1) / block;
   hipLaunchKernelGGL(lzgpu_decode_batch_kernel, dim3(grid), dim3(block), 0, stream, d_descs,
                      d_order, n, d_src, d_dst, d_ws, d_results);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+extern "C" int lzgpu_launch_decode_lds(const LzmaGpuStreamDesc* d_descs, const uint32_t* d_order,
+                                       uint32_t n, const uint8_t* d_src, uint8_t* d_dst,
+                                       uint16_t* d_ws, LzmaGpuResult* d_results, uint32_t lanes,
+                                       uint32_t stride, hipStream_t stream) {
+  if (n == 0) return 0;
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(lzgpu_decode_lds_kernel),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr_set = true;
+  }
+  const size_t lds = size_t(lanes) * stride * 2;
+  const uint32_t grid = (n + lanes - 1) / lanes;
+  hipLaunchKernelGGL(lzgpu_decode_lds_kernel, dim3(grid), dim3(lanes), lds, stream, d_descs,
+                     d_order, n, d_src, d_dst, d_ws, d_results, stride);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

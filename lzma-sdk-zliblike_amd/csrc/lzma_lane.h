@@ -30,6 +30,9 @@ struct LzgpuSession {
 
 namespace lzgpu {
 
+// One batch item with the whole probability table in global memory (the
+// generic kernel: any lc/lp/pb, LZMA or LZMA2).  The item's workspace slice
+// holds table_cells() cells: lo first, hi behind it.
 __device__ __forceinline__ LzmaGpuResult lane_decode(const LzmaGpuStreamDesc& d,
                                                      const uint8_t* __restrict__ src,
                                                      uint8_t* __restrict__ dst,
@@ -39,13 +42,14 @@ __device__ __forceinline__ LzmaGpuResult lane_decode(const LzmaGpuStreamDesc& d,
   r.dest_len = 0;
   r.src_len = 0;
   if (d.kind == LZMA_GPU_KIND_LZMA2) {
-    Lz2State p;
-    r.res = lz2_init(p, d.props[0], ws + d.probs_off, dst + d.dst_off, d.dst_cap);
-    if (r.res != kOk) return r;
     if (d.probs_off == LZMA_GPU_NO_WORKSPACE) {
-      r.res = kErrMem;
+      r.res = (d.props[0] > 40) ? kErrUnsupported : kErrMem;
       return r;
     }
+    Lz2StateT<uint16_t*> p;
+    uint16_t* lo = ws + d.probs_off;
+    r.res = lz2_init(p, d.props[0], lo, lo + lo_cells(4, 0, 4), dst + d.dst_off, d.dst_cap);
+    if (r.res != kOk) return r;
     uint64_t sl = d.src_len;
     int status = kStNone;
     // the batch contract for an LZMA2 range is Lzma2Dec_DecodeToDic's own
@@ -61,14 +65,15 @@ __device__ __forceinline__ LzmaGpuResult lane_decode(const LzmaGpuStreamDesc& d,
     r.res = kErrInputEof;
     return r;
   }
-  LzState s;
+  LzStateT<uint16_t*> s;
   r.res = lz_props_parse(d.props, d.props_size, s.lc, s.lp, s.pb, s.dict_size);
   if (r.res != kOk) return r;
   if (d.probs_off == LZMA_GPU_NO_WORKSPACE) {
     r.res = kErrMem;
     return r;
   }
-  s.probs = ws + d.probs_off;
+  s.lo = ws + d.probs_off;
+  s.hi = s.lo + lo_cells(s.lc, s.lp, s.pb);
   s.dic = dst + d.dst_off;
   s.cap = d.dst_cap;
   s.pos = 0;
@@ -79,7 +84,7 @@ __device__ __forceinline__ LzmaGpuResult lane_decode(const LzmaGpuStreamDesc& d,
   lz_init_dic_state(s, true, true);
   uint64_t sl = d.src_len;
   int status = kStNone;
-  int res = lz_decode_to_dic(s, d.dst_cap, src + d.src_off, sl, d.finish_mode, status);
+  int res = lz_decode_to_dic<false>(s, d.dst_cap, src + d.src_off, sl, d.finish_mode, status);
   if (res == kOk && status == kStMoreInput) res = kErrInputEof;
   r.res = res;
   r.status = status;
@@ -88,13 +93,60 @@ __device__ __forceinline__ LzmaGpuResult lane_decode(const LzmaGpuStreamDesc& d,
   return r;
 }
 
+// One LZMA batch item with the lo table in the lane's LDS slice (lo_cap
+// cells) and the LenHigh trees at the start of its global workspace slice.
+// The planner only routes items here whose lo table fits lo_cap.
+__device__ __forceinline__ LzmaGpuResult lane_decode_lds(const LzmaGpuStreamDesc& d,
+                                                         const uint8_t* __restrict__ src,
+                                                         uint8_t* __restrict__ dst,
+                                                         uint16_t* __restrict__ ws, lds_u16* lo,
+                                                         uint32_t lo_cap) {
+  LzmaGpuResult r;
+  r.status = -1;
+  r.dest_len = 0;
+  r.src_len = 0;
+  if (d.src_len < 5) {
+    r.res = kErrInputEof;
+    return r;
+  }
+  LzStateT<lds_u16*> s;
+  r.res = lz_props_parse(d.props, d.props_size, s.lc, s.lp, s.pb, s.dict_size);
+  if (r.res != kOk) return r;
+  if (d.probs_off == LZMA_GPU_NO_WORKSPACE || lo_cells(s.lc, s.lp, s.pb) > lo_cap) {
+    r.res = kErrMem;
+    return r;
+  }
+  s.lo = lo;
+  s.hi = ws + d.probs_off;
+  s.dic = dst + d.dst_off;
+  s.cap = d.dst_cap;
+  s.pos = 0;
+  s.range = s.code = 0;
+  s.st = 0;
+  s.rep0 = s.rep1 = s.rep2 = s.rep3 = 1;
+  s.need_state_init = 0;
+  lz_init_dic_state(s, true, true);
+  uint64_t sl = d.src_len;
+  int status = kStNone;
+  int res = lz_decode_to_dic<false>(s, d.dst_cap, src + d.src_off, sl, d.finish_mode, status);
+  if (res == kOk && status == kStMoreInput) res = kErrInputEof;
+  r.res = res;
+  r.status = status;
+  r.dest_len = s.pos;
+  r.src_len = sl;
+  return r;
+}
+
+// One LzmaDec_DecodeToDic call on a device-resident decoder (compact layout in
+// q.probs: lo then hi, for the current lc/lp/pb).
 __device__ __forceinline__ void lane_session(LzgpuSession& q) {
-  LzState s;
+  LzStateT<uint16_t*> s;
   s.lc = q.lc;
   s.lp = q.lp;
   s.pb = q.pb;
   s.dict_size = q.dict_size;
-  s.probs = q.probs;
+  s.lo = q.probs;
+  s.hi = q.probs + lo_cells(q.lc, q.lp, q.pb);
   s.dic = q.dic;
   s.cap = q.cap;
   s.pos = q.pos;
@@ -114,7 +166,7 @@ __device__ __forceinline__ void lane_session(LzgpuSession& q) {
   for (int i = 0; i < int(kLookahead); ++i) s.tmp[i] = q.tmp[i];
   uint64_t sl = q.in_len;
   int status = kStNone;
-  int res = lz_decode_to_dic(s, q.dic_limit, q.in, sl, q.finish_mode, status);
+  int res = lz_decode_to_dic<true>(s, q.dic_limit, q.in, sl, q.finish_mode, status);
   q.pos = s.pos;
   q.range = s.range;
   q.code = s.code;

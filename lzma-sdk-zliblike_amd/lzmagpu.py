@@ -71,6 +71,13 @@ class Result(ctypes.Structure):
                 ("dest_len", ctypes.c_uint64), ("src_len", ctypes.c_uint64)]
 
 
+class Plan(ctypes.Structure):
+    _fields_ = [("workspace_bytes", ctypes.c_uint64), ("n", ctypes.c_uint64),
+                ("n_lds", ctypes.c_uint64), ("lanes_per_group", ctypes.c_uint32),
+                ("lds_cells_per_lane", ctypes.c_uint32), ("groups_per_cu", ctypes.c_uint32),
+                ("reserved", ctypes.c_uint32 * 9)]
+
+
 assert ctypes.sizeof(StreamDesc) == 48 and ctypes.sizeof(Result) == 24
 assert ctypes.sizeof(CLzmaDec) == 136
 
@@ -95,6 +102,8 @@ _sig = {
     "Lzma2Decode": (ctypes.c_int, [_P, _sp, _P, _sp, ctypes.c_ubyte, ctypes.c_int, _ip, ctypes.POINTER(ISzAlloc)]),
     "LzmaGpu_PlanBatch": (ctypes.c_size_t, [ctypes.POINTER(StreamDesc), ctypes.c_size_t, _P]),
     "LzmaGpu_DecodeBatch": (ctypes.c_int, [_P, _P, ctypes.c_size_t, _P, _P, _P, ctypes.c_size_t, _P, _P]),
+    "LzmaGpu_PlanBatchEx": (ctypes.c_int, [ctypes.POINTER(StreamDesc), ctypes.c_size_t, _P, ctypes.POINTER(Plan)]),
+    "LzmaGpu_DecodeBatchEx": (ctypes.c_int, [ctypes.POINTER(Plan), _P, _P, _P, _P, _P, _P, _P]),
     "LzmaGpu_DecodeBatchHost": (ctypes.c_int, [ctypes.POINTER(StreamDesc), ctypes.c_size_t, _P, ctypes.c_size_t, _P, ctypes.c_size_t, ctypes.POINTER(Result)]),
     "Lzma2Gpu_SplitBlocks": (ctypes.c_size_t, [_P, ctypes.c_size_t, _P, _P, _P, ctypes.c_size_t]),
     "LzmaGpu_DeviceCount": (ctypes.c_int, []),
@@ -247,6 +256,23 @@ def decode_batch_host(descs, src, dst_bytes):
 def plan(descs, order=None):
     """Fill probs_off (and the lane order, a ctypes uint32 array). Returns workspace bytes."""
     return _lib.LzmaGpu_PlanBatch(descs, len(descs), order)
+
+
+def plan_ex(descs):
+    """LzmaGpu_PlanBatchEx: returns (Plan, order[ctypes uint32 array])."""
+    n = len(descs)
+    order = (ctypes.c_uint32 * max(n, 1))()
+    p = Plan()
+    r = _lib.LzmaGpu_PlanBatchEx(descs, n, order, ctypes.byref(p))
+    if r != SZ_OK:
+        raise RuntimeError(f"LzmaGpu_PlanBatchEx failed: {r}")
+    return p, order
+
+
+def decode_batch_device_ex(plan, d_descs, d_order, d_src, d_dst, d_ws, d_results, stream=0):
+    """LzmaGpu_DecodeBatchEx over raw device pointers (ints)."""
+    return _lib.LzmaGpu_DecodeBatchEx(ctypes.byref(plan), d_descs, d_order, d_src, d_dst, d_ws,
+                                      d_results, stream or None)
 
 
 def decode_batch_device(d_descs, d_order, n, d_src, d_dst, d_ws, ws_bytes, d_results, stream=0):

@@ -19,6 +19,17 @@ void emu_decode_batch(const LzmaGpuStreamDesc* descs, size_t n, const uint8_t* s
   for (size_t i = 0; i < n; ++i) results[i] = lane_decode(descs[i], src, dst, ws);
 }
 
+// LDS-variant kernel body: each lane gets a private "LDS" slice of stride cells.
+void emu_decode_batch_lds(const LzmaGpuStreamDesc* descs, size_t n, const uint8_t* src,
+                          uint8_t* dst, uint16_t* ws, LzmaGpuResult* results, uint32_t stride) {
+  uint16_t* slab = (uint16_t*)malloc(size_t(stride) * 2 + 16);
+  for (size_t i = 0; i < n; ++i) {
+    memset(slab, 0xA5, size_t(stride) * 2);  // LDS is not zeroed between workgroups
+    results[i] = lane_decode_lds(descs[i], src, dst, ws, slab, stride);
+  }
+  free(slab);
+}
+
 // zlib-like DecodeToBuf loop driven through lane_session (the session
 // kernel's body), same contract as orc_lzma_stream_decode.
 int emu_stream_decode(const uint8_t* props, const uint8_t* src, size_t src_total, uint8_t* out,

@@ -112,7 +112,19 @@ def test_plan_batch_workspace_and_order():
     descs = L.make_descs(items)
     order = (ctypes.c_uint32 * 3)()
     ws = L.plan(descs, order)
+    # compact device layout: lo = 56 * 2^pb + 438 + 0x300 << (lc+lp), hi = 512 cells
+    def cells(lc, lp, pb):
+        return 56 * (1 << pb) + 438 + (768 << (lc + lp)) + 512
     assert descs[0].probs_off == 0
-    assert descs[1].probs_off == (1846 + 768 * 8 + 7) // 8 * 8
-    assert ws == 2 * (descs[1].probs_off + (1846 + 768 + 7) // 8 * 8)
+    assert descs[1].probs_off == (cells(3, 0, 2) + 7) // 8 * 8
+    assert ws == 2 * (descs[1].probs_off + (cells(0, 0, 0) + 7) // 8 * 8)
     assert list(order) == [1, 2, 0]
+    # compact table never exceeds what LzmaDec_AllocateProbs allocates (numProbs)
+    for lc in range(9):
+        for lp in range(5):
+            for pb in range(5):
+                assert cells(lc, lp, pb) <= 1846 + (768 << (lc + lp))
+    plan, order2 = L.plan_ex(descs)
+    assert plan.n == 3 and plan.n_lds == 2 and list(order2) == [1, 0, 2]
+    assert plan.lds_cells_per_lane == (56 * 1 + 438 + 768 + 3) // 4 * 4 or \
+        plan.lds_cells_per_lane >= 56 * 4 + 438 + 768 * 8

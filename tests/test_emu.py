@@ -20,6 +20,10 @@ EMU_SO = os.path.join(native.ROOT, "tests", "emu", "liblane_emu.so")
 def emu():
     subprocess.run(["make", "-s", "-f", "tests/emu/Makefile"], cwd=native.ROOT, check=True)
     lib = ctypes.CDLL(EMU_SO)
+    lib.emu_decode_batch_lds.restype = None
+    lib.emu_decode_batch_lds.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_char_p,
+                                         ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                         ctypes.c_uint32]
     lib.emu_decode_batch.restype = None
     lib.emu_decode_batch.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_char_p,
                                      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
@@ -32,20 +36,37 @@ def emu():
     return lib
 
 
-def run_batch(emu, items, src):
+def run_batch(emu, items, src, lds=False):
+    """The kernel bodies on the host.  lds=True follows the planner: items it puts
+    on the LDS kernel run through lane_decode_lds, the rest through lane_decode."""
     import lzmagpu as L
     descs = L.make_descs(items)
-    ws = L.plan(descs)
     n = len(items)
-    wsbuf = ctypes.create_string_buffer(max(ws, 16))
+    order = (ctypes.c_uint32 * max(n, 1))()
+    plan = L.Plan()
+    assert L.lib.LzmaGpu_PlanBatchEx(descs, n, order, ctypes.byref(plan)) == 0
+    wsbuf = ctypes.create_string_buffer(max(plan.workspace_bytes, 16))
     dst_bytes = max((it["dst_off"] + it["dst_cap"] for it in items), default=0)
     dst = ctypes.create_string_buffer(max(dst_bytes, 1))
     res = (L.Result * max(n, 1))()
-    emu.emu_decode_batch(descs, n, src, dst, wsbuf, res)
+    if not lds:
+        emu.emu_decode_batch(descs, n, src, dst, wsbuf, res)
+        return res, dst.raw
+    one = (L.StreamDesc * 1)()
+    r1 = (L.Result * 1)()
+    for k in range(n):
+        i = order[k]
+        one[0] = descs[i]
+        if k < plan.n_lds:
+            emu.emu_decode_batch_lds(one, 1, src, dst, wsbuf, r1, plan.lds_cells_per_lane)
+        else:
+            emu.emu_decode_batch(one, 1, src, dst, wsbuf, r1)
+        res[i] = r1[0]
     return res, dst.raw
 
 
-def test_emu_golden_lzma_batch(emu):
+@pytest.mark.parametrize("lds", [False, True])
+def test_emu_golden_lzma_batch(emu, lds):
     d = G.load()
     items, srcs, off, doff = [], [], 0, 0
     cs = G.cases("lzma")
@@ -56,7 +77,7 @@ def test_emu_golden_lzma_batch(emu):
         srcs.append(s)
         off += len(s)
         doff += c["dest_cap"]
-    res, dst = run_batch(emu, items, b"".join(srcs) + b"\0" * 8)
+    res, dst = run_batch(emu, items, b"".join(srcs) + b"\0" * 8, lds)
     bad = []
     for k, (i, c) in enumerate(cs):
         e = c["expect"]
@@ -99,7 +120,8 @@ def test_emu_golden_streaming(emu):
         assert G.sha(out.raw[:ol.value]) == e["sha256"]
 
 
-def test_emu_fuzz_vs_oracle(emu):
+@pytest.mark.parametrize("lds", [False, True])
+def test_emu_fuzz_vs_oracle(emu, lds):
     rng = random.Random(77)
     orc = native.oracle()
     items, srcs, exp, off, doff = [], [], [], 0, 0
@@ -134,7 +156,7 @@ def test_emu_fuzz_vs_oracle(emu):
         exp.append(native.decode(orc, "orc", comp, props, cap, fin))
         off += len(comp)
         doff += cap
-    res, dst = run_batch(emu, items, b"".join(srcs) + b"\0" * 8)
+    res, dst = run_batch(emu, items, b"".join(srcs) + b"\0" * 8, lds)
     for k in range(len(items)):
         got = (res[k].res, res[k].status, res[k].dest_len, res[k].src_len)
         out = dst[items[k]["dst_off"]:items[k]["dst_off"] + res[k].dest_len]
