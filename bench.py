@@ -259,7 +259,8 @@ def main():
                        "kernel_plan": {"lds_streams": int(plan.n_lds),
                                        "streams_per_workgroup": int(plan.lanes_per_group),
                                        "lds_bytes_per_stream": int(plan.lds_cells_per_lane) * 2,
-                                       "workgroups_per_cu": int(plan.groups_per_cu)}},
+                                       "workgroups_per_cu": int(plan.groups_per_cu),
+                                       "waves_per_simd": int(plan.waves_per_simd)}},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
                          "traffic": traffic,

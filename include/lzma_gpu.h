@@ -216,7 +216,8 @@ size_t LzmaGpu_PlanBatch(LzmaGpuStreamDesc *descs, size_t n, uint32_t *order);
  * workgroup, lds_cells_per_lane cells each); order[n_lds, n) runs on the
  * generic kernel (tables in the global workspace: LZMA2 ranges, lc+lp too
  * wide for LDS).  Environment overrides for experiments:
- * LZGPU_KERNEL=global|lds, LZGPU_LANES=<streams per workgroup>. */
+ * LZGPU_KERNEL=global|lds, LZGPU_LANES=<streams per workgroup>,
+ * LZGPU_OCC=<4|6|8 waves per SIMD>. */
 typedef struct LzmaGpuPlan {
   uint64_t workspace_bytes;
   uint64_t n;
@@ -224,7 +225,8 @@ typedef struct LzmaGpuPlan {
   uint32_t lanes_per_group;
   uint32_t lds_cells_per_lane;
   uint32_t groups_per_cu;
-  uint32_t reserved[9];
+  uint32_t waves_per_simd; /* LDS kernel register budget: 4, 6 or 8 waves per SIMD */
+  uint32_t reserved[8];
 } LzmaGpuPlan;
 
 SRes LzmaGpu_PlanBatchEx(LzmaGpuStreamDesc *descs, size_t n, uint32_t *order, LzmaGpuPlan *plan);

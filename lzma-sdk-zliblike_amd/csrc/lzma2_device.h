@@ -75,7 +75,7 @@ __device__ inline int lz2_header_byte(Lz2StateT<Lo>& p, uint32_t b) {
 // Lzma2Dec_DecodeToDic for one lane (src in global memory).
 template <class Lo>
 __device__ __forceinline__ int lz2_decode_to_dic(Lz2StateT<Lo>& p, uint64_t dic_limit,
-                                                 const uint8_t* src, uint64_t& src_len, int fin,
+                                                 const gbyte* src, uint64_t& src_len, int fin,
                                                  int& status) {
   const uint64_t in_size = src_len;
   src_len = 0;
@@ -157,8 +157,8 @@ __device__ __forceinline__ int lz2_decode_to_dic(Lz2StateT<Lo>& p, uint64_t dic_
 // lc = 4, lp = 0, pb = 0 for the allocation; dictionary size from the prop.
 // lo must hold lo_cells(4, 0, 4) cells (the largest an LZMA2 chunk can ask for).
 template <class Lo>
-__device__ __forceinline__ int lz2_init(Lz2StateT<Lo>& p, uint32_t prop, Lo lo, uint16_t* hi,
-                                        uint8_t* dic, uint64_t cap) {
+__device__ __forceinline__ int lz2_init(Lz2StateT<Lo>& p, uint32_t prop, Lo lo, gu16* hi,
+                                        gbyte* dic, uint64_t cap) {
   if (prop > 40) return kErrUnsupported;
   uint32_t dict = (prop == 40) ? 0xFFFFFFFFu : ((2u | (prop & 1u)) << (prop / 2 + 11));
   p.dec.lc = 4;

@@ -709,13 +709,21 @@ SRes LzmaGpu_PlanBatchEx(LzmaGpuStreamDesc* descs, size_t n, uint32_t* order,
     stride = (stride + 3) & ~3u;  // 8-byte aligned per-lane slices
     const uint32_t lds_per_cu = 160 * 1024;
     const uint32_t per_cu = std::max<uint32_t>(1, lds_per_cu / (stride * 2));
+    // Measured (r01 sweep, 64K x 4 KiB): few streams per wave and many waves
+    // per SIMD win -- each stream is a serial chain, so the CU needs many
+    // independent waves in flight; SIMT width only adds divergence.  Aim for
+    // 16 workgroups (waves) per CU at 4 waves/SIMD.
     uint32_t lanes = 1;
-    while (lanes * 2 <= 64 && lanes * 2 * 4 <= per_cu) lanes *= 2;  // ~4 groups per CU
+    while (lanes * 2 <= 64 && lanes * 2 * 16 <= per_cu) lanes *= 2;
     const int over = env_int("LZGPU_LANES", 0);
     if (over > 0 && over <= 64 && uint32_t(over) * stride * 2 <= lds_per_cu) lanes = uint32_t(over);
+    uint32_t occ = 4;
+    const int occ_over = env_int("LZGPU_OCC", 0);
+    if (occ_over == 4 || occ_over == 6 || occ_over == 8) occ = uint32_t(occ_over);
     plan->lanes_per_group = lanes;
     plan->lds_cells_per_lane = stride;
-    plan->groups_per_cu = lds_per_cu / (lanes * stride * 2);
+    plan->groups_per_cu = std::min<uint32_t>(lds_per_cu / (lanes * stride * 2), 4 * occ);
+    plan->waves_per_simd = occ;
   }
   return SZ_OK;
 }
@@ -730,7 +738,7 @@ SRes LzmaGpu_DecodeBatchEx(const LzmaGpuPlan* plan, const LzmaGpuStreamDesc* d_d
   const uint32_t n_lds = uint32_t(plan->n_lds), n_glob = uint32_t(plan->n - plan->n_lds);
   if (n_lds && lzgpu_launch_decode_lds(d_descs, d_order, n_lds, d_src, d_dst, ws, d_results,
                                        plan->lanes_per_group, plan->lds_cells_per_lane,
-                                       st) != 0) {
+                                       plan->waves_per_simd, st) != 0) {
     set_error("LDS decode kernel launch failed");
     return SZ_ERROR_FAIL;
   }

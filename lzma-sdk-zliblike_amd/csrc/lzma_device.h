@@ -88,22 +88,30 @@ __host__ __device__ inline uint32_t num_probs(uint32_t lc, uint32_t lp) {
   return 1846u + (768u << (lc + lp));
 }
 
+// Explicit address spaces: LDS (3) for the lo table of the fast kernel, global
+// (1) for everything else.  Generic pointers would compile to flat_* memory
+// instructions, which count against both vmcnt and lgkmcnt -- every LDS wait
+// would then also drain the lane's outstanding global stores.
 #ifdef LZGPU_HOST_EMU
 typedef uint16_t lds_u16;
-typedef uint32_t lds_u32;
+typedef uint8_t gbyte;
+typedef uint16_t gu16;
+typedef uint32_t gu32;
 #else
 typedef __attribute__((address_space(3))) uint16_t lds_u16;
-typedef __attribute__((address_space(3))) uint32_t lds_u32;
+typedef __attribute__((address_space(1))) uint8_t gbyte;
+typedef __attribute__((address_space(1))) uint16_t gu16;
+typedef __attribute__((address_space(1))) uint32_t gu32;
 #endif
 
 // Per-lane decoder state (CLzmaDec fields, LzmaDec.h:50-69).  Lo = pointer type
-// of the lo table (uint16_t* global, or lds_u16* for LDS).
+// of the lo table (gu16* global, or lds_u16* for LDS).
 template <class Lo>
 struct LzStateT {
   uint32_t lc, lp, pb, dict_size;
   Lo lo;
-  uint16_t* hi;
-  uint8_t* dic;
+  gu16* hi;
+  gbyte* dic;
   uint64_t cap;   // dicBufSize
   uint64_t pos;   // dicPos
   uint32_t range, code;
@@ -129,19 +137,19 @@ __device__ __forceinline__ uint64_t ring_back(uint64_t pos, uint32_t dist, uint6
 // was issued.  Never loads an aligned word that lies wholly outside
 // [base, base+avail) (so it cannot fault past the end of an allocation).
 struct GlobalReader {
-  const uint32_t* wp;    // next aligned word to prefetch
-  const uint32_t* wend;  // one past the last word that holds a valid byte
+  const gu32* wp;    // next aligned word to prefetch
+  const gu32* wend;  // one past the last word that holds a valid byte
   uint64_t win;
   uint32_t nb;
   uint32_t pend;
   uint32_t idx;  // bytes consumed since init
 
-  __device__ __forceinline__ void init(const uint8_t* p, uint64_t avail) {
-    uintptr_t a = reinterpret_cast<uintptr_t>(p);
+  __device__ __forceinline__ void init(const gbyte* p, uint64_t avail) {
+    uintptr_t a = (uintptr_t)p;
     uintptr_t a0 = a & ~uintptr_t(3);
     uint32_t skip = uint32_t(a & 3);
-    wend = reinterpret_cast<const uint32_t*>((a + avail + 3) & ~uintptr_t(3));
-    const uint32_t* w = reinterpret_cast<const uint32_t*>(a0);
+    wend = (const gu32*)((a + avail + 3) & ~uintptr_t(3));
+    const gu32* w = (const gu32*)a0;
     idx = 0;
     if (avail == 0) {
       win = 0; nb = 0; pend = 0; wp = w; return;
@@ -222,12 +230,12 @@ struct Rc {
 // Copy n bytes of an LZ match: dic[pos..pos+n) = dic[from..], byte-serial
 // overlap semantics (rep0 < n replicates the period), ring wrap at cap.
 // Non-overlapping, non-wrapping spans go 8 bytes per round trip.
-__device__ __forceinline__ uint32_t lz_copy(uint8_t* dic, uint64_t pos, uint64_t from, uint32_t n,
+__device__ __forceinline__ uint32_t lz_copy(gbyte* dic, uint64_t pos, uint64_t from, uint32_t n,
                                             uint32_t dist, uint64_t cap) {
   uint32_t last = 0;
   if (from + n <= cap) {
-    uint8_t* d = dic + pos;
-    const uint8_t* s = dic + from;
+    gbyte* d = dic + pos;
+    const gbyte* s = dic + from;
     uint32_t i = 0;
     if (dist >= 8) {
       for (; i + 8 <= n; i += 8) {
@@ -263,7 +271,7 @@ template <class Lo, class Rd>
 __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
                                       uint32_t in_limit) {
   const Lo pr = s.lo;
-  uint16_t* const hi = s.hi;
+  gu16* const hi = s.hi;
   const uint32_t pb = s.pb;
   uint32_t st = s.st;
   uint32_t r0 = s.rep0, r1 = s.rep1, r2 = s.rep2, r3 = s.rep3;
@@ -272,7 +280,7 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
   const uint32_t o_rep0long = off_rep0long(pb), o_is_rep = off_is_rep(pb);
   const uint32_t o_slot = off_slot(pb), o_spec = off_spec(pb), o_align = off_align(pb);
   const uint32_t o_len = off_len(pb), o_replen = off_replen(pb), o_lit = off_lit(pb);
-  uint8_t* __restrict__ dic = s.dic;
+  gbyte* __restrict__ dic = s.dic;
   const uint64_t cap = s.cap;
   uint64_t pos = s.pos;
   uint32_t total = s.total;
@@ -460,10 +468,11 @@ __device__ __forceinline__ int lz_run_split(LzStateT<Lo>& s, uint64_t limit, Rd&
 
 enum : int { PROBE_SHORT = 0, PROBE_LIT = 1, PROBE_MATCH = 2, PROBE_REP = 3 };
 
+template <class BP>
 struct Probe {
   uint32_t range, code;
-  const uint8_t* in;
-  const uint8_t* end;
+  BP in;
+  BP end;
   __device__ __forceinline__ bool norm() {
     if (range < kTop) {
       if (in >= end) return false;
@@ -496,14 +505,14 @@ struct Probe {
 };
 
 // Would one more symbol decode from [in, in+n)?  (LzmaDec_TryDummy)
-template <class Lo>
-__device__ int lz_probe(const LzStateT<Lo>& s, const uint8_t* in, uint64_t n) {
+template <class Lo, class BP>
+__device__ int lz_probe(const LzStateT<Lo>& s, BP in, uint64_t n) {
   const Lo pr = s.lo;
   const uint32_t pb = s.pb;
   const uint32_t ps = s.total & ((1u << pb) - 1);
   uint32_t st = s.st, lcoder, hcoder, len = 0;
   int kind, b;
-  Probe t{s.range, s.code, in, in + n};
+  Probe<BP> t{s.range, s.code, in, in + n};
 #define LZ_PB(p) do { b = t.bit(p); if (b < 0) return PROBE_SHORT; } while (0)
   LZ_PB(pr + (st << pb) + ps);
   if (b == 0) {
@@ -635,7 +644,7 @@ __device__ __forceinline__ void lz_init_dic_state(LzStateT<Lo>& s, bool init_dic
 // present) never takes: its first need is a NEEDS_MORE_INPUT return.
 template <bool WithTemp, class Lo>
 __device__ __forceinline__ int lz_decode_to_dic(LzStateT<Lo>& s, uint64_t dic_limit,
-                                                const uint8_t* src, uint64_t& src_len, int fin,
+                                                const gbyte* src, uint64_t& src_len, int fin,
                                                 int& status) {
   uint64_t avail = src_len;
   src_len = 0;
@@ -695,7 +704,7 @@ __device__ __forceinline__ int lz_decode_to_dic(LzStateT<Lo>& s, uint64_t dic_li
       while (have < kLookahead && taken < avail) s.tmp[have++] = src[taken++];
       s.tmp_n = have;
       if (have < kLookahead || at_end_check) {
-        int k = lz_probe(s, s.tmp, have);
+        int k = lz_probe(s, (const uint8_t*)s.tmp, have);
         if (k == PROBE_SHORT) {
           src_len += taken;
           status = kStMoreInput;

@@ -14,4 +14,5 @@ extern "C" int lzgpu_launch_session(LzgpuSession* d_sess, uint32_t n, hipStream_
 extern "C" int lzgpu_launch_decode_lds(const LzmaGpuStreamDesc* d_descs, const uint32_t* d_order,
                                        uint32_t n, const uint8_t* d_src, uint8_t* d_dst,
                                        uint16_t* d_ws, LzmaGpuResult* d_results, uint32_t lanes,
-                                       uint32_t stride, hipStream_t stream);
+                                       uint32_t stride, uint32_t waves_per_simd,
+                                       hipStream_t stream);

@@ -31,7 +31,11 @@ __global__ void __launch_bounds__(64) lzgpu_decode_batch_kernel(
   results[id] = lane_decode(d, src, dst, ws);
 }
 
-__global__ void __launch_bounds__(64) lzgpu_decode_lds_kernel(
+// W = minimum waves per SIMD the register allocation must allow (the
+// planner's occupancy target; more resident waves hide the serial decode
+// chain of each stream better, at the price of register spills).
+template <int W>
+__global__ void __launch_bounds__(64, W) lzgpu_decode_lds_kernel(
     const LzmaGpuStreamDesc* __restrict__ descs, const uint32_t* __restrict__ order, uint32_t n,
     const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, uint16_t* __restrict__ ws,
     LzmaGpuResult* __restrict__ results, uint32_t stride) {
@@ -65,22 +69,35 @@ extern "C" int lzgpu_launch_decode_batch(const LzmaGpuStreamDesc* d_descs, const
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-extern "C" int lzgpu_launch_decode_lds(const LzmaGpuStreamDesc* d_descs, const uint32_t* d_order,
-                                       uint32_t n, const uint8_t* d_src, uint8_t* d_dst,
-                                       uint16_t* d_ws, LzmaGpuResult* d_results, uint32_t lanes,
-                                       uint32_t stride, hipStream_t stream) {
-  if (n == 0) return 0;
+template <int W>
+static int launch_lds(const LzmaGpuStreamDesc* d_descs, const uint32_t* d_order, uint32_t n,
+                      const uint8_t* d_src, uint8_t* d_dst, uint16_t* d_ws,
+                      LzmaGpuResult* d_results, uint32_t lanes, uint32_t stride,
+                      hipStream_t stream) {
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(lzgpu_decode_lds_kernel),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(lzgpu_decode_lds_kernel<W>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
   }
   const size_t lds = size_t(lanes) * stride * 2;
   const uint32_t grid = (n + lanes - 1) / lanes;
-  hipLaunchKernelGGL(lzgpu_decode_lds_kernel, dim3(grid), dim3(lanes), lds, stream, d_descs,
+  hipLaunchKernelGGL(lzgpu_decode_lds_kernel<W>, dim3(grid), dim3(lanes), lds, stream, d_descs,
                      d_order, n, d_src, d_dst, d_ws, d_results, stride);
   return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+extern "C" int lzgpu_launch_decode_lds(const LzmaGpuStreamDesc* d_descs, const uint32_t* d_order,
+                                       uint32_t n, const uint8_t* d_src, uint8_t* d_dst,
+                                       uint16_t* d_ws, LzmaGpuResult* d_results, uint32_t lanes,
+                                       uint32_t stride, uint32_t waves_per_simd,
+                                       hipStream_t stream) {
+  if (n == 0) return 0;
+  switch (waves_per_simd) {
+    case 8: return launch_lds<8>(d_descs, d_order, n, d_src, d_dst, d_ws, d_results, lanes, stride, stream);
+    case 6: return launch_lds<6>(d_descs, d_order, n, d_src, d_dst, d_ws, d_results, lanes, stride, stream);
+    default: return launch_lds<4>(d_descs, d_order, n, d_src, d_dst, d_ws, d_results, lanes, stride, stream);
+  }
 }
 
 extern "C" int lzgpu_launch_session(LzgpuSession* d_sess, uint32_t n, hipStream_t stream) {

@@ -46,15 +46,17 @@ __device__ __forceinline__ LzmaGpuResult lane_decode(const LzmaGpuStreamDesc& d,
       r.res = (d.props[0] > 40) ? kErrUnsupported : kErrMem;
       return r;
     }
-    Lz2StateT<uint16_t*> p;
-    uint16_t* lo = ws + d.probs_off;
-    r.res = lz2_init(p, d.props[0], lo, lo + lo_cells(4, 0, 4), dst + d.dst_off, d.dst_cap);
+    Lz2StateT<gu16*> p;
+    gu16* lo = (gu16*)(ws + d.probs_off);
+    r.res = lz2_init(p, d.props[0], lo, lo + lo_cells(4, 0, 4), (gbyte*)(dst + d.dst_off),
+                     d.dst_cap);
     if (r.res != kOk) return r;
     uint64_t sl = d.src_len;
     int status = kStNone;
     // the batch contract for an LZMA2 range is Lzma2Dec_DecodeToDic's own
     // result (NEEDS_MORE_INPUT stays SZ_OK); Lzma2Decode maps it to INPUT_EOF
-    int res = lz2_decode_to_dic(p, d.dst_cap, src + d.src_off, sl, d.finish_mode, status);
+    int res = lz2_decode_to_dic(p, d.dst_cap, (const gbyte*)(src + d.src_off), sl, d.finish_mode,
+                                status);
     r.res = res;
     r.status = status;
     r.dest_len = p.dec.pos;
@@ -65,16 +67,16 @@ __device__ __forceinline__ LzmaGpuResult lane_decode(const LzmaGpuStreamDesc& d,
     r.res = kErrInputEof;
     return r;
   }
-  LzStateT<uint16_t*> s;
+  LzStateT<gu16*> s;
   r.res = lz_props_parse(d.props, d.props_size, s.lc, s.lp, s.pb, s.dict_size);
   if (r.res != kOk) return r;
   if (d.probs_off == LZMA_GPU_NO_WORKSPACE) {
     r.res = kErrMem;
     return r;
   }
-  s.lo = ws + d.probs_off;
+  s.lo = (gu16*)(ws + d.probs_off);
   s.hi = s.lo + lo_cells(s.lc, s.lp, s.pb);
-  s.dic = dst + d.dst_off;
+  s.dic = (gbyte*)(dst + d.dst_off);
   s.cap = d.dst_cap;
   s.pos = 0;
   s.range = s.code = 0;
@@ -84,7 +86,8 @@ __device__ __forceinline__ LzmaGpuResult lane_decode(const LzmaGpuStreamDesc& d,
   lz_init_dic_state(s, true, true);
   uint64_t sl = d.src_len;
   int status = kStNone;
-  int res = lz_decode_to_dic<false>(s, d.dst_cap, src + d.src_off, sl, d.finish_mode, status);
+  int res = lz_decode_to_dic<false>(s, d.dst_cap, (const gbyte*)(src + d.src_off), sl,
+                                    d.finish_mode, status);
   if (res == kOk && status == kStMoreInput) res = kErrInputEof;
   r.res = res;
   r.status = status;
@@ -117,8 +120,8 @@ __device__ __forceinline__ LzmaGpuResult lane_decode_lds(const LzmaGpuStreamDesc
     return r;
   }
   s.lo = lo;
-  s.hi = ws + d.probs_off;
-  s.dic = dst + d.dst_off;
+  s.hi = (gu16*)(ws + d.probs_off);
+  s.dic = (gbyte*)(dst + d.dst_off);
   s.cap = d.dst_cap;
   s.pos = 0;
   s.range = s.code = 0;
@@ -128,7 +131,8 @@ __device__ __forceinline__ LzmaGpuResult lane_decode_lds(const LzmaGpuStreamDesc
   lz_init_dic_state(s, true, true);
   uint64_t sl = d.src_len;
   int status = kStNone;
-  int res = lz_decode_to_dic<false>(s, d.dst_cap, src + d.src_off, sl, d.finish_mode, status);
+  int res = lz_decode_to_dic<false>(s, d.dst_cap, (const gbyte*)(src + d.src_off), sl,
+                                    d.finish_mode, status);
   if (res == kOk && status == kStMoreInput) res = kErrInputEof;
   r.res = res;
   r.status = status;
@@ -140,14 +144,14 @@ __device__ __forceinline__ LzmaGpuResult lane_decode_lds(const LzmaGpuStreamDesc
 // One LzmaDec_DecodeToDic call on a device-resident decoder (compact layout in
 // q.probs: lo then hi, for the current lc/lp/pb).
 __device__ __forceinline__ void lane_session(LzgpuSession& q) {
-  LzStateT<uint16_t*> s;
+  LzStateT<gu16*> s;
   s.lc = q.lc;
   s.lp = q.lp;
   s.pb = q.pb;
   s.dict_size = q.dict_size;
-  s.lo = q.probs;
-  s.hi = q.probs + lo_cells(q.lc, q.lp, q.pb);
-  s.dic = q.dic;
+  s.lo = (gu16*)q.probs;
+  s.hi = s.lo + lo_cells(q.lc, q.lp, q.pb);
+  s.dic = (gbyte*)q.dic;
   s.cap = q.cap;
   s.pos = q.pos;
   s.range = q.range;
@@ -166,7 +170,7 @@ __device__ __forceinline__ void lane_session(LzgpuSession& q) {
   for (int i = 0; i < int(kLookahead); ++i) s.tmp[i] = q.tmp[i];
   uint64_t sl = q.in_len;
   int status = kStNone;
-  int res = lz_decode_to_dic<true>(s, q.dic_limit, q.in, sl, q.finish_mode, status);
+  int res = lz_decode_to_dic<true>(s, q.dic_limit, (const gbyte*)q.in, sl, q.finish_mode, status);
   q.pos = s.pos;
   q.range = s.range;
   q.code = s.code;

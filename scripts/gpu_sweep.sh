@@ -11,9 +11,10 @@ s=$?; echo "pytest exit $s"; tail -6 gpurun_out/${TAG}_pytest.log
 timeout -k 10 600 python bench.py --steps 5 --warmup 1 > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err
 s=$?; echo "bench exit $s"; cat gpurun_out/${TAG}_bench.json
 [ $s -eq 0 ] || exit $s
-for v in ${SWEEP_LANES:-4 8 32}; do
-  LZGPU_LANES=$v timeout -k 10 300 python bench.py --steps 5 --warmup 1 --no-cpu-baseline > gpurun_out/${TAG}_lanes$v.json 2>> gpurun_out/${TAG}_bench.err
-  s=$?; echo "lanes=$v exit $s: $(python -c "import json;d=json.load(open('gpurun_out/${TAG}_lanes$v.json'));print(d['value'], d['ms_per_step'], d['config']['kernel_plan'], d['verified'])")"
+for lv in ${SWEEP:-4:4 2:4 2:8 2:6 1:8 4:6 8:4}; do
+  v=${lv%%:*}; o=${lv##*:}
+  LZGPU_LANES=$v LZGPU_OCC=$o timeout -k 10 300 python bench.py --steps 5 --warmup 1 --no-cpu-baseline > gpurun_out/${TAG}_l${v}o${o}.json 2>> gpurun_out/${TAG}_bench.err
+  s=$?; echo "lanes=$v occ=$o exit $s: $(python -c "import json;d=json.load(open('gpurun_out/${TAG}_l${v}o${o}.json'));print(d['value'], d['ms_per_step'], d['config']['kernel_plan'], d['verified'])")"
   [ $s -eq 0 ] || exit $s
 done
 for cfg in ${SWEEP_CFGS:-cfg2}; do
