@@ -131,46 +131,61 @@ __device__ __forceinline__ uint64_t ring_back(uint64_t pos, uint32_t dist, uint6
 
 // ------------------------------------------------------------------ input readers
 
+#ifdef LZGPU_HOST_EMU
+static uint32_t g_lz_zero_word = 0;
+#else
+__device__ uint32_t g_lz_zero_word = 0;  // always-valid target for exhausted prefetches
+#endif
+
 // Prefetching reader over a lane's compressed bytes in global memory.  Holds up
 // to 7 bytes in `win` plus one prefetched aligned word in `pend`; the word is
 // merged only when fewer than 4 bytes remain, one full word after its load
-// was issued.  Never loads an aligned word that lies wholly outside
-// [base, base+avail) (so it cannot fault past the end of an allocation).
+// was issued.  The prefetch load is unconditional (an exhausted reader loads a
+// zero word from g_lz_zero_word instead), so the compiler can leave it in
+// flight until the merge instead of waiting on it at a control-flow join.
+// Never loads a word wholly outside [p, p+avail).
 struct GlobalReader {
-  const gu32* wp;    // next aligned word to prefetch
-  const gu32* wend;  // one past the last word that holds a valid byte
+  const gu32* wp;  // next aligned word to prefetch
+  uint32_t left;   // words with a valid byte still to prefetch
+  uint32_t nb;     // valid bytes in win
   uint64_t win;
-  uint32_t nb;
   uint32_t pend;
-  uint32_t idx;  // bytes consumed since init
+  uint32_t idx;    // bytes consumed since init
 
-  __device__ __forceinline__ void init(const gbyte* p, uint64_t avail) {
-    uintptr_t a = (uintptr_t)p;
-    uintptr_t a0 = a & ~uintptr_t(3);
-    uint32_t skip = uint32_t(a & 3);
-    wend = (const gu32*)((a + avail + 3) & ~uintptr_t(3));
-    const gu32* w = (const gu32*)a0;
-    idx = 0;
-    if (avail == 0) {
-      win = 0; nb = 0; pend = 0; wp = w; return;
-    }
-    win = uint64_t(*w >> (8 * skip));
-    nb = 4 - skip;
-    wp = w + 1;
-    pend = (wp < wend) ? *wp : 0u;
-    ++wp;
+  __device__ __forceinline__ uint32_t fetch() {
+    const gu32* a = left ? wp : (const gu32*)&g_lz_zero_word;
+    const uint32_t v = *a;
+    wp += left ? 1 : 0;
+    left -= left ? 1u : 0u;
+    return v;
   }
-  __device__ __forceinline__ uint32_t next() {
-    uint32_t b = uint32_t(win) & 0xFFu;
-    win >>= 8;
-    --nb;
-    ++idx;
+  __device__ __forceinline__ void init(const gbyte* p, uint64_t avail) {
+    const uintptr_t a = (uintptr_t)p;
+    const uintptr_t a0 = a & ~uintptr_t(3);
+    const uint32_t skip = uint32_t(a & 3);
+    const uint64_t words = avail ? (((a + avail + 3) & ~uintptr_t(3)) - a0) >> 2 : 0;
+    wp = (const gu32*)a0;
+    left = words > 0xFFFFFFF0ull ? 0xFFFFFFF0u : uint32_t(words);
+    idx = 0;
+    win = uint64_t(fetch() >> (8 * skip));
+    nb = avail ? 4 - skip : 0;
+    pend = fetch();
+  }
+  __device__ __forceinline__ uint32_t peek() const { return uint32_t(win) & 0xFFu; }
+  // consume the peeked byte when n is set
+  __device__ __forceinline__ void advance(bool n) {
+    win = n ? (win >> 8) : win;
+    nb -= n ? 1u : 0u;
+    idx += n ? 1u : 0u;
     if (nb < 4) {
       win |= uint64_t(pend) << (8 * nb);
       nb += 4;
-      pend = (wp < wend) ? *wp : 0u;
-      ++wp;
+      pend = fetch();
     }
+  }
+  __device__ __forceinline__ uint32_t next() {
+    const uint32_t b = peek();
+    advance(true);
     return b;
   }
 };
@@ -180,48 +195,55 @@ struct LocalReader {
   const uint8_t* p;
   uint32_t idx;
   __device__ __forceinline__ void init(const uint8_t* q) { p = q; idx = 0; }
+  __device__ __forceinline__ uint32_t peek() const { return p[idx]; }
+  __device__ __forceinline__ void advance(bool n) { idx += n ? 1u : 0u; }
   __device__ __forceinline__ uint32_t next() { return p[idx++]; }
 };
 
 // ------------------------------------------------------------------ range decoder
 
+// Branch-free primitives: lanes of a wave take different symbol paths, so
+// every decision is written as selects (v_cndmask) rather than if/else blocks.
 template <class Rd>
 struct Rc {
   uint32_t range, code;
   Rd* rd;
+  // NORMALIZE (LzmaDec.c:17): shift in one input byte when range < 2^24
   __device__ __forceinline__ void norm() {
-    if (range < kTop) {
-      range <<= 8;
-      code = (code << 8) | rd->next();
-    }
+    const bool n = range < kTop;
+    const uint32_t byte = rd->peek();
+    range = n ? (range << 8) : range;
+    code = n ? ((code << 8) | byte) : code;
+    rd->advance(n);
   }
-  // one adaptive decision on *prob (any address space)
+  // one adaptive decision on *prob (any address space), IF_BIT_0/UPDATE_0/1
   template <class P>
   __device__ __forceinline__ uint32_t bit(P prob) {
-    uint32_t p = *prob;
+    const uint32_t p = *prob;
     norm();
-    uint32_t bound = (range >> 11) * p;
-    if (code < bound) {
-      range = bound;
-      *prob = uint16_t(p + ((kProbOne - p) >> 5));
-      return 0;
-    }
-    range -= bound;
-    code -= bound;
-    *prob = uint16_t(p - (p >> 5));
-    return 1;
+    const uint32_t bound = (range >> 11) * p;
+    // mask arithmetic instead of selects: the compiler otherwise turns the
+    // two probability updates back into a divergent if/else
+    const uint32_t mask = 0u - uint32_t(code >= bound);
+    code -= bound & mask;
+    range = bound ^ ((bound ^ (range - bound)) & mask);
+    *prob = uint16_t(p + (((kProbOne - p) >> 5) & ~mask) - ((p >> 5) & mask));
+    return mask & 1u;
   }
-  template <class P>
-  __device__ __forceinline__ uint32_t tree(P probs, uint32_t bits) {
-    uint32_t m = 1, lim = 1u << bits;
-    while (m < lim) m = (m << 1) | bit(probs + m);
-    return m - lim;
+  // MSB-first bit tree of BITS levels (TREE_DECODE); returns [0, 1 << BITS)
+  template <int BITS, class P>
+  __device__ __forceinline__ uint32_t tree(P probs) {
+    uint32_t m = 1;
+#pragma unroll
+    for (int k = 0; k < BITS; ++k) m = (m << 1) | bit(probs + m);
+    return m - (1u << BITS);
   }
+  // fixed-probability bit in the reference's exact arithmetic (LzmaDec.c:325-334)
   __device__ __forceinline__ void direct(uint32_t& v) {
     norm();
     range >>= 1;
     code -= range;
-    uint32_t t = 0u - (code >> 31);
+    const uint32_t t = 0u - (code >> 31);
     v = (v << 1) + (t + 1u);
     code += range & t;
   }
@@ -301,18 +323,20 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
         lit += 768u * (((total & lp_mask) << lc) + (prev >> (8 - lc)));
       if (st < 7) {
         st = (st < 4) ? 0 : st - 3;
-        do sym = (sym << 1) | rc.bit(lit + sym); while (sym < 0x100);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) sym = (sym << 1) | rc.bit(lit + sym);
       } else {
         uint32_t mbyte = dic[ring_back(pos, r0, cap)];
         uint32_t offs = 0x100;
         st = (st < 10) ? st - 3 : st - 6;
-        do {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
           mbyte <<= 1;
-          uint32_t mbit = mbyte & offs;
-          uint32_t b = rc.bit(lit + offs + mbit + sym);
+          const uint32_t mbit = mbyte & offs;
+          const uint32_t b = rc.bit(lit + offs + mbit + sym);
           sym = (sym << 1) | b;
           offs = b ? (offs & mbit) : (offs & ~mbit);
-        } while (sym < 0x100);
+        }
       }
       prev = sym & 0xFFu;
       dic[pos++] = uint8_t(prev);
@@ -354,15 +378,15 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
       hcoder = 256;
     }
     if (!rc.bit(pr + lcoder))
-      len = rc.tree(pr + lcoder + 2 + (ps << 3), 3);
+      len = rc.template tree<3>(pr + lcoder + 2 + (ps << 3));
     else if (!rc.bit(pr + lcoder + 1))
-      len = 8 + rc.tree(pr + lcoder + 2 + (8u << pb) + (ps << 3), 3);
+      len = 8 + rc.template tree<3>(pr + lcoder + 2 + (8u << pb) + (ps << 3));
     else
-      len = 16 + rc.tree(hi + hcoder, 8);
+      len = 16 + rc.template tree<8>(hi + hcoder);
 
     if (st >= 12) {
       const uint32_t lstate = len < 4 ? len : 3;
-      uint32_t dist = rc.tree(pr + o_slot + (lstate << 6), 6);
+      uint32_t dist = rc.template tree<6>(pr + o_slot + (lstate << 6));
       if (dist >= 4) {
         const uint32_t slot = dist;
         uint32_t nbits = (slot >> 1) - 1;
