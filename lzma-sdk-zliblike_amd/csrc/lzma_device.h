@@ -202,19 +202,34 @@ struct LocalReader {
 
 // ------------------------------------------------------------------ range decoder
 
-// Branch-free primitives: lanes of a wave take different symbol paths, so
-// every decision is written as selects (v_cndmask) rather than if/else blocks.
+// Build-time code-shape switches (A/B'd on MI355X):
+//   LZGPU_NORM_BRANCHLESS  NORMALIZE as selects instead of a skip-able branch
+//   LZGPU_BIT_MASK         decision/update as mask arithmetic instead of if/else
+#ifndef LZGPU_NORM_BRANCHLESS
+#define LZGPU_NORM_BRANCHLESS 0
+#endif
+#ifndef LZGPU_BIT_MASK
+#define LZGPU_BIT_MASK 1
+#endif
+
 template <class Rd>
 struct Rc {
   uint32_t range, code;
   Rd* rd;
   // NORMALIZE (LzmaDec.c:17): shift in one input byte when range < 2^24
   __device__ __forceinline__ void norm() {
+#if LZGPU_NORM_BRANCHLESS
     const bool n = range < kTop;
     const uint32_t byte = rd->peek();
     range = n ? (range << 8) : range;
     code = n ? ((code << 8) | byte) : code;
     rd->advance(n);
+#else
+    if (range < kTop) {
+      range <<= 8;
+      code = (code << 8) | rd->next();
+    }
+#endif
   }
   // one adaptive decision on *prob (any address space), IF_BIT_0/UPDATE_0/1
   template <class P>
@@ -222,13 +237,25 @@ struct Rc {
     const uint32_t p = *prob;
     norm();
     const uint32_t bound = (range >> 11) * p;
-    // mask arithmetic instead of selects: the compiler otherwise turns the
-    // two probability updates back into a divergent if/else
+#if LZGPU_BIT_MASK
+    // mask arithmetic: lanes of a wave sit on different symbol paths, and the
+    // compiler otherwise turns the two updates into a divergent if/else
     const uint32_t mask = 0u - uint32_t(code >= bound);
     code -= bound & mask;
     range = bound ^ ((bound ^ (range - bound)) & mask);
     *prob = uint16_t(p + (((kProbOne - p) >> 5) & ~mask) - ((p >> 5) & mask));
     return mask & 1u;
+#else
+    if (code < bound) {
+      range = bound;
+      *prob = uint16_t(p + ((kProbOne - p) >> 5));
+      return 0;
+    }
+    range -= bound;
+    code -= bound;
+    *prob = uint16_t(p - (p >> 5));
+    return 1;
+#endif
   }
   // MSB-first bit tree of BITS levels (TREE_DECODE); returns [0, 1 << BITS)
   template <int BITS, class P>

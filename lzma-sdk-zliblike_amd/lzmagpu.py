@@ -14,7 +14,8 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "lib", "liblzmagpu.so")
+# LZGPU_LIB may name a code-shape variant build (lib/variants/, A/B runs only)
+LIB_PATH = os.environ.get("LZGPU_LIB") or os.path.join(HERE, "lib", "liblzmagpu.so")
 
 if not os.path.exists(LIB_PATH):
     raise ImportError(f"liblzmagpu.so not built ({LIB_PATH}); run __graft_entry__.build()")
