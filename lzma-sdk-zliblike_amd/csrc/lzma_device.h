@@ -209,7 +209,7 @@ struct LocalReader {
 #define LZGPU_NORM_BRANCHLESS 0
 #endif
 #ifndef LZGPU_BIT_MASK
-#define LZGPU_BIT_MASK 1
+#define LZGPU_BIT_MASK 0
 #endif
 
 template <class Rd>
