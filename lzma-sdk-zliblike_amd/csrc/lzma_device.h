@@ -104,6 +104,36 @@ typedef __attribute__((address_space(1))) uint16_t gu16;
 typedef __attribute__((address_space(1))) uint32_t gu32;
 #endif
 
+// Build-time code-shape switches (A/B'd on MI355X, see DESIGN.md §4):
+//   LZGPU_NORM_BRANCHLESS  NORMALIZE as selects instead of a skip-able branch
+//   LZGPU_BIT_MASK         decision/update as mask arithmetic instead of if/else
+#ifndef LZGPU_NORM_BRANCHLESS
+#define LZGPU_NORM_BRANCHLESS 0
+#endif
+#ifndef LZGPU_BIT_MASK
+#define LZGPU_BIT_MASK 0
+#endif
+//   LZGPU_TREE_PF      bit-trees read both children of the next level (one
+//                      32-bit read) while the current decision resolves
+//   LZGPU_MB_PF        the matched-literal byte dic[pos - rep0] is loaded as
+//                      soon as a match ends, not after the next IsMatch decision
+//   LZGPU_COPY_SHORT   overlapping matches (rep0 < 8) load the period once and
+//                      replicate it from registers instead of byte round trips
+//   LZGPU_READER16     input window refilled 16 bytes per load (one vmcnt drain
+//                      per 16 input bytes instead of per 4)
+#ifndef LZGPU_TREE_PF
+#define LZGPU_TREE_PF 0
+#endif
+#ifndef LZGPU_MB_PF
+#define LZGPU_MB_PF 0
+#endif
+#ifndef LZGPU_COPY_SHORT
+#define LZGPU_COPY_SHORT 0
+#endif
+#ifndef LZGPU_READER16
+#define LZGPU_READER16 0
+#endif
+
 // Per-lane decoder state (CLzmaDec fields, LzmaDec.h:50-69).  Lo = pointer type
 // of the lo table (gu16* global, or lds_u16* for LDS).
 template <class Lo>
@@ -131,10 +161,11 @@ __device__ __forceinline__ uint64_t ring_back(uint64_t pos, uint32_t dist, uint6
 
 // ------------------------------------------------------------------ input readers
 
+// always-valid, 16-byte aligned target for exhausted prefetches
 #ifdef LZGPU_HOST_EMU
-static uint32_t g_lz_zero_word = 0;
+alignas(16) static uint32_t g_lz_zero_word[4] = {0, 0, 0, 0};
 #else
-__device__ uint32_t g_lz_zero_word = 0;  // always-valid target for exhausted prefetches
+__device__ __attribute__((aligned(16))) uint32_t g_lz_zero_word[4] = {0, 0, 0, 0};
 #endif
 
 // Prefetching reader over a lane's compressed bytes in global memory.  Holds up
@@ -153,7 +184,7 @@ struct GlobalReader {
   uint32_t idx;    // bytes consumed since init
 
   __device__ __forceinline__ uint32_t fetch() {
-    const gu32* a = left ? wp : (const gu32*)&g_lz_zero_word;
+    const gu32* a = left ? wp : (const gu32*)g_lz_zero_word;
     const uint32_t v = *a;
     wp += left ? 1 : 0;
     left -= left ? 1u : 0u;
@@ -190,6 +221,91 @@ struct GlobalReader {
   }
 };
 
+// Same contract, 16-byte refills: `win` holds up to 8 bytes; `nxt` is the
+// next 16-byte aligned block (its low half is taken when win empties, the high
+// half 8 bytes later, and only then is the following block requested), so one
+// load and one drain per 16 input bytes.
+struct GlobalReader16 {
+  const gu32* wp;  // next 16-byte block to prefetch (as words)
+  uint32_t left;   // 16-byte blocks with a valid byte still to prefetch
+  uint32_t nb;     // valid bytes in win
+  uint32_t half;   // 0: nxt untouched, 1: nxt low half already taken
+  uint64_t win;
+  uint64_t nlo, nhi;
+  uint32_t idx;
+
+  __device__ __forceinline__ void fetch() {
+    // unconditional load (no phi on the loaded registers)
+    const gu32* a = left ? wp : (const gu32*)g_lz_zero_word;
+#ifdef LZGPU_HOST_EMU
+    nlo = uint64_t(a[0]) | (uint64_t(a[1]) << 32);
+    nhi = uint64_t(a[2]) | (uint64_t(a[3]) << 32);
+#else
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 v = *(const __attribute__((address_space(1))) u32x4*)a;
+    nlo = uint64_t(v.x) | (uint64_t(v.y) << 32);
+    nhi = uint64_t(v.z) | (uint64_t(v.w) << 32);
+#endif
+    wp += left ? 4 : 0;
+    left -= left ? 1u : 0u;
+  }
+  __device__ __forceinline__ void init(const gbyte* p, uint64_t avail) {
+    const uintptr_t a = (uintptr_t)p;
+    const uintptr_t a0 = a & ~uintptr_t(15);
+    const uint32_t skip = uint32_t(a & 15);
+    const uint64_t blocks = avail ? (((a + avail + 15) & ~uintptr_t(15)) - a0) >> 4 : 0;
+    wp = (const gu32*)a0;
+    left = blocks > 0xFFFFFFF0ull ? 0xFFFFFFF0u : uint32_t(blocks);
+    idx = 0;
+    fetch();  // first block: nlo/nhi
+    if (skip < 8) {
+      win = nlo >> (8 * skip);
+      nb = 8 - skip;
+      half = 1;
+    } else {
+      win = nhi >> (8 * (skip - 8));
+      nb = 16 - skip;
+      fetch();
+      half = 0;
+    }
+    if (!avail) nb = 0;
+  }
+  __device__ __forceinline__ uint32_t peek() const { return uint32_t(win) & 0xFFu; }
+  __device__ __forceinline__ void refill() {
+    if (half == 0) {
+      win = nlo;
+      half = 1;
+    } else {
+      win = nhi;
+      fetch();
+      half = 0;
+    }
+    nb = 8;
+  }
+  __device__ __forceinline__ void advance(bool n) {
+    if (n) {
+      win >>= 8;
+      --nb;
+      ++idx;
+      if (nb == 0) refill();
+    }
+  }
+  __device__ __forceinline__ uint32_t next() {
+    const uint32_t b = peek();
+    win >>= 8;
+    --nb;
+    ++idx;
+    if (nb == 0) refill();
+    return b;
+  }
+};
+
+#if LZGPU_READER16
+typedef GlobalReader16 BulkReader;
+#else
+typedef GlobalReader BulkReader;
+#endif
+
 // Reader over a lane-private byte array (the tempBuf path).
 struct LocalReader {
   const uint8_t* p;
@@ -202,14 +318,14 @@ struct LocalReader {
 
 // ------------------------------------------------------------------ range decoder
 
-// Build-time code-shape switches (A/B'd on MI355X, see DESIGN.md §4):
-//   LZGPU_NORM_BRANCHLESS  NORMALIZE as selects instead of a skip-able branch
-//   LZGPU_BIT_MASK         decision/update as mask arithmetic instead of if/else
-#ifndef LZGPU_NORM_BRANCHLESS
-#define LZGPU_NORM_BRANCHLESS 0
-#endif
-#ifndef LZGPU_BIT_MASK
-#define LZGPU_BIT_MASK 0
+// 32-bit view of a 16-bit cell pointer in the same address space
+#ifdef LZGPU_HOST_EMU
+__device__ __forceinline__ const uint32_t* wide(const uint16_t* p) { return (const uint32_t*)p; }
+__device__ __forceinline__ const uint32_t* wide(uint16_t* p) { return (const uint32_t*)p; }
+#else
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+__device__ __forceinline__ const lds_u32* wide(lds_u16* p) { return (const lds_u32*)p; }
+__device__ __forceinline__ const gu32* wide(gu16* p) { return (const gu32*)p; }
 #endif
 
 template <class Rd>
@@ -257,12 +373,40 @@ struct Rc {
     return 1;
 #endif
   }
+  // decision on an already-loaded probability value p, update stored to *prob
+  template <class P>
+  __device__ __forceinline__ uint32_t bit_v(uint32_t p, P prob) {
+    norm();
+    const uint32_t bound = (range >> 11) * p;
+    if (code < bound) {
+      range = bound;
+      *prob = uint16_t(p + ((kProbOne - p) >> 5));
+      return 0;
+    }
+    range -= bound;
+    code -= bound;
+    *prob = uint16_t(p - (p >> 5));
+    return 1;
+  }
   // MSB-first bit tree of BITS levels (TREE_DECODE); returns [0, 1 << BITS)
   template <int BITS, class P>
   __device__ __forceinline__ uint32_t tree(P probs) {
     uint32_t m = 1;
+#if LZGPU_TREE_PF
+    // probs must be 4-byte aligned: children 2m, 2m+1 form one 32-bit word
+    uint32_t p = probs[1];
+#pragma unroll
+    for (int k = 0; k < BITS; ++k) {
+      uint32_t pair = 0;
+      if (k + 1 < BITS) pair = *wide(probs + 2 * m);
+      const uint32_t b = bit_v(p, probs + m);
+      m = (m << 1) | b;
+      if (k + 1 < BITS) p = b ? (pair >> 16) : (pair & 0xFFFFu);
+    }
+#else
 #pragma unroll
     for (int k = 0; k < BITS; ++k) m = (m << 1) | bit(probs + m);
+#endif
     return m - (1u << BITS);
   }
   // fixed-probability bit in the reference's exact arithmetic (LzmaDec.c:325-334)
@@ -282,6 +426,23 @@ struct Rc {
 __device__ __forceinline__ uint32_t lz_copy(gbyte* dic, uint64_t pos, uint64_t from, uint32_t n,
                                             uint32_t dist, uint64_t cap) {
   uint32_t last = 0;
+#if LZGPU_COPY_SHORT
+  if (dist < 8 && dist < n && from + dist <= cap && from < pos) {
+    // overlapping: the output is the dist-byte period starting at `from`,
+    // repeated; load the period once, then stream it from registers
+    uint64_t per = 0;
+    for (uint32_t k = 0; k < dist; ++k) per |= uint64_t(dic[from + k]) << (8 * k);
+    gbyte* d = dic + pos;
+    uint32_t k = 0;
+    for (uint32_t i = 0; i < n; ++i) {
+      const uint32_t b = uint32_t(per >> (8 * k)) & 0xFFu;
+      d[i] = uint8_t(b);
+      last = b;
+      k = (k + 1 == dist) ? 0 : k + 1;
+    }
+    return last;
+  }
+#endif
   if (from + n <= cap) {
     gbyte* d = dic + pos;
     const gbyte* s = dic + from;
@@ -339,6 +500,10 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
   // previous byte (literal context), kept in a register
   uint32_t prev = 0;
   if (full != 0 || total != 0) prev = dic[(pos == 0 ? cap : pos) - 1];
+#if LZGPU_MB_PF
+  // byte at distance rep0, needed by a matched literal (state >= 7)
+  uint32_t mb_pf = (st >= 7) ? uint32_t(dic[ring_back(pos, r0, cap)]) : 0u;
+#endif
 
   do {
     const uint32_t ps = total & pb_mask;
@@ -350,10 +515,13 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
         lit += 768u * (((total & lp_mask) << lc) + (prev >> (8 - lc)));
       if (st < 7) {
         st = (st < 4) ? 0 : st - 3;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) sym = (sym << 1) | rc.bit(lit + sym);
+        sym = 0x100u | rc.template tree<8>(lit);
       } else {
+#if LZGPU_MB_PF
+        uint32_t mbyte = mb_pf;
+#else
         uint32_t mbyte = dic[ring_back(pos, r0, cap)];
+#endif
         uint32_t offs = 0x100;
         st = (st < 10) ? st - 3 : st - 6;
 #pragma unroll
@@ -382,6 +550,9 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
           dic[pos++] = uint8_t(prev);
           total++;
           st = (st < 7) ? 9 : 11;
+#if LZGPU_MB_PF
+          mb_pf = dic[ring_back(pos, r0, cap)];
+#endif
           continue;
         }
       } else {
@@ -467,6 +638,9 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
       len -= n;
       prev = lz_copy(dic, pos, from, n, r0, cap);
       pos += n;
+#if LZGPU_MB_PF
+      mb_pf = dic[ring_back(pos, r0, cap)];
+#endif
     }
   } while (pos < limit && rd.idx < in_limit);
 
@@ -743,7 +917,7 @@ __device__ __forceinline__ int lz_decode_to_dic(LzStateT<Lo>& s, uint64_t dic_li
         uint64_t lim = avail - kLookahead;
         in_limit = lim > 0xFFFFFFF0ull ? 0xFFFFFFF0u : uint32_t(lim);
       }
-      GlobalReader rd;
+      BulkReader rd;
       rd.init(src, avail);
       if (lz_run_split(s, dic_limit, rd, in_limit) != kOk) return kErrData;
       const uint32_t used = rd.idx;

@@ -16,10 +16,20 @@ import native
 EMU_SO = os.path.join(native.ROOT, "tests", "emu", "liblane_emu.so")
 
 
-@pytest.fixture(scope="module")
-def emu():
-    subprocess.run(["make", "-s", "-f", "tests/emu/Makefile"], cwd=native.ROOT, check=True)
-    lib = ctypes.CDLL(EMU_SO)
+# code-shape variants of lzma_device.h the GPU builds may use (see its flag block)
+EMU_VARIANTS = {
+    "default": "",
+    "all_on": "-DLZGPU_TREE_PF=1 -DLZGPU_MB_PF=1 -DLZGPU_COPY_SHORT=1 -DLZGPU_READER16=1 "
+              "-DLZGPU_NORM_BRANCHLESS=1 -DLZGPU_BIT_MASK=1",
+}
+
+
+@pytest.fixture(scope="module", params=sorted(EMU_VARIANTS))
+def emu(request):
+    out = EMU_SO if request.param == "default" else EMU_SO.replace(".so", f"_{request.param}.so")
+    subprocess.run(["make", "-s", "-f", "tests/emu/Makefile", f"EMU_OUT={out}",
+                    f"EMU_FLAGS={EMU_VARIANTS[request.param]}"], cwd=native.ROOT, check=True)
+    lib = ctypes.CDLL(out)
     lib.emu_decode_batch_lds.restype = None
     lib.emu_decode_batch_lds.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_char_p,
                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
@@ -77,7 +87,7 @@ def test_emu_golden_lzma_batch(emu, lds):
         srcs.append(s)
         off += len(s)
         doff += c["dest_cap"]
-    res, dst = run_batch(emu, items, b"".join(srcs) + b"\0" * 8, lds)
+    res, dst = run_batch(emu, items, b"".join(srcs) + b"\0" * 16, lds)
     bad = []
     for k, (i, c) in enumerate(cs):
         e = c["expect"]
@@ -95,7 +105,7 @@ def test_emu_golden_lzma2_batch(emu):
         s = G.case_input(d, c)
         items = [dict(src_off=0, src_len=len(s), dst_off=0, dst_cap=c["dest_cap"],
                       props=bytes([c["prop"]]), finish=c["finish"], kind=L.KIND_LZMA2)]
-        res, dst = run_batch(emu, items, s + b"\0" * 8)
+        res, dst = run_batch(emu, items, s + b"\0" * 16)
         e = c["expect"]
         got = (res[0].res, res[0].status, res[0].dest_len, res[0].src_len)
         assert got == (e["res"], e["status"], e["dest_len"], e["src_len"]), (i, c["note"])
@@ -156,7 +166,7 @@ def test_emu_fuzz_vs_oracle(emu, lds):
         exp.append(native.decode(orc, "orc", comp, props, cap, fin))
         off += len(comp)
         doff += cap
-    res, dst = run_batch(emu, items, b"".join(srcs) + b"\0" * 8, lds)
+    res, dst = run_batch(emu, items, b"".join(srcs) + b"\0" * 16, lds)
     for k in range(len(items)):
         got = (res[k].res, res[k].status, res[k].dest_len, res[k].src_len)
         out = dst[items[k]["dst_off"]:items[k]["dst_off"] + res[k].dest_len]
