@@ -125,13 +125,13 @@ typedef __attribute__((address_space(1))) uint32_t gu32;
 #define LZGPU_TREE_PF 0
 #endif
 #ifndef LZGPU_MB_PF
-#define LZGPU_MB_PF 0
+#define LZGPU_MB_PF 1
 #endif
 #ifndef LZGPU_COPY_SHORT
 #define LZGPU_COPY_SHORT 0
 #endif
 #ifndef LZGPU_READER16
-#define LZGPU_READER16 0
+#define LZGPU_READER16 1
 #endif
 
 // Per-lane decoder state (CLzmaDec fields, LzmaDec.h:50-69).  Lo = pointer type
