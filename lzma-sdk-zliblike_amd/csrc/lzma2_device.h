@@ -72,8 +72,8 @@ __device__ inline int lz2_header_byte(Lz2StateT<Lo>& p, uint32_t b) {
   return C2_ERROR;
 }
 
-// Lzma2Dec_DecodeToDic for one lane (src in global memory).
-template <class Lo>
+// Lzma2Dec_DecodeToDic for one lane (src in global memory); M = table placement.
+template <uint32_t M, class Lo>
 __device__ __forceinline__ int lz2_decode_to_dic(Lz2StateT<Lo>& p, uint64_t dic_limit,
                                                  const gbyte* src, uint64_t& src_len, int fin,
                                                  int& status) {
@@ -134,7 +134,7 @@ __device__ __forceinline__ int lz2_decode_to_dic(Lz2StateT<Lo>& p, uint64_t dic_
       if (in_cur > p.pack_left) in_cur = p.pack_left;
       // each chunk is one DecodeToDic call over all of its bytes: the
       // tempBuf continuation path is never taken (as in a one-call decode)
-      int res = lz_decode_to_dic<false>(p.dec, pos0 + out_cur, src, in_cur, cur_fin, status);
+      int res = lz_decode_to_dic<false, M>(p.dec, pos0 + out_cur, src, in_cur, cur_fin, status);
       src += in_cur;
       src_len += in_cur;
       p.pack_left -= uint32_t(in_cur);
@@ -155,9 +155,10 @@ __device__ __forceinline__ int lz2_decode_to_dic(Lz2StateT<Lo>& p, uint64_t dic_
 
 // Lzma2Dec_Init (Lzma2Dec.c:90-97) after Lzma2Dec_AllocateProbs(prop):
 // lc = 4, lp = 0, pb = 0 for the allocation; dictionary size from the prop.
-// lo must hold lo_cells(4, 0, 4) cells (the largest an LZMA2 chunk can ask for).
+// The tables must hold table_cells(4, 0, 4) cells in total (the largest an
+// LZMA2 chunk's props can ask for).
 template <class Lo>
-__device__ __forceinline__ int lz2_init(Lz2StateT<Lo>& p, uint32_t prop, Lo lo, gu16* hi,
+__device__ __forceinline__ int lz2_init(Lz2StateT<Lo>& p, uint32_t prop, Lo lo, gu16* gl,
                                         gbyte* dic, uint64_t cap) {
   if (prop > 40) return kErrUnsupported;
   uint32_t dict = (prop == 40) ? 0xFFFFFFFFu : ((2u | (prop & 1u)) << (prop / 2 + 11));
@@ -166,7 +167,7 @@ __device__ __forceinline__ int lz2_init(Lz2StateT<Lo>& p, uint32_t prop, Lo lo, 
   p.dec.pb = 0;
   p.dec.dict_size = dict < 4096 ? 4096 : dict;
   p.dec.lo = lo;
-  p.dec.hi = hi;
+  p.dec.gl = gl;
   p.dec.dic = dic;
   p.dec.cap = cap;
   p.dec.pos = 0;

@@ -649,7 +649,7 @@ static uint64_t plan_workspace(LzmaGpuStreamDesc* descs, size_t n, std::vector<u
       uint32_t lc, lp, pb, dict;
       if (lzgpu::lz_props_parse(d.props, d.props_size, lc, lp, pb, dict) == SZ_OK) {
         np = lzgpu::table_cells(lc, lp, pb);
-        if (lo_w) (*lo_w)[i] = lzgpu::lo_cells(lc, lp, pb);
+        if (lo_w) (*lo_w)[i] = lzgpu::make_layout(lc, lp, pb, LZGPU_LDS_MASK).lds_cells;
       }
     }
     d.probs_off = off;

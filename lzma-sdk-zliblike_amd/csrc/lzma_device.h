@@ -57,36 +57,78 @@ constexpr uint32_t kLenDone = 274u;   // kMatchSpecLenStart
 
 // ------------------------------------------------------------------ compact layout
 
-// Section offsets (in 16-bit cells) of the lo table for posState count P = 1 << pb:
-//   IsMatch[12P] | IsRep0Long[12P] | IsRep[12] IsRepG0[12] IsRepG1[12] IsRepG2[12] |
-//   PosSlot[4][64] | SpecPos[114] | Align[16] | Len{choice,choice2,low[P][8],mid[P][8]} |
-//   RepLen{same} | Literal[0x300 << (lc+lp)]
-// hi table: LenHigh[256] | RepLenHigh[256].
-__host__ __device__ __forceinline__ uint32_t off_rep0long(uint32_t pb) { return 12u << pb; }
-__host__ __device__ __forceinline__ uint32_t off_is_rep(uint32_t pb) { return 24u << pb; }
-__host__ __device__ __forceinline__ uint32_t off_slot(uint32_t pb) { return (24u << pb) + 48u; }
-__host__ __device__ __forceinline__ uint32_t off_spec(uint32_t pb) { return (24u << pb) + 304u; }
-__host__ __device__ __forceinline__ uint32_t off_align(uint32_t pb) { return (24u << pb) + 418u; }
-__host__ __device__ __forceinline__ uint32_t off_len(uint32_t pb) { return (24u << pb) + 434u; }
-__host__ __device__ __forceinline__ uint32_t len_coder_cells(uint32_t pb) { return 2u + (16u << pb); }
-__host__ __device__ __forceinline__ uint32_t off_replen(uint32_t pb) {
-  return off_len(pb) + len_coder_cells(pb);
+// The probability table is stored as sections (cells = 16-bit probabilities,
+// P = 1 << pb reachable posStates instead of the reference's fixed 16):
+enum : uint32_t {
+  S_MATCH,   // IsMatch[12][P]
+  S_REP0L,   // IsRep0Long[12][P]
+  S_REP,     // IsRep[12] IsRepG0[12] IsRepG1[12] IsRepG2[12]
+  S_LEN,     // Len: choice, choice2, low[P][8], mid[P][8]
+  S_REPLEN,  // RepLen: same
+  S_SLOT,    // PosSlot[4][64]
+  S_SPEC,    // SpecPos[114]
+  S_ALIGN,   // Align[16]
+  S_LITP,    // literal trees, plain part: [ctx][0x100]
+  S_LITM,    // literal trees, matched part: [ctx][0x200] (reference offsets 0x100..0x2FF)
+  S_LENHI,   // LenHigh[256] | RepLenHigh[256]
+  S_NSEC
+};
+
+__host__ __device__ __forceinline__ uint32_t sec_cells(uint32_t sec, uint32_t lc, uint32_t lp,
+                                                       uint32_t pb) {
+  switch (sec) {
+    case S_MATCH: case S_REP0L: return 12u << pb;
+    case S_REP: return 48u;
+    case S_LEN: case S_REPLEN: return 2u + (16u << pb);
+    case S_SLOT: return 256u;
+    case S_SPEC: return 114u;
+    case S_ALIGN: return 16u;
+    case S_LITP: return 256u << (lc + lp);
+    case S_LITM: return 512u << (lc + lp);
+    default: return 512u;  // S_LENHI
+  }
 }
-__host__ __device__ __forceinline__ uint32_t off_lit(uint32_t pb) {
-  return off_len(pb) + 2u * len_coder_cells(pb);
+
+// Section placement: bit s of `lds_mask` set = section s lives in the lane's
+// LDS slice, otherwise in its global workspace slice (mask 0: all global).
+// Offsets are assigned in section order within each of the two tables.
+struct Layout {
+  uint32_t o[S_NSEC];
+  uint32_t lds_cells, glb_cells;
+};
+__host__ __device__ __forceinline__ Layout make_layout(uint32_t lc, uint32_t lp, uint32_t pb,
+                                                       uint32_t lds_mask) {
+  Layout L;
+  uint32_t a = 0, b = 0;
+  for (uint32_t sec = 0; sec < S_NSEC; ++sec) {
+    const uint32_t n = sec_cells(sec, lc, lp, pb);
+    if ((lds_mask >> sec) & 1u) {
+      L.o[sec] = a;
+      a += n;
+    } else {
+      L.o[sec] = b;
+      b += n;
+    }
+  }
+  L.lds_cells = a;
+  L.glb_cells = b;
+  return L;
 }
-__host__ __device__ __forceinline__ uint32_t lo_cells(uint32_t lc, uint32_t lp, uint32_t pb) {
-  return off_lit(pb) + (768u << (lc + lp));
-}
-constexpr uint32_t kHiCells = 512u;
+// whole table (all sections): 56P + 950 + 0x300 << (lc+lp) cells
 __host__ __device__ __forceinline__ uint32_t table_cells(uint32_t lc, uint32_t lp, uint32_t pb) {
-  return lo_cells(lc, lp, pb) + kHiCells;
+  return (56u << pb) + 950u + (768u << (lc + lp));
 }
 // reference numProbs (LzmaDec.c:110): what LzmaDec_AllocateProbs allocates;
-// table_cells() <= num_probs() for every pb <= 4.
+// table_cells() <= num_probs() for every pb <= 4 (equal at pb = 4).
 __host__ __device__ inline uint32_t num_probs(uint32_t lc, uint32_t lp) {
   return 1846u + (768u << (lc + lp));
 }
+
+// Placement used by the fast kernel (build-time; A/B'd on MI355X): default =
+// everything in LDS except the rarely used LenHigh trees.
+#ifndef LZGPU_LDS_MASK
+#define LZGPU_LDS_MASK 0x3FFu
+#endif
 
 // Explicit address spaces: LDS (3) for the lo table of the fast kernel, global
 // (1) for everything else.  Generic pointers would compile to flat_* memory
@@ -134,13 +176,14 @@ typedef __attribute__((address_space(1))) uint32_t gu32;
 #define LZGPU_READER16 1
 #endif
 
-// Per-lane decoder state (CLzmaDec fields, LzmaDec.h:50-69).  Lo = pointer type
-// of the lo table (gu16* global, or lds_u16* for LDS).
+// Per-lane decoder state (CLzmaDec fields, LzmaDec.h:50-69).  lo = the LDS
+// table (pointer type Lo: lds_u16*; or gu16* aliasing gl when everything is
+// global), gl = the global table.
 template <class Lo>
 struct LzStateT {
   uint32_t lc, lp, pb, dict_size;
   Lo lo;
-  gu16* hi;
+  gu16* gl;
   gbyte* dic;
   uint64_t cap;   // dicBufSize
   uint64_t pos;   // dicPos
@@ -153,6 +196,24 @@ struct LzStateT {
   uint32_t need_rc_init, need_state_init;
   uint32_t tmp_n;
   uint8_t tmp[kLookahead];
+};
+
+// Section accessor for placement mask M (compile-time): at<S>(i) is a pointer to
+// cell i of section S in whichever table holds it.
+template <uint32_t M, class Lo>
+struct Tab {
+  Lo lo;
+  gu16* gl;
+  Layout L;
+  __device__ __forceinline__ Tab(const LzStateT<Lo>& s)
+      : lo(s.lo), gl(s.gl), L(make_layout(s.lc, s.lp, s.pb, M)) {}
+  template <uint32_t S>
+  __device__ __forceinline__ auto at(uint32_t i) const {
+    if constexpr (((M >> S) & 1u) != 0u)
+      return lo + (L.o[S] + i);
+    else
+      return gl + (L.o[S] + i);
+  }
 };
 
 __device__ __forceinline__ uint64_t ring_back(uint64_t pos, uint32_t dist, uint64_t cap) {
@@ -474,22 +535,38 @@ __device__ __forceinline__ uint32_t lz_copy(gbyte* dic, uint64_t pos, uint64_t f
 
 // ------------------------------------------------------------------ symbol loop
 
+// Literal-tree cell for reference literal offset `rel` (0..0x2FF) of context ctx:
+// plain part for rel < 0x100, matched part above.  Both parts in LDS (or both
+// global) -> a branch-free offset select; split placement -> a real branch.
+template <uint32_t M, class Lo, class Rd>
+__device__ __forceinline__ uint32_t lit_bit(Rc<Rd>& rc, const Tab<M, Lo>& T, uint32_t ctx,
+                                            uint32_t offs_mbit, uint32_t sym) {
+  constexpr bool p_lds = ((M >> S_LITP) & 1u) != 0u, m_lds = ((M >> S_LITM) & 1u) != 0u;
+  if constexpr (p_lds == m_lds) {
+    const uint32_t rel = offs_mbit ? (T.L.o[S_LITM] + (ctx << 9) + offs_mbit - 0x100u)
+                                   : (T.L.o[S_LITP] + (ctx << 8));
+    if constexpr (p_lds)
+      return rc.bit(T.lo + (rel + sym));
+    else
+      return rc.bit(T.gl + (rel + sym));
+  } else {
+    if (offs_mbit) return rc.bit(T.template at<S_LITM>((ctx << 9) + offs_mbit - 0x100u + sym));
+    return rc.bit(T.template at<S_LITP>((ctx << 8) + sym));
+  }
+}
+
 // Decode symbols until pos reaches `limit` or the reader index reaches
 // `in_limit` (checked after each whole symbol; the first is always decoded).
 // State is written back only on success, as LzmaDec_DecodeReal does.
-template <class Lo, class Rd>
+template <uint32_t M, class Lo, class Rd>
 __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
                                       uint32_t in_limit) {
-  const Lo pr = s.lo;
-  gu16* const hi = s.hi;
+  const Tab<M, Lo> T(s);
   const uint32_t pb = s.pb;
   uint32_t st = s.st;
   uint32_t r0 = s.rep0, r1 = s.rep1, r2 = s.rep2, r3 = s.rep3;
   const uint32_t pb_mask = (1u << pb) - 1, lp_mask = (1u << s.lp) - 1;
   const uint32_t lc = s.lc;
-  const uint32_t o_rep0long = off_rep0long(pb), o_is_rep = off_is_rep(pb);
-  const uint32_t o_slot = off_slot(pb), o_spec = off_spec(pb), o_align = off_align(pb);
-  const uint32_t o_len = off_len(pb), o_replen = off_replen(pb), o_lit = off_lit(pb);
   gbyte* __restrict__ dic = s.dic;
   const uint64_t cap = s.cap;
   uint64_t pos = s.pos;
@@ -507,15 +584,14 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
 
   do {
     const uint32_t ps = total & pb_mask;
-    uint32_t lcoder, hcoder;
-    if (!rc.bit(pr + (st << pb) + ps)) {
-      Lo lit = pr + o_lit;
+    uint32_t lcoder_is_rep;
+    if (!rc.bit(T.template at<S_MATCH>((st << pb) + ps))) {
       uint32_t sym = 1;
-      if (full != 0 || total != 0)
-        lit += 768u * (((total & lp_mask) << lc) + (prev >> (8 - lc)));
+      uint32_t ctx = 0;
+      if (full != 0 || total != 0) ctx = ((total & lp_mask) << lc) + (prev >> (8 - lc));
       if (st < 7) {
         st = (st < 4) ? 0 : st - 3;
-        sym = 0x100u | rc.template tree<8>(lit);
+        sym = 0x100u | rc.template tree<8>(T.template at<S_LITP>(ctx << 8));
       } else {
 #if LZGPU_MB_PF
         uint32_t mbyte = mb_pf;
@@ -528,7 +604,7 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
         for (int k = 0; k < 8; ++k) {
           mbyte <<= 1;
           const uint32_t mbit = mbyte & offs;
-          const uint32_t b = rc.bit(lit + offs + mbit + sym);
+          const uint32_t b = lit_bit(rc, T, ctx, offs + mbit, sym);
           sym = (sym << 1) | b;
           offs = b ? (offs & mbit) : (offs & ~mbit);
         }
@@ -538,14 +614,13 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
       total++;
       continue;
     }
-    if (!rc.bit(pr + o_is_rep + st)) {
+    if (!rc.bit(T.template at<S_REP>(st))) {
       st += 12;
-      lcoder = o_len;
-      hcoder = 0;
+      lcoder_is_rep = 0;
     } else {
       if (full == 0 && total == 0) return kErrData;
-      if (!rc.bit(pr + o_is_rep + 12 + st)) {
-        if (!rc.bit(pr + o_rep0long + (st << pb) + ps)) {
+      if (!rc.bit(T.template at<S_REP>(12 + st))) {
+        if (!rc.bit(T.template at<S_REP0L>((st << pb) + ps))) {
           prev = dic[ring_back(pos, r0, cap)];
           dic[pos++] = uint8_t(prev);
           total++;
@@ -557,10 +632,10 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
         }
       } else {
         uint32_t dist;
-        if (!rc.bit(pr + o_is_rep + 24 + st)) {
+        if (!rc.bit(T.template at<S_REP>(24 + st))) {
           dist = r1;
         } else {
-          if (!rc.bit(pr + o_is_rep + 36 + st)) {
+          if (!rc.bit(T.template at<S_REP>(36 + st))) {
             dist = r2;
           } else {
             dist = r3;
@@ -572,29 +647,37 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
         r0 = dist;
       }
       st = (st < 7) ? 8 : 11;
-      lcoder = o_replen;
-      hcoder = 256;
+      lcoder_is_rep = 1;
     }
-    if (!rc.bit(pr + lcoder))
-      len = rc.template tree<3>(pr + lcoder + 2 + (ps << 3));
-    else if (!rc.bit(pr + lcoder + 1))
-      len = 8 + rc.template tree<3>(pr + lcoder + 2 + (8u << pb) + (ps << 3));
-    else
-      len = 16 + rc.template tree<8>(hi + hcoder);
+    {
+      // length coder of this match kind (LzmaDec.c:261-292)
+      const uint32_t lsec_o = lcoder_is_rep ? T.L.o[S_REPLEN] : T.L.o[S_LEN];
+      static_assert(((M >> S_LEN) & 1u) == ((M >> S_REPLEN) & 1u), "Len/RepLen placement");
+      constexpr bool len_lds = ((M >> S_LEN) & 1u) != 0u;
+      auto lbase = [&]() {
+        if constexpr (len_lds) return T.lo + lsec_o; else return T.gl + lsec_o;
+      }();
+      if (!rc.bit(lbase))
+        len = rc.template tree<3>(lbase + 2 + (ps << 3));
+      else if (!rc.bit(lbase + 1))
+        len = 8 + rc.template tree<3>(lbase + 2 + (8u << pb) + (ps << 3));
+      else
+        len = 16 + rc.template tree<8>(T.template at<S_LENHI>(lcoder_is_rep << 8));
+    }
 
     if (st >= 12) {
       const uint32_t lstate = len < 4 ? len : 3;
-      uint32_t dist = rc.template tree<6>(pr + o_slot + (lstate << 6));
+      uint32_t dist = rc.template tree<6>(T.template at<S_SLOT>(lstate << 6));
       if (dist >= 4) {
         const uint32_t slot = dist;
         uint32_t nbits = (slot >> 1) - 1;
         dist = 2 | (slot & 1);
         if (slot < 14) {
           dist <<= nbits;
-          Lo sp = pr + o_spec + dist - slot - 1;
           uint32_t mask = 1, node = 1;
+          const uint32_t sp = dist - slot - 1;
           do {
-            uint32_t b = rc.bit(sp + node);
+            uint32_t b = rc.bit(T.template at<S_SPEC>(sp + node));
             node = (node << 1) | b;
             dist |= b ? mask : 0u;
             mask <<= 1;
@@ -606,7 +689,7 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
           uint32_t node = 1;
 #pragma unroll
           for (uint32_t k = 0; k < 4; ++k) {
-            uint32_t b = rc.bit(pr + o_align + node);
+            uint32_t b = rc.bit(T.template at<S_ALIGN>(node));
             node = (node << 1) | b;
             dist |= b << k;
           }
@@ -672,7 +755,7 @@ __device__ __forceinline__ void lz_flush_pending(LzStateT<Lo>& s, uint64_t limit
   }
 }
 
-template <class Lo, class Rd>
+template <uint32_t M, class Lo, class Rd>
 __device__ __forceinline__ int lz_run_split(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
                                             uint32_t in_limit) {
   do {
@@ -681,7 +764,7 @@ __device__ __forceinline__ int lz_run_split(LzStateT<Lo>& s, uint64_t limit, Rd&
       uint32_t left = s.dict_size - s.total;
       if (limit - s.pos > left) lim = s.pos + left;
     }
-    if (lz_run(s, lim, rd, in_limit) != kOk) return kErrData;
+    if (lz_run<M>(s, lim, rd, in_limit) != kOk) return kErrData;
     if (s.total >= s.dict_size) s.full = s.dict_size;
     lz_flush_pending(s, limit);
   } while (s.pos < limit && rd.idx < in_limit && s.pending < kLenDone);
@@ -730,26 +813,25 @@ struct Probe {
 };
 
 // Would one more symbol decode from [in, in+n)?  (LzmaDec_TryDummy)
-template <class Lo, class BP>
+template <uint32_t M, class Lo, class BP>
 __device__ int lz_probe(const LzStateT<Lo>& s, BP in, uint64_t n) {
-  const Lo pr = s.lo;
+  const Tab<M, Lo> T(s);
   const uint32_t pb = s.pb;
   const uint32_t ps = s.total & ((1u << pb) - 1);
-  uint32_t st = s.st, lcoder, hcoder, len = 0;
+  uint32_t st = s.st, is_rep, len = 0;
   int kind, b;
   Probe<BP> t{s.range, s.code, in, in + n};
 #define LZ_PB(p) do { b = t.bit(p); if (b < 0) return PROBE_SHORT; } while (0)
-  LZ_PB(pr + (st << pb) + ps);
+  LZ_PB(T.template at<S_MATCH>((st << pb) + ps));
   if (b == 0) {
-    Lo lit = pr + off_lit(pb);
-    uint32_t sym = 1;
+    uint32_t sym = 1, ctx = 0;
     if (s.full != 0 || s.total != 0) {
       uint32_t prev = s.dic[(s.pos == 0 ? s.cap : s.pos) - 1];
-      lit += 768u * (((s.total & ((1u << s.lp) - 1)) << s.lc) + (prev >> (8 - s.lc)));
+      ctx = ((s.total & ((1u << s.lp) - 1)) << s.lc) + (prev >> (8 - s.lc));
     }
     if (st < 7) {
       while (sym < 0x100) {
-        LZ_PB(lit + sym);
+        LZ_PB(T.template at<S_LITP>((ctx << 8) + sym));
         sym = (sym << 1) | uint32_t(b);
       }
     } else {
@@ -757,55 +839,63 @@ __device__ int lz_probe(const LzStateT<Lo>& s, BP in, uint64_t n) {
       uint32_t offs = 0x100;
       while (sym < 0x100) {
         mbyte <<= 1;
-        uint32_t mbit = mbyte & offs;
-        LZ_PB(lit + offs + mbit + sym);
+        const uint32_t mbit = mbyte & offs;
+        if (offs + mbit)
+          LZ_PB(T.template at<S_LITM>((ctx << 9) + offs + mbit - 0x100u + sym));
+        else
+          LZ_PB(T.template at<S_LITP>((ctx << 8) + sym));
         sym = (sym << 1) | uint32_t(b);
         offs = b ? (offs & mbit) : (offs & ~mbit);
       }
     }
     kind = PROBE_LIT;
   } else {
-    LZ_PB(pr + off_is_rep(pb) + st);
+    LZ_PB(T.template at<S_REP>(st));
     if (b == 0) {
       st = 0;
-      lcoder = off_len(pb);
-      hcoder = 0;
+      is_rep = 0;
       kind = PROBE_MATCH;
     } else {
       kind = PROBE_REP;
-      LZ_PB(pr + off_is_rep(pb) + 12 + st);
+      LZ_PB(T.template at<S_REP>(12 + st));
       if (b == 0) {
-        LZ_PB(pr + off_rep0long(pb) + (st << pb) + ps);
+        LZ_PB(T.template at<S_REP0L>((st << pb) + ps));
         if (b == 0) return t.norm() ? PROBE_REP : PROBE_SHORT;
       } else {
-        LZ_PB(pr + off_is_rep(pb) + 24 + st);
-        if (b != 0) LZ_PB(pr + off_is_rep(pb) + 36 + st);
+        LZ_PB(T.template at<S_REP>(24 + st));
+        if (b != 0) LZ_PB(T.template at<S_REP>(36 + st));
       }
       st = 12;
-      lcoder = off_replen(pb);
-      hcoder = 256;
+      is_rep = 1;
     }
-    LZ_PB(pr + lcoder);
+    const uint32_t lo_off = is_rep ? T.L.o[S_REPLEN] : T.L.o[S_LEN];
+    auto lbase = [&]() {
+      if constexpr (((M >> S_LEN) & 1u) != 0u) return T.lo + lo_off; else return T.gl + lo_off;
+    }();
+    LZ_PB(lbase);
     if (b == 0) {
-      if (!t.tree(pr + lcoder + 2 + (ps << 3), 3, len)) return PROBE_SHORT;
+      if (!t.tree(lbase + 2 + (ps << 3), 3, len)) return PROBE_SHORT;
     } else {
-      LZ_PB(pr + lcoder + 1);
+      LZ_PB(lbase + 1);
       if (b == 0) {
-        if (!t.tree(pr + lcoder + 2 + (8u << pb) + (ps << 3), 3, len)) return PROBE_SHORT;
+        if (!t.tree(lbase + 2 + (8u << pb) + (ps << 3), 3, len)) return PROBE_SHORT;
         len += 8;
       } else {
-        if (!t.tree(s.hi + hcoder, 8, len)) return PROBE_SHORT;
+        if (!t.tree(T.template at<S_LENHI>(is_rep << 8), 8, len)) return PROBE_SHORT;
         len += 16;
       }
     }
     if (st < 4) {
       uint32_t slot;
-      if (!t.tree(pr + off_slot(pb) + ((len < 4 ? len : 3) << 6), 6, slot)) return PROBE_SHORT;
+      if (!t.tree(T.template at<S_SLOT>((len < 4 ? len : 3) << 6), 6, slot)) return PROBE_SHORT;
       if (slot >= 4) {
         uint32_t nbits = (slot >> 1) - 1, node = 1;
-        Lo base;
         if (slot < 14) {
-          base = pr + off_spec(pb) + ((2u | (slot & 1)) << nbits) - slot - 1;
+          const uint32_t sp = ((2u | (slot & 1)) << nbits) - slot - 1;
+          do {
+            LZ_PB(T.template at<S_SPEC>(sp + node));
+            node = (node << 1) | uint32_t(b);
+          } while (--nbits != 0);
         } else {
           nbits -= 4;
           do {
@@ -813,13 +903,12 @@ __device__ int lz_probe(const LzStateT<Lo>& s, BP in, uint64_t n) {
             t.range >>= 1;
             t.code -= t.range & (((t.code - t.range) >> 31) - 1);
           } while (--nbits != 0);
-          base = pr + off_align(pb);
           nbits = 4;
+          do {
+            LZ_PB(T.template at<S_ALIGN>(node));
+            node = (node << 1) | uint32_t(b);
+          } while (--nbits != 0);
         }
-        do {
-          LZ_PB(base + node);
-          node = (node << 1) | uint32_t(b);
-        } while (--nbits != 0);
       }
     }
   }
@@ -829,22 +918,17 @@ __device__ int lz_probe(const LzStateT<Lo>& s, BP in, uint64_t n) {
 
 // ------------------------------------------------------------------ init + driver
 
-// All cells to 1024 (LzmaDec_InitStateReal, LzmaDec.c:707-717).  lo and hi
-// start 4-byte aligned; stores go two cells at a time.
-template <class Lo>
-__device__ __forceinline__ void fill_prob_init(Lo p, uint32_t n) {
-  uint32_t i = 0;
-  for (; i + 2 <= n; i += 2) {
-    p[i] = uint16_t(kProbInit);
-    p[i + 1] = uint16_t(kProbInit);
-  }
-  if (i < n) p[i] = uint16_t(kProbInit);
+// All cells to 1024 (LzmaDec_InitStateReal, LzmaDec.c:707-717), both tables.
+template <class P>
+__device__ __forceinline__ void fill_prob_init(P p, uint32_t n) {
+  for (uint32_t i = 0; i < n; ++i) p[i] = uint16_t(kProbInit);
 }
 
-template <class Lo>
+template <uint32_t M, class Lo>
 __device__ __forceinline__ void lz_init_state_real(LzStateT<Lo>& s) {
-  fill_prob_init(s.lo, lo_cells(s.lc, s.lp, s.pb));
-  fill_prob_init(s.hi, kHiCells);
+  const Layout L = make_layout(s.lc, s.lp, s.pb, M);
+  if constexpr (M != 0u) fill_prob_init(s.lo, L.lds_cells);
+  fill_prob_init(s.gl, L.glb_cells);
   s.rep0 = s.rep1 = s.rep2 = s.rep3 = 1;
   s.st = 0;
   s.need_state_init = 0;
@@ -867,7 +951,7 @@ __device__ __forceinline__ void lz_init_dic_state(LzStateT<Lo>& s, bool init_dic
 // LzmaDec_DecodeToDic for one lane.  src is global memory.  WithTemp = false
 // drops the tempBuf continuation path, which a one-call decode (all input
 // present) never takes: its first need is a NEEDS_MORE_INPUT return.
-template <bool WithTemp, class Lo>
+template <bool WithTemp, uint32_t M, class Lo>
 __device__ __forceinline__ int lz_decode_to_dic(LzStateT<Lo>& s, uint64_t dic_limit,
                                                 const gbyte* src, uint64_t& src_len, int fin,
                                                 int& status) {
@@ -898,12 +982,12 @@ __device__ __forceinline__ int lz_decode_to_dic(LzStateT<Lo>& s, uint64_t dic_li
       if (s.pending != 0) { status = kStNotDone; return kErrData; }
       at_end_check = true;
     }
-    if (s.need_state_init) lz_init_state_real(s);
+    if (s.need_state_init) lz_init_state_real<M>(s);
 
     if (!WithTemp || s.tmp_n == 0) {
       uint32_t in_limit;
       if (avail < kLookahead || at_end_check) {
-        int k = lz_probe(s, src, avail);
+        int k = lz_probe<M>(s, src, avail);
         if (k == PROBE_SHORT) {
           for (uint32_t i = 0; i < uint32_t(avail); ++i) s.tmp[i] = src[i];
           s.tmp_n = uint32_t(avail);
@@ -919,7 +1003,7 @@ __device__ __forceinline__ int lz_decode_to_dic(LzStateT<Lo>& s, uint64_t dic_li
       }
       BulkReader rd;
       rd.init(src, avail);
-      if (lz_run_split(s, dic_limit, rd, in_limit) != kOk) return kErrData;
+      if (lz_run_split<M>(s, dic_limit, rd, in_limit) != kOk) return kErrData;
       const uint32_t used = rd.idx;
       src_len += used;
       src += used;
@@ -929,7 +1013,7 @@ __device__ __forceinline__ int lz_decode_to_dic(LzStateT<Lo>& s, uint64_t dic_li
       while (have < kLookahead && taken < avail) s.tmp[have++] = src[taken++];
       s.tmp_n = have;
       if (have < kLookahead || at_end_check) {
-        int k = lz_probe(s, (const uint8_t*)s.tmp, have);
+        int k = lz_probe<M>(s, (const uint8_t*)s.tmp, have);
         if (k == PROBE_SHORT) {
           src_len += taken;
           status = kStMoreInput;
@@ -939,7 +1023,7 @@ __device__ __forceinline__ int lz_decode_to_dic(LzStateT<Lo>& s, uint64_t dic_li
       }
       LocalReader rd;
       rd.init(s.tmp);
-      if (lz_run_split(s, dic_limit, rd, 0) != kOk) return kErrData;
+      if (lz_run_split<M>(s, dic_limit, rd, 0) != kOk) return kErrData;
       taken -= (have - rd.idx);
       src_len += taken;
       src += taken;

@@ -47,16 +47,15 @@ __device__ __forceinline__ LzmaGpuResult lane_decode(const LzmaGpuStreamDesc& d,
       return r;
     }
     Lz2StateT<gu16*> p;
-    gu16* lo = (gu16*)(ws + d.probs_off);
-    r.res = lz2_init(p, d.props[0], lo, lo + lo_cells(4, 0, 4), (gbyte*)(dst + d.dst_off),
-                     d.dst_cap);
+    gu16* gl = (gu16*)(ws + d.probs_off);
+    r.res = lz2_init(p, d.props[0], gl, gl, (gbyte*)(dst + d.dst_off), d.dst_cap);
     if (r.res != kOk) return r;
     uint64_t sl = d.src_len;
     int status = kStNone;
     // the batch contract for an LZMA2 range is Lzma2Dec_DecodeToDic's own
     // result (NEEDS_MORE_INPUT stays SZ_OK); Lzma2Decode maps it to INPUT_EOF
-    int res = lz2_decode_to_dic(p, d.dst_cap, (const gbyte*)(src + d.src_off), sl, d.finish_mode,
-                                status);
+    int res = lz2_decode_to_dic<0u>(p, d.dst_cap, (const gbyte*)(src + d.src_off), sl,
+                                    d.finish_mode, status);
     r.res = res;
     r.status = status;
     r.dest_len = p.dec.pos;
@@ -74,8 +73,8 @@ __device__ __forceinline__ LzmaGpuResult lane_decode(const LzmaGpuStreamDesc& d,
     r.res = kErrMem;
     return r;
   }
-  s.lo = (gu16*)(ws + d.probs_off);
-  s.hi = s.lo + lo_cells(s.lc, s.lp, s.pb);
+  s.gl = (gu16*)(ws + d.probs_off);
+  s.lo = s.gl;
   s.dic = (gbyte*)(dst + d.dst_off);
   s.cap = d.dst_cap;
   s.pos = 0;
@@ -86,7 +85,7 @@ __device__ __forceinline__ LzmaGpuResult lane_decode(const LzmaGpuStreamDesc& d,
   lz_init_dic_state(s, true, true);
   uint64_t sl = d.src_len;
   int status = kStNone;
-  int res = lz_decode_to_dic<false>(s, d.dst_cap, (const gbyte*)(src + d.src_off), sl,
+  int res = lz_decode_to_dic<false, 0u>(s, d.dst_cap, (const gbyte*)(src + d.src_off), sl,
                                     d.finish_mode, status);
   if (res == kOk && status == kStMoreInput) res = kErrInputEof;
   r.res = res;
@@ -96,9 +95,9 @@ __device__ __forceinline__ LzmaGpuResult lane_decode(const LzmaGpuStreamDesc& d,
   return r;
 }
 
-// One LZMA batch item with the lo table in the lane's LDS slice (lo_cap
-// cells) and the LenHigh trees at the start of its global workspace slice.
-// The planner only routes items here whose lo table fits lo_cap.
+// One LZMA batch item with the LDS-placed sections (LZGPU_LDS_MASK) in the
+// lane's LDS slice (lo_cap cells) and the others in its global workspace
+// slice.  The planner only routes items here whose LDS part fits lo_cap.
 __device__ __forceinline__ LzmaGpuResult lane_decode_lds(const LzmaGpuStreamDesc& d,
                                                          const uint8_t* __restrict__ src,
                                                          uint8_t* __restrict__ dst,
@@ -115,12 +114,13 @@ __device__ __forceinline__ LzmaGpuResult lane_decode_lds(const LzmaGpuStreamDesc
   LzStateT<lds_u16*> s;
   r.res = lz_props_parse(d.props, d.props_size, s.lc, s.lp, s.pb, s.dict_size);
   if (r.res != kOk) return r;
-  if (d.probs_off == LZMA_GPU_NO_WORKSPACE || lo_cells(s.lc, s.lp, s.pb) > lo_cap) {
+  if (d.probs_off == LZMA_GPU_NO_WORKSPACE ||
+      make_layout(s.lc, s.lp, s.pb, LZGPU_LDS_MASK).lds_cells > lo_cap) {
     r.res = kErrMem;
     return r;
   }
   s.lo = lo;
-  s.hi = (gu16*)(ws + d.probs_off);
+  s.gl = (gu16*)(ws + d.probs_off);
   s.dic = (gbyte*)(dst + d.dst_off);
   s.cap = d.dst_cap;
   s.pos = 0;
@@ -131,7 +131,7 @@ __device__ __forceinline__ LzmaGpuResult lane_decode_lds(const LzmaGpuStreamDesc
   lz_init_dic_state(s, true, true);
   uint64_t sl = d.src_len;
   int status = kStNone;
-  int res = lz_decode_to_dic<false>(s, d.dst_cap, (const gbyte*)(src + d.src_off), sl,
+  int res = lz_decode_to_dic<false, LZGPU_LDS_MASK>(s, d.dst_cap, (const gbyte*)(src + d.src_off), sl,
                                     d.finish_mode, status);
   if (res == kOk && status == kStMoreInput) res = kErrInputEof;
   r.res = res;
@@ -141,16 +141,16 @@ __device__ __forceinline__ LzmaGpuResult lane_decode_lds(const LzmaGpuStreamDesc
   return r;
 }
 
-// One LzmaDec_DecodeToDic call on a device-resident decoder (compact layout in
-// q.probs: lo then hi, for the current lc/lp/pb).
+// One LzmaDec_DecodeToDic call on a device-resident decoder (compact layout,
+// all sections in q.probs, for the current lc/lp/pb).
 __device__ __forceinline__ void lane_session(LzgpuSession& q) {
   LzStateT<gu16*> s;
   s.lc = q.lc;
   s.lp = q.lp;
   s.pb = q.pb;
   s.dict_size = q.dict_size;
-  s.lo = (gu16*)q.probs;
-  s.hi = s.lo + lo_cells(q.lc, q.lp, q.pb);
+  s.gl = (gu16*)q.probs;
+  s.lo = s.gl;
   s.dic = (gbyte*)q.dic;
   s.cap = q.cap;
   s.pos = q.pos;
@@ -170,7 +170,7 @@ __device__ __forceinline__ void lane_session(LzgpuSession& q) {
   for (int i = 0; i < int(kLookahead); ++i) s.tmp[i] = q.tmp[i];
   uint64_t sl = q.in_len;
   int status = kStNone;
-  int res = lz_decode_to_dic<true>(s, q.dic_limit, (const gbyte*)q.in, sl, q.finish_mode, status);
+  int res = lz_decode_to_dic<true, 0u>(s, q.dic_limit, (const gbyte*)q.in, sl, q.finish_mode, status);
   q.pos = s.pos;
   q.range = s.range;
   q.code = s.code;

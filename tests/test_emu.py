@@ -21,6 +21,8 @@ EMU_VARIANTS = {
     "default": "",
     "all_on": "-DLZGPU_TREE_PF=1 -DLZGPU_MB_PF=1 -DLZGPU_COPY_SHORT=1 -DLZGPU_READER16=1 "
               "-DLZGPU_NORM_BRANCHLESS=1 -DLZGPU_BIT_MASK=1",
+    "litm_global": "-DLZGPU_LDS_MASK=0x1FF -DLZGPU_MB_PF=0 -DLZGPU_READER16=0",
+    "hot_only_lds": "-DLZGPU_LDS_MASK=0x107",
 }
 
 
