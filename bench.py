@@ -60,10 +60,14 @@ def _compress_range(args):
     return lo, out
 
 
-def build_workload(cfg, rank, workers):
-    """Plaintext (C generator, seeds rank*count + i) and liblzma-encoded streams.
-    Cached under $TMPDIR keyed by config + rank."""
+def build_workload(cfg, rank, workers, world=1):
+    """Rank's shard of the global batch (world x count streams): plaintext from
+    the C generator (stream i seeded by its global index) and liblzma-encoded
+    streams.  Cached under $TMPDIR keyed by config + rank."""
     count, n, lc, lp, pb, dsz, _ = CONFIGS[cfg]
+    import dist_bench as D
+    first, mine = D.shard(count * world, world, rank)
+    assert mine == count
     tmp = os.environ.get("TMPDIR", "/tmp")
     key = f"lzgpu_{cfg}_r{rank}_v1"
     plain_path = os.path.join(tmp, key + ".plain")
@@ -71,7 +75,7 @@ def build_workload(cfg, rank, workers):
     import native
     if not os.path.exists(plain_path):
         plain = np.zeros(count * n, dtype=np.uint8)
-        native.synth().synth_batch(0, rank * count, plain.ctypes.data, n, count, max(1, workers))
+        native.synth().synth_batch(0, first, plain.ctypes.data, n, count, max(1, workers))
         plain.tofile(plain_path)
     plain = np.fromfile(plain_path, dtype=np.uint8)
     if os.path.exists(comp_path):
@@ -146,15 +150,14 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    import dist_bench as D
+    world, rank, local_rank = D.world_info()
     cpus = os.cpu_count() or 8
     workers = max(1, min(16, cpus // max(1, world)))
 
     count, n, lc, lp, pb, dsz, desc_txt = CONFIGS[args.config]
     # workload first: the compression pool forks before this process touches the GPU
-    plain, comp, lens, props = build_workload(args.config, rank, workers)
+    plain, comp, lens, props = build_workload(args.config, rank, workers, world)
 
     import torch
     import torch.distributed as dist
@@ -184,8 +187,7 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    D.barrier()
     torch.cuda.synchronize()
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
            for _ in range(args.steps)]
@@ -195,15 +197,11 @@ def main():
         step()
         evs[i][1].record(stream)
     torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
+    D.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     kern_ms = [a.elapsed_time(b) for a, b in evs]
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = D.reduce_max(elapsed, dev)  # slowest rank sets the job time
 
     # ---- verify (bit-exact vs plaintext + per-stream result invariants)
     res = np.frombuffer(d_res.cpu().numpy().tobytes(), dtype=np.dtype(
@@ -212,10 +210,7 @@ def main():
               (res["dest_len"] == n).all() and (res["src_len"] == lens).all())
     out = d_dst.cpu().numpy()
     ok = ok and bool(np.array_equal(out, plain))
-    if world > 1:
-        f = torch.tensor([1 if ok else 0], dtype=torch.int32, device=dev)
-        dist.all_reduce(f, op=dist.ReduceOp.MIN)
-        ok = bool(f.item())
+    ok = D.all_true(ok, dev)
     if not ok:
         log(f"[rank {rank}] VERIFY FAILED: res={np.unique(res['res'])} "
             f"status={np.unique(res['status'])}")
