@@ -124,10 +124,11 @@ __host__ __device__ inline uint32_t num_probs(uint32_t lc, uint32_t lp) {
   return 1846u + (768u << (lc + lp));
 }
 
-// Placement used by the fast kernel (build-time; A/B'd on MI355X): default =
-// everything in LDS except the rarely used LenHigh trees.
+// Placement used by the fast kernel (build-time; A/B'd on MI355X):
+// default = everything in LDS except SpecPos, the matched-literal trees and the
+// LenHigh trees (1272 B per lc0/pb0 stream, 128 resident streams per CU).
 #ifndef LZGPU_LDS_MASK
-#define LZGPU_LDS_MASK 0x3FFu
+#define LZGPU_LDS_MASK 0x1BFu
 #endif
 
 // Explicit address spaces: LDS (3) for the lo table of the fast kernel, global

@@ -23,6 +23,7 @@ EMU_VARIANTS = {
               "-DLZGPU_NORM_BRANCHLESS=1 -DLZGPU_BIT_MASK=1",
     "litm_global": "-DLZGPU_LDS_MASK=0x1FF -DLZGPU_MB_PF=0 -DLZGPU_READER16=0",
     "hot_only_lds": "-DLZGPU_LDS_MASK=0x107",
+    "full_lds": "-DLZGPU_LDS_MASK=0x3FF",
 }
 
 
@@ -66,11 +67,17 @@ def run_batch(emu, items, src, lds=False):
         return res, dst.raw
     one = (L.StreamDesc * 1)()
     r1 = (L.Result * 1)()
+    # LDS slice large enough for any placement variant: the whole table
+    stride = 0
+    for k in range(plan.n_lds):
+        pr = bytes(descs[order[k]].props)
+        lc, lp, pb = pr[0] % 9, (pr[0] // 9) % 5, pr[0] // 45
+        stride = max(stride, (56 << pb) + 950 + (768 << (lc + lp)))
     for k in range(n):
         i = order[k]
         one[0] = descs[i]
         if k < plan.n_lds:
-            emu.emu_decode_batch_lds(one, 1, src, dst, wsbuf, r1, plan.lds_cells_per_lane)
+            emu.emu_decode_batch_lds(one, 1, src, dst, wsbuf, r1, (stride + 3) // 4 * 4)
         else:
             emu.emu_decode_batch(one, 1, src, dst, wsbuf, r1)
         res[i] = r1[0]
