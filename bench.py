@@ -120,6 +120,51 @@ def make_descs(lens, n, props, finish=1):
     return descs, order, plan, offs
 
 
+def measure_crc(L, torch, descs, d_desc, d_res, d_dst, plain, count, n, stream, dev, steps):
+    """CRC-32 of every decoded stream straight from the decode's device buffers
+    (LzmaGpu_Crc32Batch), timed apart from the decode with
+    HIP events on the same stream; checked against zlib.crc32 (same CRC-32)."""
+    import zlib
+    base, crange, total = L.crc32_plan_decoded(descs)
+    d_base = torch.frombuffer(bytearray(base), dtype=torch.uint8).to(dev)
+    d_range = torch.frombuffer(bytearray(crange), dtype=torch.uint8).to(dev)
+    d_chunks = torch.empty(max(total, 1) * 4, dtype=torch.uint8, device=dev)
+    d_crc = torch.empty(count * 4, dtype=torch.uint8, device=dev)
+    sh = stream.cuda_stream
+
+    def run():
+        r = L.crc32_batch_decoded(d_desc.data_ptr(), d_res.data_ptr(), count, d_dst.data_ptr(),
+                                  d_base.data_ptr(), d_range.data_ptr(), total,
+                                  d_chunks.data_ptr(), d_crc.data_ptr(), sh)
+        if r != 0:
+            raise RuntimeError("LzmaGpu_Crc32Batch failed: " + L.last_error())
+
+    run()
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(steps)]
+    for a, b in evs:
+        a.record(stream)
+        run()
+        b.record(stream)
+    torch.cuda.synchronize()
+    ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    got = np.frombuffer(d_crc.cpu().numpy().tobytes(), dtype="<u4")
+    rows = plain.reshape(count, n)
+    want = np.array([zlib.crc32(rows[i].tobytes()) for i in range(count)], dtype=np.uint32)
+    # bytes per launch: decoded output read once + chunk registers written and re-read
+    alg = count * n
+    moved = alg + 8 * total + count * (8 + 8 + 4)
+    gbs = moved / (ms * 1e-3) / 1e9
+    return {"kernels": "lzgpu_crc_chunk_kernel + lzgpu_crc_fold_kernel",
+            "value": round(alg / (ms * 1e-3) / 1e6, 2), "unit": "MB/s", "avg_ms": round(ms, 4),
+            "chunks": int(total),
+            "roofline": {"bound": "hbm", "achieved": round(gbs, 3), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
+                         "alg_bytes_per_launch": int(moved)},
+            "verified": bool(np.array_equal(got, want))}
+
+
 def cpu_baseline(comp, lens, offs, n, props, threads, sample_streams):
     """The oracle restatement (CPU port of LzmaDec) on a bounded sample."""
     import native
@@ -148,6 +193,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="cfg3", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-crc", action="store_true", help="skip the CRC-32 (8(f) row 1) leg")
     args = ap.parse_args()
 
     import dist_bench as D
@@ -215,6 +261,11 @@ def main():
         log(f"[rank {rank}] VERIFY FAILED: res={np.unique(res['res'])} "
             f"status={np.unique(res['status'])}")
 
+    crc = measure_crc(L, torch, descs, d_desc, d_res, d_dst, plain, count, n, stream, dev,
+                      args.steps) if not args.no_crc else None
+    if crc is not None:
+        ok = D.all_true(ok and crc["verified"], dev)
+
     total_bytes = count * n * world * args.steps
     value = total_bytes / elapsed / 1e6
     avg_kern_ms = float(np.mean(kern_ms))
@@ -264,6 +315,7 @@ def main():
                          "kernel_avg_ms": round(avg_kern_ms, 4),
                          "alg_bytes_per_launch": alg_bytes},
             "cpu_baseline": cpu,
+            "crc32": crc,
             "verified": ok,
         }
         print(json.dumps(line), flush=True)

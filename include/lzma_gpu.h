@@ -260,6 +260,45 @@ SRes LzmaGpu_DecodeBatchHost(const LzmaGpuStreamDesc *descs, size_t n, const Byt
 size_t Lzma2Gpu_SplitBlocks(const Byte *src, size_t src_len, uint64_t *src_off,
                             uint64_t *block_src_len, uint64_t *unpack, size_t max_blocks);
 
+/* ---------------------------------------------------------------- CRC-32 */
+
+/* Drop-ins for 7zCrc.h (poly 0xEDB88320, 7zCrc.c:7):
+ *   CrcGenerateTable  replaces 7zCrc.h:14 / 7zCrc.c:56-80 (no-op: device tables are constants)
+ *   CrcUpdate         replaces 7zCrc.h:20 / 7zCrc.c:44-47 (raw register, no final XOR)
+ *   CrcCalc           replaces 7zCrc.h:21 / 7zCrc.c:49-52 (init and final XOR 0xFFFFFFFF)
+ * Over host buffers (upload + the batch kernels).  They have no error
+ * channel: without a device they print once to stderr and return 0. */
+void CrcGenerateTable(void);
+UInt32 CrcUpdate(UInt32 crc, const void *data, size_t size);
+UInt32 CrcCalc(const void *data, size_t size);
+
+/* Batch CRC: range i is d_data[off[i] .. off[i] + len[i]).  Ranges are cut into
+ * 2048-byte chunks (aligned to the range end) that decode in parallel.
+ * Plan on the host from per-range capacities (len[i] <= caps[i]):
+ *   n_chunks = CrcGpu_PlanChunks(caps, n, NULL, NULL);
+ *   CrcGpu_PlanChunks(caps, n, chunk_base, chunk_range);  // n and n_chunks entries
+ * then upload chunk_base / chunk_range.  Returns (size_t)-1 if n_chunks
+ * would exceed 2^32 - 1.  d_chunk_crc: n_chunks uint32 of device scratch. */
+size_t CrcGpu_PlanChunks(const uint64_t *caps, size_t n, uint32_t *chunk_base,
+                         uint32_t *chunk_range);
+/* d_crc[i] = register after range i from `init`, XOR `xorout`
+ * (CrcCalc: init = xorout = 0xFFFFFFFF; CrcUpdate(v, ...): init = v, xorout = 0).
+ * All pointers device memory; asynchronous on `stream`. */
+SRes CrcGpu_Batch(const Byte *d_data, const uint64_t *d_off, const uint64_t *d_len, size_t n,
+                  const uint32_t *d_chunk_base, const uint32_t *d_chunk_range, size_t n_chunks,
+                  uint32_t init, uint32_t xorout, uint32_t *d_chunk_crc, uint32_t *d_crc,
+                  void *stream);
+/* CrcCalc of every decoded stream of a batch, straight from the decode's device
+ * buffers: d_crc[i] = CrcCalc(d_dst + descs[i].dst_off, results[i].dest_len)
+ * (the 7z folder / file check after decode, 7zIn.c:1380, 1397).  Plan with
+ * capacities = descs[i].dst_cap via LzmaGpu_Crc32Plan (host descs). */
+size_t LzmaGpu_Crc32Plan(const LzmaGpuStreamDesc *descs, size_t n, uint32_t *chunk_base,
+                         uint32_t *chunk_range);
+SRes LzmaGpu_Crc32Batch(const LzmaGpuStreamDesc *d_descs, const LzmaGpuResult *d_results,
+                        size_t n, const Byte *d_dst, const uint32_t *d_chunk_base,
+                        const uint32_t *d_chunk_range, size_t n_chunks, uint32_t *d_chunk_crc,
+                        uint32_t *d_crc, void *stream);
+
 /* Device / diagnostics. */
 int LzmaGpu_DeviceCount(void);
 const char *LzmaGpu_LastError(void);

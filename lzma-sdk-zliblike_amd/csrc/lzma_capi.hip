@@ -18,6 +18,7 @@
 #include <string>
 #include <vector>
 
+#include "crc32_device.h"
 #include "lzma_device.h"
 #include "lzma_gpu_internal.h"
 
@@ -81,7 +82,7 @@ struct DevBuf {
 };
 
 struct Scratch {
-  DevBuf probs, dic, src, sess, desc, res, dst;
+  DevBuf probs, dic, src, sess, desc, res, dst, crc_meta, crc_chunks;
 };
 
 Scratch& scratch() {
@@ -862,6 +863,101 @@ size_t Lzma2Gpu_SplitBlocks(const Byte* src, size_t src_len, uint64_t* src_off,
   if (pos > src_len) return size_t(-1);
   close_block(src_len);  // no EOS byte: the last block runs to the end
   return nb;
+}
+
+// ------------------------------------------------------------------ CRC-32
+
+size_t CrcGpu_PlanChunks(const uint64_t* caps, size_t n, uint32_t* chunk_base,
+                         uint32_t* chunk_range) {
+  uint64_t total = 0;
+  for (size_t i = 0; i < n; ++i) {
+    const uint64_t c = (caps[i] + lzgpu::kCrcChunk - 1) / lzgpu::kCrcChunk;
+    if (total + c > 0xFFFFFFFFull) return size_t(-1);
+    if (chunk_base) chunk_base[i] = uint32_t(total);
+    if (chunk_range)
+      for (uint64_t k = 0; k < c; ++k) chunk_range[total + k] = uint32_t(i);
+    total += c;
+  }
+  return size_t(total);
+}
+
+size_t LzmaGpu_Crc32Plan(const LzmaGpuStreamDesc* descs, size_t n, uint32_t* chunk_base,
+                         uint32_t* chunk_range) {
+  std::vector<uint64_t> caps(n);
+  for (size_t i = 0; i < n; ++i) caps[i] = descs[i].dst_cap;
+  return CrcGpu_PlanChunks(caps.data(), n, chunk_base, chunk_range);
+}
+
+SRes CrcGpu_Batch(const Byte* d_data, const uint64_t* d_off, const uint64_t* d_len, size_t n,
+                  const uint32_t* d_chunk_base, const uint32_t* d_chunk_range, size_t n_chunks,
+                  uint32_t init, uint32_t xorout, uint32_t* d_chunk_crc, uint32_t* d_crc,
+                  void* stream) {
+  if (!ensure_device()) return SZ_ERROR_FAIL;
+  if (n > 0xFFFFFFFFull || n_chunks > 0xFFFFFFFFull) return SZ_ERROR_PARAM;
+  if (lzgpu_launch_crc_arrays(d_data, d_off, d_len, uint32_t(n), d_chunk_base, d_chunk_range,
+                              uint32_t(n_chunks), init, xorout, d_chunk_crc, d_crc,
+                              static_cast<hipStream_t>(stream)) != 0) {
+    set_error("CRC kernel launch failed");
+    return SZ_ERROR_FAIL;
+  }
+  return SZ_OK;
+}
+
+SRes LzmaGpu_Crc32Batch(const LzmaGpuStreamDesc* d_descs, const LzmaGpuResult* d_results,
+                        size_t n, const Byte* d_dst, const uint32_t* d_chunk_base,
+                        const uint32_t* d_chunk_range, size_t n_chunks, uint32_t* d_chunk_crc,
+                        uint32_t* d_crc, void* stream) {
+  if (!ensure_device()) return SZ_ERROR_FAIL;
+  if (n > 0xFFFFFFFFull || n_chunks > 0xFFFFFFFFull) return SZ_ERROR_PARAM;
+  if (lzgpu_launch_crc_decoded(d_descs, d_results, d_dst, uint32_t(n), d_chunk_base,
+                               d_chunk_range, uint32_t(n_chunks), d_chunk_crc, d_crc,
+                               static_cast<hipStream_t>(stream)) != 0) {
+    set_error("CRC kernel launch failed");
+    return SZ_ERROR_FAIL;
+  }
+  return SZ_OK;
+}
+
+// 7zCrc.h drop-ins over host buffers (upload + the batch kernels, n = 1).
+// They cannot report errors; without a device they print once and return 0.
+void CrcGenerateTable(void) {}  // tables are compile-time constants on the device
+
+static uint32_t crc_host_one(uint32_t init, const void* data, size_t size, uint32_t xorout) {
+  if (!ensure_device()) return 0;
+  if (size == 0) return init ^ xorout;
+  Scratch& S = scratch();
+  const uint64_t cap = size;
+  const size_t nch = CrcGpu_PlanChunks(&cap, 1, nullptr, nullptr);
+  std::vector<uint32_t> meta(1 + nch, 0);
+  CrcGpu_PlanChunks(&cap, 1, meta.data(), meta.data() + 1);
+  const uint64_t ol[2] = {0, cap};
+  uint8_t* d_data = static_cast<uint8_t*>(S.src.get(size));
+  uint8_t* d_meta = static_cast<uint8_t*>(S.crc_meta.get(16 + 4 * (1 + nch) + 8));
+  uint32_t* d_chunks = static_cast<uint32_t*>(S.crc_chunks.get(4 * (nch + 1)));
+  if (!d_data || !d_meta || !d_chunks) {
+    set_error("CRC: device allocation failed");
+    return 0;
+  }
+  uint64_t* d_ol = reinterpret_cast<uint64_t*>(d_meta);
+  uint32_t* d_base = reinterpret_cast<uint32_t*>(d_meta + 16);
+  uint32_t* d_crc = d_base + 1 + nch;
+  uint32_t out = 0;
+  if (!hip_ok(hipMemcpy(d_data, data, size, hipMemcpyHostToDevice), "CRC H2D") ||
+      !hip_ok(hipMemcpy(d_ol, ol, 16, hipMemcpyHostToDevice), "CRC H2D") ||
+      !hip_ok(hipMemcpy(d_base, meta.data(), 4 * (1 + nch), hipMemcpyHostToDevice), "CRC H2D"))
+    return 0;
+  if (lzgpu_launch_crc_arrays(d_data, d_ol, d_ol + 1, 1, d_base, d_base + 1, uint32_t(nch), init,
+                              xorout, d_chunks, d_crc, nullptr) != 0 ||
+      !hip_ok(hipDeviceSynchronize(), "CRC kernel") ||
+      !hip_ok(hipMemcpy(&out, d_crc, 4, hipMemcpyDeviceToHost), "CRC D2H"))
+    return 0;
+  return out;
+}
+
+UInt32 CrcUpdate(UInt32 v, const void* data, size_t size) { return crc_host_one(v, data, size, 0); }
+
+UInt32 CrcCalc(const void* data, size_t size) {
+  return crc_host_one(0xFFFFFFFFu, data, size, 0xFFFFFFFFu);
 }
 
 int LzmaGpu_DeviceCount(void) { return device_count(); }

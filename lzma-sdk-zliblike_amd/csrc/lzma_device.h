@@ -164,6 +164,10 @@ typedef __attribute__((address_space(1))) uint32_t gu32;
 //                      replicate it from registers instead of byte round trips
 //   LZGPU_READER16     input window refilled 16 bytes per load (one vmcnt drain
 //                      per 16 input bytes instead of per 4)
+//   LZGPU_COPY_V2      match copies: every 8-byte step is one batch of loads
+//                      (the tail too, stores predicated), and rep0 < 8 builds
+//                      the periodic pattern in a register once -- one load
+//                      round trip per 8 bytes instead of one per tail byte
 #ifndef LZGPU_TREE_PF
 #define LZGPU_TREE_PF 0
 #endif
@@ -175,6 +179,9 @@ typedef __attribute__((address_space(1))) uint32_t gu32;
 #endif
 #ifndef LZGPU_READER16
 #define LZGPU_READER16 1
+#endif
+#ifndef LZGPU_COPY_V2
+#define LZGPU_COPY_V2 0
 #endif
 
 // Per-lane decoder state (CLzmaDec fields, LzmaDec.h:50-69).  lo = the LDS
@@ -485,9 +492,67 @@ struct Rc {
 // Copy n bytes of an LZ match: dic[pos..pos+n) = dic[from..], byte-serial
 // overlap semantics (rep0 < n replicates the period), ring wrap at cap.
 // Non-overlapping, non-wrapping spans go 8 bytes per round trip.
+#if LZGPU_COPY_V2
+// low min(rem, 8) bytes of v to d[0..)
+__device__ __forceinline__ void lz_store_upto8(gbyte* d, uint64_t v, uint32_t rem) {
+  if (rem >= 8) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) d[k] = uint8_t(v >> (8 * k));
+  } else {
+    for (uint32_t k = 0; k < rem; ++k) d[k] = uint8_t(v >> (8 * k));
+  }
+}
+#endif
+
 __device__ __forceinline__ uint32_t lz_copy(gbyte* dic, uint64_t pos, uint64_t from, uint32_t n,
                                             uint32_t dist, uint64_t cap) {
   uint32_t last = 0;
+#if LZGPU_COPY_V2
+  if (from + n <= cap && from < pos) {
+    // source span [from, from+n) does not wrap; from < pos always holds here
+    // except for the ring case handled below
+    gbyte* d = dic + pos;
+    const gbyte* src = dic + from;
+    uint64_t v;
+    if (dist >= 8) {
+      // src[i..i+8) lies below d + i: written before this step reads it
+      uint32_t i = 0;
+      do {
+        v = 0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v |= uint64_t(src[i + k]) << (8 * k);
+        const uint32_t rem = n - i;
+        lz_store_upto8(d + i, v, rem);
+        if (rem <= 8) {
+          last = uint32_t(v >> (8 * (rem - 1))) & 0xFFu;
+          break;
+        }
+        i += 8;
+      } while (true);
+      return last;
+    }
+    // rep0 < 8: the output is src[0..dist) repeated; build 8 bytes of it
+    v = 0;
+    for (uint32_t k = 0; k < dist; ++k) v |= uint64_t(src[k]) << (8 * k);
+    v |= v << (8 * dist);
+    if (dist < 4) v |= v << (16 * dist);
+    if (dist < 2) v |= v << 32;
+    // next 8 bytes of the period: shift by t = 8 mod dist
+    const uint32_t t = 8u % dist;
+    uint32_t i = 0;
+    do {
+      const uint32_t rem = n - i;
+      lz_store_upto8(d + i, v, rem);
+      if (rem <= 8) {
+        last = uint32_t(v >> (8 * (rem - 1))) & 0xFFu;
+        break;
+      }
+      v = (v >> (8 * t)) | (v << (8 * (dist - t)));
+      i += 8;
+    } while (true);
+    return last;
+  }
+#endif
 #if LZGPU_COPY_SHORT
   if (dist < 8 && dist < n && from + dist <= cap && from < pos) {
     // overlapping: the output is the dist-byte period starting at `from`,

@@ -16,3 +16,15 @@ extern "C" int lzgpu_launch_decode_lds(const LzmaGpuStreamDesc* d_descs, const u
                                        uint16_t* d_ws, LzmaGpuResult* d_results, uint32_t lanes,
                                        uint32_t stride, uint32_t waves_per_simd,
                                        hipStream_t stream);
+extern "C" int lzgpu_launch_crc_arrays(const uint8_t* d_data, const uint64_t* d_off,
+                                       const uint64_t* d_len, uint32_t n,
+                                       const uint32_t* d_chunk_base,
+                                       const uint32_t* d_chunk_range, uint32_t n_chunks,
+                                       uint32_t init, uint32_t xorout, uint32_t* d_chunk_crc,
+                                       uint32_t* d_crc, hipStream_t stream);
+extern "C" int lzgpu_launch_crc_decoded(const LzmaGpuStreamDesc* d_descs,
+                                        const LzmaGpuResult* d_results, const uint8_t* d_dst,
+                                        uint32_t n, const uint32_t* d_chunk_base,
+                                        const uint32_t* d_chunk_range, uint32_t n_chunks,
+                                        uint32_t* d_chunk_crc, uint32_t* d_crc,
+                                        hipStream_t stream);

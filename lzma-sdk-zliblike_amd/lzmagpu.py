@@ -107,6 +107,13 @@ _sig = {
     "LzmaGpu_DecodeBatchEx": (ctypes.c_int, [ctypes.POINTER(Plan), _P, _P, _P, _P, _P, _P, _P]),
     "LzmaGpu_DecodeBatchHost": (ctypes.c_int, [ctypes.POINTER(StreamDesc), ctypes.c_size_t, _P, ctypes.c_size_t, _P, ctypes.c_size_t, ctypes.POINTER(Result)]),
     "Lzma2Gpu_SplitBlocks": (ctypes.c_size_t, [_P, ctypes.c_size_t, _P, _P, _P, ctypes.c_size_t]),
+    "CrcGenerateTable": (None, []),
+    "CrcUpdate": (ctypes.c_uint32, [ctypes.c_uint32, _P, ctypes.c_size_t]),
+    "CrcCalc": (ctypes.c_uint32, [_P, ctypes.c_size_t]),
+    "CrcGpu_PlanChunks": (ctypes.c_size_t, [_P, ctypes.c_size_t, _P, _P]),
+    "CrcGpu_Batch": (ctypes.c_int, [_P, _P, _P, ctypes.c_size_t, _P, _P, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint32, _P, _P, _P]),
+    "LzmaGpu_Crc32Plan": (ctypes.c_size_t, [ctypes.POINTER(StreamDesc), ctypes.c_size_t, _P, _P]),
+    "LzmaGpu_Crc32Batch": (ctypes.c_int, [_P, _P, ctypes.c_size_t, _P, _P, _P, ctypes.c_size_t, _P, _P, _P]),
     "LzmaGpu_DeviceCount": (ctypes.c_int, []),
     "LzmaGpu_LastError": (ctypes.c_char_p, []),
     "LzmaGpu_Version": (ctypes.c_char_p, []),
@@ -296,3 +303,55 @@ def split_lzma2_blocks(src):
         if nb <= cap:
             return [(o[i], ln[i], u[i]) for i in range(nb)]
         cap = nb
+
+
+# ---------------------------------------------------------------- CRC-32 (7zCrc.h)
+
+CRC_CHUNK = 2048  # kCrcChunk in csrc/crc32_device.h
+
+
+def CrcCalc(data):
+    """7zCrc.c CrcCalc on the GPU (host buffer in, CRC out)."""
+    return _lib.CrcCalc(_buf(data), len(data))
+
+
+def CrcUpdate(crc, data):
+    """7zCrc.c CrcUpdate (raw register, no final XOR) on the GPU."""
+    return _lib.CrcUpdate(crc, _buf(data), len(data))
+
+
+def crc_plan(caps):
+    """CrcGpu_PlanChunks: (chunk_base[n], chunk_range[n_chunks]) as ctypes arrays."""
+    n = len(caps)
+    c = (ctypes.c_uint64 * max(n, 1))(*caps)
+    total = _lib.CrcGpu_PlanChunks(c, n, None, None)
+    if total == ctypes.c_size_t(-1).value:
+        raise ValueError("too many CRC chunks")
+    base = (ctypes.c_uint32 * max(n, 1))()
+    rng = (ctypes.c_uint32 * max(total, 1))()
+    _lib.CrcGpu_PlanChunks(c, n, base, rng)
+    return base, rng, total
+
+
+def crc32_plan_decoded(descs):
+    """LzmaGpu_Crc32Plan over planned decode descriptors (host)."""
+    n = len(descs)
+    total = _lib.LzmaGpu_Crc32Plan(descs, n, None, None)
+    base = (ctypes.c_uint32 * max(n, 1))()
+    rng = (ctypes.c_uint32 * max(total, 1))()
+    _lib.LzmaGpu_Crc32Plan(descs, n, base, rng)
+    return base, rng, total
+
+
+def crc_batch_device(d_data, d_off, d_len, n, d_base, d_range, n_chunks, init, xorout,
+                     d_chunk_crc, d_crc, stream=0):
+    """CrcGpu_Batch over raw device pointers (ints)."""
+    return _lib.CrcGpu_Batch(d_data, d_off, d_len, n, d_base, d_range, n_chunks, init, xorout,
+                             d_chunk_crc, d_crc, stream or None)
+
+
+def crc32_batch_decoded(d_descs, d_results, n, d_dst, d_base, d_range, n_chunks, d_chunk_crc,
+                        d_crc, stream=0):
+    """LzmaGpu_Crc32Batch over raw device pointers (ints)."""
+    return _lib.LzmaGpu_Crc32Batch(d_descs, d_results, n, d_dst, d_base, d_range, n_chunks,
+                                   d_chunk_crc, d_crc, stream or None)

@@ -1016,3 +1016,27 @@ int orc_lzma_decode_batch(const uint8_t *src, const uint64_t *src_off,
   pthread_mutex_destroy(&b.mu);
   return b.errors;
 }
+
+/* ------------------------------------------------------------------ CRC-32 */
+
+static uint32_t orc_crc_table[256];
+static pthread_once_t orc_crc_once = PTHREAD_ONCE_INIT;
+
+/* table of 7zCrc.c:56-65 (CrcGenerateTable, first 256 entries) */
+static void orc_crc_init(void) {
+  for (uint32_t i = 0; i < 256; i++) {
+    uint32_t r = i;
+    for (int j = 0; j < 8; j++) r = (r >> 1) ^ ((r & 1u) ? 0xEDB88320u : 0u);
+    orc_crc_table[i] = r;
+  }
+}
+
+uint32_t orc_crc_update(uint32_t crc, const uint8_t *data, size_t size) {
+  pthread_once(&orc_crc_once, orc_crc_init);
+  for (size_t i = 0; i < size; i++) crc = orc_crc_table[(crc ^ data[i]) & 0xFFu] ^ (crc >> 8);
+  return crc;
+}
+
+uint32_t orc_crc_calc(const uint8_t *data, size_t size) {
+  return orc_crc_update(0xFFFFFFFFu, data, size) ^ 0xFFFFFFFFu;
+}

@@ -49,6 +49,13 @@ int orc_lzma_decode_batch(const uint8_t *src, const uint64_t *src_off,
                           uint64_t *dest_len_out, uint64_t *src_len_out, size_t n,
                           int threads);
 
+/* CRC-32 as 7zCrc.c computes it: CrcUpdate (7zCrc.c:44-47) = the byte step
+ * CRC_UPDATE_BYTE (7zCrc.h:18) over a 256-entry table of the reflected
+ * polynomial 0xEDB88320 (7zCrc.c:7, 56-65) starting from `crc`, no final XOR;
+ * CrcCalc (7zCrc.c:49-52) = CrcUpdate(0xFFFFFFFF, ...) ^ 0xFFFFFFFF. */
+uint32_t orc_crc_update(uint32_t crc, const uint8_t *data, size_t size);
+uint32_t orc_crc_calc(const uint8_t *data, size_t size);
+
 #ifdef __cplusplus
 }
 #endif

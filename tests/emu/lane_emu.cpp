@@ -7,7 +7,10 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <vector>
+
 #include "../../lzma-sdk-zliblike_amd/csrc/lzma_lane.h"
+#include "../../lzma-sdk-zliblike_amd/csrc/crc32_device.h"
 
 using namespace lzgpu;
 
@@ -86,6 +89,21 @@ int emu_stream_decode(const uint8_t* props, const uint8_t* src, size_t src_total
   *out_len = out_pos;
   *in_used = in_pos;
   return calls;
+}
+
+// CRC-32 kernels' per-lane code (crc_chunk per chunk slot, then crc_fold),
+// range by range.  The blocks read may extend up to 15 bytes either side of a
+// range (aligned 16-byte loads): callers pad their buffers.
+void emu_crc_ranges(const uint8_t* data, const uint64_t* off, const uint64_t* len, size_t n,
+                    uint32_t init, uint32_t xorout, uint32_t* out) {
+  static const CrcTables T = crc_make_tables();
+  for (size_t i = 0; i < n; ++i) {
+    const uint64_t nch = (len[i] + kCrcChunk - 1) / kCrcChunk;
+    std::vector<uint32_t> c(nch + 1);
+    for (uint64_t j = 0; j < nch; ++j)
+      crc_chunk(&T.slice[0][0], data + off[i], len[i], uint32_t(j), init, &c[j]);
+    out[i] = crc_fold(&T.shift[0][0], c.data(), len[i], init) ^ xorout;
+  }
 }
 
 }  // extern "C"

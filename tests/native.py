@@ -72,6 +72,15 @@ def ref():
     return lib
 
 
+def crc_funcs(lib, update, calc):
+    """(update, calc) ctypes callables of a CRC-32 implementation in lib."""
+    u, c = getattr(lib, update), getattr(lib, calc)
+    u.restype, c.restype = ctypes.c_uint32, ctypes.c_uint32
+    u.argtypes = [ctypes.c_uint32, ctypes.c_char_p, ctypes.c_size_t]
+    c.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
+    return u, c
+
+
 def synth():
     lib = _load(SYNTH_SO)
     if not getattr(lib, "_declared", False):

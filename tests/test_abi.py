@@ -23,7 +23,7 @@ LIB = os.path.join(ROOT, "lzma-sdk-zliblike_amd", "lib", "liblzmagpu.so")
 def header_functions():
     txt = open(HEADER).read()
     txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
-    names = re.findall(r"^\s*(?:SRes|void|int|size_t|const char \*)\s*\*?\s*(\w+)\s*\(", txt,
+    names = re.findall(r"^\s*(?:SRes|void|int|size_t|UInt32|const char \*)\s*\*?\s*(\w+)\s*\(", txt,
                        flags=re.M)
     return sorted(set(names))
 
@@ -34,7 +34,8 @@ def test_header_declares_reference_surface():
                      "LzmaDec_Allocate", "LzmaDec_Free", "LzmaDec_Init", "LzmaDec_DecodeToDic",
                      "LzmaDec_DecodeToBuf", "LzmaDecode", "LzmaUncompress",
                      "Lzma2Dec_AllocateProbs", "Lzma2Dec_Allocate", "Lzma2Dec_Init",
-                     "Lzma2Dec_DecodeToDic", "Lzma2Dec_DecodeToBuf", "Lzma2Decode"):
+                     "Lzma2Dec_DecodeToDic", "Lzma2Dec_DecodeToBuf", "Lzma2Decode",
+                     "CrcGenerateTable", "CrcUpdate", "CrcCalc"):
         assert ref_name in names
 
 
@@ -75,6 +76,8 @@ def test_no_device_fails_loudly():
     res, st, dl, sl, out = L.LzmaDecode(b"\x00" * 32, b"\x5d\x00\x00\x01\x00", 100)
     assert res == L.SZ_ERROR_FAIL and dl == 0
     assert "no HIP device" in L.last_error()
+    # CRC drop-ins have no error channel: 0 (never a silently CPU-computed value)
+    assert L.CrcCalc(b"123456789") == 0
 
 
 def test_lzma2_split_blocks_matches_reference_layout():

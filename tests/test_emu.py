@@ -24,6 +24,7 @@ EMU_VARIANTS = {
     "litm_global": "-DLZGPU_LDS_MASK=0x1FF -DLZGPU_MB_PF=0 -DLZGPU_READER16=0",
     "hot_only_lds": "-DLZGPU_LDS_MASK=0x107",
     "full_lds": "-DLZGPU_LDS_MASK=0x3FF",
+    "copy_v2": "-DLZGPU_COPY_V2=1",
 }
 
 
