@@ -217,7 +217,9 @@ size_t LzmaGpu_PlanBatch(LzmaGpuStreamDesc *descs, size_t n, uint32_t *order);
  * generic kernel (tables in the global workspace: LZMA2 ranges, lc+lp too
  * wide for LDS).  Environment overrides for experiments:
  * LZGPU_KERNEL=global|lds, LZGPU_LANES=<streams per workgroup>,
- * LZGPU_OCC=<4|6|8 waves per SIMD>. */
+ * LZGPU_OCC=<4|6|8 waves per SIMD>, LZGPU_PERSIST=0 (one stream per lane).
+ * workspace_bytes includes the LDS kernel's 4-byte work counter at
+ * queue_offset (zeroed by every DecodeBatchEx launch on its stream). */
 typedef struct LzmaGpuPlan {
   uint64_t workspace_bytes;
   uint64_t n;
@@ -226,7 +228,9 @@ typedef struct LzmaGpuPlan {
   uint32_t lds_cells_per_lane;
   uint32_t groups_per_cu;
   uint32_t waves_per_simd; /* LDS kernel register budget: 4, 6 or 8 waves per SIMD */
-  uint32_t reserved[8];
+  uint64_t queue_offset;   /* byte offset in the workspace of the LDS kernel's work counter */
+  uint32_t persistent;     /* 1: grid = resident workgroups, lanes pull streams from the queue */
+  uint32_t reserved[5];
 } LzmaGpuPlan;
 
 SRes LzmaGpu_PlanBatchEx(LzmaGpuStreamDesc *descs, size_t n, uint32_t *order, LzmaGpuPlan *plan);

@@ -646,6 +646,7 @@ static uint64_t plan_workspace(LzmaGpuStreamDesc* descs, size_t n, std::vector<u
     uint32_t np = 0;
     if (d.kind == LZMA_GPU_KIND_LZMA2) {
       np = lzgpu::table_cells(4, 0, 4);
+      if (lo_w && d.props[0] <= 40) (*lo_w)[i] = lzgpu::lzma2_lds_cells(LZGPU_LDS_MASK);
     } else {
       uint32_t lc, lp, pb, dict;
       if (lzgpu::lz_props_parse(d.props, d.props_size, lc, lp, pb, dict) == SZ_OK) {
@@ -696,8 +697,14 @@ SRes LzmaGpu_PlanBatchEx(LzmaGpuStreamDesc* descs, size_t n, uint32_t* order,
       glob_idx.push_back(uint32_t(i));
     }
   }
+  // Longest work first, and streams of similar work side by side: a wave
+  // runs until its slowest lane is done.  Work ~ range-coder decisions, which
+  // track the compressed bits (~1.5 decisions per input bit on text), plus a
+  // little per output byte for literals writes and match copies.
+  auto work = [&](uint32_t i) { return 24 * descs[i].src_len + descs[i].dst_cap; };
   auto by_len = [&](uint32_t a, uint32_t b) {
-    if (descs[a].dst_cap != descs[b].dst_cap) return descs[a].dst_cap > descs[b].dst_cap;
+    const uint64_t wa = work(a), wb = work(b);
+    if (wa != wb) return wa > wb;
     return w[a] > w[b];
   };
   std::stable_sort(lds_idx.begin(), lds_idx.end(), by_len);
@@ -725,7 +732,11 @@ SRes LzmaGpu_PlanBatchEx(LzmaGpuStreamDesc* descs, size_t n, uint32_t* order,
     plan->lds_cells_per_lane = stride;
     plan->groups_per_cu = std::min<uint32_t>(lds_per_cu / (lanes * stride * 2), 4 * occ);
     plan->waves_per_simd = occ;
+    plan->persistent = env_int("LZGPU_PERSIST", 1) ? 1u : 0u;
   }
+  // the LDS kernel's work counter, after the probability slices
+  plan->queue_offset = (plan->workspace_bytes + 63) & ~uint64_t(63);
+  plan->workspace_bytes = plan->queue_offset + 64;
   return SZ_OK;
 }
 
@@ -737,9 +748,22 @@ SRes LzmaGpu_DecodeBatchEx(const LzmaGpuPlan* plan, const LzmaGpuStreamDesc* d_d
   hipStream_t st = static_cast<hipStream_t>(stream);
   uint16_t* ws = static_cast<uint16_t*>(d_workspace);
   const uint32_t n_lds = uint32_t(plan->n_lds), n_glob = uint32_t(plan->n - plan->n_lds);
+  uint32_t max_groups = 0;
+  if (plan->persistent) {
+    static int cus = 0;
+    if (cus == 0) {
+      int dev = 0, v = 0;
+      (void)hipGetDevice(&dev);
+      if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
+        cus = v;
+    }
+    max_groups = uint32_t(cus) * plan->groups_per_cu;
+  }
+  uint32_t* queue = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(d_workspace) +
+                                                plan->queue_offset);
   if (n_lds && lzgpu_launch_decode_lds(d_descs, d_order, n_lds, d_src, d_dst, ws, d_results,
                                        plan->lanes_per_group, plan->lds_cells_per_lane,
-                                       plan->waves_per_simd, st) != 0) {
+                                       plan->waves_per_simd, max_groups, queue, st) != 0) {
     set_error("LDS decode kernel launch failed");
     return SZ_ERROR_FAIL;
   }

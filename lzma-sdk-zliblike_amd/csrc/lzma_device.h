@@ -183,6 +183,11 @@ typedef __attribute__((address_space(1))) uint32_t gu32;
 #ifndef LZGPU_COPY_V2
 #define LZGPU_COPY_V2 0
 #endif
+//   LZGPU_LIT_BATCH    literals decoded per pass of the symbol loop before a
+//                      lane's match path runs (1 = one symbol per pass)
+#ifndef LZGPU_LIT_BATCH
+#define LZGPU_LIT_BATCH 6
+#endif
 
 // Per-lane decoder state (CLzmaDec fields, LzmaDec.h:50-69).  lo = the LDS
 // table (pointer type Lo: lds_u16*; or gu16* aliasing gl when everything is
@@ -649,9 +654,20 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
 #endif
 
   do {
-    const uint32_t ps = total & pb_mask;
+    uint32_t ps;
     uint32_t lcoder_is_rep;
-    if (!rc.bit(T.template at<S_MATCH>((st << pb) + ps))) {
+    // Up to LZGPU_LIT_BATCH symbols per pass of this loop while they are
+    // literals: a lane's symbol sequence is unchanged, but lanes of a wave
+    // that sit in literal runs keep decoding together instead of idling
+    // behind a neighbour's match path on every symbol.
+    bool is_match = false, stop = false;
+#pragma unroll 1
+    for (int lit = 0; lit < LZGPU_LIT_BATCH; ++lit) {
+      ps = total & pb_mask;
+      if (rc.bit(T.template at<S_MATCH>((st << pb) + ps))) {
+        is_match = true;
+        break;
+      }
       uint32_t sym = 1;
       uint32_t ctx = 0;
       if (full != 0 || total != 0) ctx = ((total & lp_mask) << lc) + (prev >> (8 - lc));
@@ -678,8 +694,13 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
       prev = sym & 0xFFu;
       dic[pos++] = uint8_t(prev);
       total++;
-      continue;
+      if (!(pos < limit && rd.idx < in_limit)) {
+        stop = true;
+        break;
+      }
     }
+    if (stop) break;
+    if (!is_match) continue;
     if (!rc.bit(T.template at<S_REP>(st))) {
       st += 12;
       lcoder_is_rep = 0;

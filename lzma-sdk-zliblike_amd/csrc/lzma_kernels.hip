@@ -34,19 +34,26 @@ __global__ void __launch_bounds__(64) lzgpu_decode_batch_kernel(
 // W = minimum waves per SIMD the register allocation must allow (the
 // planner's occupancy target; more resident waves hide the serial decode
 // chain of each stream better, at the price of register spills).
+// Persistent lanes: the grid is sized to what is resident at once; a lane
+// that finishes its stream takes the next one from `queue` (a counter the
+// launcher zeroes), so no lane idles behind a slower neighbour in its wave
+// and the chip drains without a partial last round of workgroups.  Every
+// lane exits once the queue passes n.
 template <int W>
 __global__ void __launch_bounds__(64, W) lzgpu_decode_lds_kernel(
     const LzmaGpuStreamDesc* __restrict__ descs, const uint32_t* __restrict__ order, uint32_t n,
     const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, uint16_t* __restrict__ ws,
-    LzmaGpuResult* __restrict__ results, uint32_t stride) {
+    LzmaGpuResult* __restrict__ results, uint32_t stride, uint32_t* __restrict__ queue) {
   extern __shared__ uint32_t lz_smem[];
-  const uint32_t lane = blockIdx.x * blockDim.x + threadIdx.x;
-  if (lane >= n) return;
-  const uint32_t id = order ? order[lane] : lane;
-  const LzmaGpuStreamDesc d = descs[id];
-  lds_u16* lo = (lds_u16*)((uint16_t*)lz_smem) +
-                threadIdx.x * stride;
-  results[id] = lane_decode_lds(d, src, dst, ws, lo, stride);
+  lds_u16* lo = (lds_u16*)((uint16_t*)lz_smem) + threadIdx.x * stride;
+  const uint32_t lanes_total = gridDim.x * blockDim.x;
+  uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x;
+  while (idx < n) {
+    const uint32_t id = order ? order[idx] : idx;
+    const LzmaGpuStreamDesc d = descs[id];
+    results[id] = lane_decode_lds(d, src, dst, ws, lo, stride);
+    idx = lanes_total + atomicAdd(queue, 1u);
+  }
 }
 
 // One DecodeToDic call per lane on a device-resident decoder state.
@@ -73,17 +80,19 @@ template <int W>
 static int launch_lds(const LzmaGpuStreamDesc* d_descs, const uint32_t* d_order, uint32_t n,
                       const uint8_t* d_src, uint8_t* d_dst, uint16_t* d_ws,
                       LzmaGpuResult* d_results, uint32_t lanes, uint32_t stride,
-                      hipStream_t stream) {
+                      uint32_t max_groups, uint32_t* d_queue, hipStream_t stream) {
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(lzgpu_decode_lds_kernel<W>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
   }
+  if (hipMemsetAsync(d_queue, 0, sizeof(uint32_t), stream) != hipSuccess) return -1;
   const size_t lds = size_t(lanes) * stride * 2;
-  const uint32_t grid = (n + lanes - 1) / lanes;
+  uint32_t grid = (n + lanes - 1) / lanes;
+  if (max_groups && grid > max_groups) grid = max_groups;
   hipLaunchKernelGGL(lzgpu_decode_lds_kernel<W>, dim3(grid), dim3(lanes), lds, stream, d_descs,
-                     d_order, n, d_src, d_dst, d_ws, d_results, stride);
+                     d_order, n, d_src, d_dst, d_ws, d_results, stride, d_queue);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -91,12 +100,19 @@ extern "C" int lzgpu_launch_decode_lds(const LzmaGpuStreamDesc* d_descs, const u
                                        uint32_t n, const uint8_t* d_src, uint8_t* d_dst,
                                        uint16_t* d_ws, LzmaGpuResult* d_results, uint32_t lanes,
                                        uint32_t stride, uint32_t waves_per_simd,
+                                       uint32_t max_groups, uint32_t* d_queue,
                                        hipStream_t stream) {
   if (n == 0) return 0;
   switch (waves_per_simd) {
-    case 8: return launch_lds<8>(d_descs, d_order, n, d_src, d_dst, d_ws, d_results, lanes, stride, stream);
-    case 6: return launch_lds<6>(d_descs, d_order, n, d_src, d_dst, d_ws, d_results, lanes, stride, stream);
-    default: return launch_lds<4>(d_descs, d_order, n, d_src, d_dst, d_ws, d_results, lanes, stride, stream);
+    case 8:
+      return launch_lds<8>(d_descs, d_order, n, d_src, d_dst, d_ws, d_results, lanes, stride,
+                           max_groups, d_queue, stream);
+    case 6:
+      return launch_lds<6>(d_descs, d_order, n, d_src, d_dst, d_ws, d_results, lanes, stride,
+                           max_groups, d_queue, stream);
+    default:
+      return launch_lds<4>(d_descs, d_order, n, d_src, d_dst, d_ws, d_results, lanes, stride,
+                           max_groups, d_queue, stream);
   }
 }
 

@@ -95,9 +95,15 @@ __device__ __forceinline__ LzmaGpuResult lane_decode(const LzmaGpuStreamDesc& d,
   return r;
 }
 
-// One LZMA batch item with the LDS-placed sections (LZGPU_LDS_MASK) in the
-// lane's LDS slice (lo_cap cells) and the others in its global workspace
-// slice.  The planner only routes items here whose LDS part fits lo_cap.
+// LDS cells an LZMA2 range needs under placement M: its chunks may carry any
+// lc + lp <= 4 (Lzma2Dec.c:148) and pb <= 4.
+__host__ __device__ __forceinline__ uint32_t lzma2_lds_cells(uint32_t m) {
+  return make_layout(4, 0, 4, m).lds_cells;
+}
+
+// One LZMA (or LZMA2) batch item with the LDS-placed sections (LZGPU_LDS_MASK)
+// in the lane's LDS slice (lo_cap cells) and the others in its global
+// workspace slice.  The planner only routes items here whose LDS part fits.
 __device__ __forceinline__ LzmaGpuResult lane_decode_lds(const LzmaGpuStreamDesc& d,
                                                          const uint8_t* __restrict__ src,
                                                          uint8_t* __restrict__ dst,
@@ -107,6 +113,25 @@ __device__ __forceinline__ LzmaGpuResult lane_decode_lds(const LzmaGpuStreamDesc
   r.status = -1;
   r.dest_len = 0;
   r.src_len = 0;
+  if (d.kind == LZMA_GPU_KIND_LZMA2) {
+    // chunks may switch lc/lp/pb (lc + lp <= 4): the slice holds the widest layout
+    if (d.probs_off == LZMA_GPU_NO_WORKSPACE || lzma2_lds_cells(LZGPU_LDS_MASK) > lo_cap) {
+      r.res = (d.props[0] > 40) ? kErrUnsupported : kErrMem;
+      return r;
+    }
+    Lz2StateT<lds_u16*> p;
+    r.res = lz2_init(p, d.props[0], lo, (gu16*)(ws + d.probs_off), (gbyte*)(dst + d.dst_off),
+                     d.dst_cap);
+    if (r.res != kOk) return r;
+    uint64_t sl = d.src_len;
+    int status = kStNone;
+    r.res = lz2_decode_to_dic<LZGPU_LDS_MASK>(p, d.dst_cap, (const gbyte*)(src + d.src_off), sl,
+                                              d.finish_mode, status);
+    r.status = status;
+    r.dest_len = p.dec.pos;
+    r.src_len = sl;
+    return r;
+  }
   if (d.src_len < 5) {
     r.res = kErrInputEof;
     return r;

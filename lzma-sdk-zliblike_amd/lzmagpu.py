@@ -76,7 +76,8 @@ class Plan(ctypes.Structure):
     _fields_ = [("workspace_bytes", ctypes.c_uint64), ("n", ctypes.c_uint64),
                 ("n_lds", ctypes.c_uint64), ("lanes_per_group", ctypes.c_uint32),
                 ("lds_cells_per_lane", ctypes.c_uint32), ("groups_per_cu", ctypes.c_uint32),
-                ("waves_per_simd", ctypes.c_uint32), ("reserved", ctypes.c_uint32 * 8)]
+                ("waves_per_simd", ctypes.c_uint32), ("queue_offset", ctypes.c_uint64),
+                ("persistent", ctypes.c_uint32), ("reserved", ctypes.c_uint32 * 5)]
 
 
 assert ctypes.sizeof(StreamDesc) == 48 and ctypes.sizeof(Result) == 24

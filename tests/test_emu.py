@@ -25,6 +25,7 @@ EMU_VARIANTS = {
     "hot_only_lds": "-DLZGPU_LDS_MASK=0x107",
     "full_lds": "-DLZGPU_LDS_MASK=0x3FF",
     "copy_v2": "-DLZGPU_COPY_V2=1",
+    "lit_batch": "-DLZGPU_LIT_BATCH=3",
 }
 
 
@@ -71,8 +72,11 @@ def run_batch(emu, items, src, lds=False):
     # LDS slice large enough for any placement variant: the whole table
     stride = 0
     for k in range(plan.n_lds):
-        pr = bytes(descs[order[k]].props)
-        lc, lp, pb = pr[0] % 9, (pr[0] // 9) % 5, pr[0] // 45
+        if descs[order[k]].kind == L.KIND_LZMA2:
+            lc, lp, pb = 4, 0, 4  # chunks may switch props: widest layout
+        else:
+            pr = bytes(descs[order[k]].props)
+            lc, lp, pb = pr[0] % 9, (pr[0] // 9) % 5, pr[0] // 45
         stride = max(stride, (56 << pb) + 950 + (768 << (lc + lp)))
     for k in range(n):
         i = order[k]
@@ -108,14 +112,15 @@ def test_emu_golden_lzma_batch(emu, lds):
     assert not bad, bad[:10]
 
 
-def test_emu_golden_lzma2_batch(emu):
+@pytest.mark.parametrize("lds", [False, True])
+def test_emu_golden_lzma2_batch(emu, lds):
     import lzmagpu as L
     d = G.load()
     for i, c in G.cases("lzma2"):
         s = G.case_input(d, c)
         items = [dict(src_off=0, src_len=len(s), dst_off=0, dst_cap=c["dest_cap"],
                       props=bytes([c["prop"]]), finish=c["finish"], kind=L.KIND_LZMA2)]
-        res, dst = run_batch(emu, items, s + b"\0" * 16)
+        res, dst = run_batch(emu, items, s + b"\0" * 16, lds)
         e = c["expect"]
         got = (res[0].res, res[0].status, res[0].dest_len, res[0].src_len)
         assert got == (e["res"], e["status"], e["dest_len"], e["src_len"]), (i, c["note"])
