@@ -675,6 +675,9 @@ size_t LzmaGpu_PlanBatch(LzmaGpuStreamDesc* descs, size_t n, uint32_t* order) {
   return size_t(bytes);
 }
 
+// CUs the planner sizes for (MI355X: 256; LZGPU_CUS overrides)
+static const uint32_t kPlanCUs = uint32_t(env_int("LZGPU_CUS", 256));
+
 SRes LzmaGpu_PlanBatchEx(LzmaGpuStreamDesc* descs, size_t n, uint32_t* order,
                          LzmaGpuPlan* plan) {
   if (!order || !plan) return SZ_ERROR_PARAM;
@@ -716,21 +719,28 @@ SRes LzmaGpu_PlanBatchEx(LzmaGpuStreamDesc* descs, size_t n, uint32_t* order,
   if (plan->n_lds) {
     stride = (stride + 3) & ~3u;  // 8-byte aligned per-lane slices
     const uint32_t lds_per_cu = 160 * 1024;
-    const uint32_t per_cu = std::max<uint32_t>(1, lds_per_cu / (stride * 2));
-    // Measured (r01 sweep, 64K x 4 KiB): few streams per wave and many waves
-    // per SIMD win -- each stream is a serial chain, so the CU needs many
-    // independent waves in flight; SIMT width only adds divergence.  Aim for
-    // 16 workgroups (waves) per CU at 4 waves/SIMD.
-    uint32_t lanes = 1;
-    while (lanes * 2 <= 64 && lanes * 2 * 16 <= per_cu) lanes *= 2;
-    const int over = env_int("LZGPU_LANES", 0);
-    if (over > 0 && over <= 64 && uint32_t(over) * stride * 2 <= lds_per_cu) lanes = uint32_t(over);
+    const uint32_t per_cu = std::max<uint32_t>(1, lds_per_cu / (stride * 2));  // streams/CU
     uint32_t occ = 4;
     const int occ_over = env_int("LZGPU_OCC", 0);
     if (occ_over == 4 || occ_over == 6 || occ_over == 8) occ = uint32_t(occ_over);
+    // Measured (r01 A/B, 64K x 4 KiB): about 12-16
+    // streams per wave (the literal batching keeps lanes converged), as many
+    // waves as LDS allows, and a power-of-two workgroup count per CU so the
+    // four SIMDs carry equal loads (6, 10 or 12 workgroups per CU ran 10-30 %
+    // slower; profiles/r01_variants/v17, v18).
+    uint32_t lanes = std::min<uint32_t>(16, std::max<uint32_t>(1, per_cu / 4));
+    const int over = env_int("LZGPU_LANES", 0);
+    if (over > 0 && over <= 64 && uint32_t(over) * stride * 2 <= lds_per_cu) lanes = uint32_t(over);
+    // small batches: spread the streams over every CU before stacking lanes
+    const uint64_t spread = (plan->n_lds + uint64_t(kPlanCUs) * 4 - 1) / (uint64_t(kPlanCUs) * 4);
+    if (!over && spread < lanes) lanes = std::max<uint32_t>(1, uint32_t(spread));
+    uint32_t groups = std::min<uint32_t>(per_cu / lanes, 4 * occ);
+    while (groups & (groups - 1)) groups &= groups - 1;  // 4, 8 or 16 (12 measured slow)
+    const int g_over = env_int("LZGPU_GROUPS", 0);
+    if (g_over > 0 && uint32_t(g_over) * lanes <= per_cu) groups = uint32_t(g_over);
     plan->lanes_per_group = lanes;
     plan->lds_cells_per_lane = stride;
-    plan->groups_per_cu = std::min<uint32_t>(lds_per_cu / (lanes * stride * 2), 4 * occ);
+    plan->groups_per_cu = std::max<uint32_t>(1, groups);
     plan->waves_per_simd = occ;
     plan->persistent = env_int("LZGPU_PERSIST", 1) ? 1u : 0u;
   }
@@ -763,7 +773,8 @@ SRes LzmaGpu_DecodeBatchEx(const LzmaGpuPlan* plan, const LzmaGpuStreamDesc* d_d
                                                 plan->queue_offset);
   if (n_lds && lzgpu_launch_decode_lds(d_descs, d_order, n_lds, d_src, d_dst, ws, d_results,
                                        plan->lanes_per_group, plan->lds_cells_per_lane,
-                                       plan->waves_per_simd, max_groups, queue, st) != 0) {
+                                       plan->waves_per_simd, plan->groups_per_cu, max_groups,
+                                       queue, st) != 0) {
     set_error("LDS decode kernel launch failed");
     return SZ_ERROR_FAIL;
   }

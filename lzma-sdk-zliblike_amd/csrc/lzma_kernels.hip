@@ -80,7 +80,8 @@ template <int W>
 static int launch_lds(const LzmaGpuStreamDesc* d_descs, const uint32_t* d_order, uint32_t n,
                       const uint8_t* d_src, uint8_t* d_dst, uint16_t* d_ws,
                       LzmaGpuResult* d_results, uint32_t lanes, uint32_t stride,
-                      uint32_t max_groups, uint32_t* d_queue, hipStream_t stream) {
+                      uint32_t groups_per_cu, uint32_t max_groups, uint32_t* d_queue,
+                      hipStream_t stream) {
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(lzgpu_decode_lds_kernel<W>),
@@ -88,7 +89,13 @@ static int launch_lds(const LzmaGpuStreamDesc* d_descs, const uint32_t* d_order,
     attr_set = true;
   }
   if (hipMemsetAsync(d_queue, 0, sizeof(uint32_t), stream) != hipSuccess) return -1;
-  const size_t lds = size_t(lanes) * stride * 2;
+  // pad each workgroup's LDS so that exactly groups_per_cu fit on a CU (an
+  // even split over its four SIMDs), whatever the dispatcher would pack
+  size_t lds = size_t(lanes) * stride * 2;
+  if (groups_per_cu) {
+    const size_t share = (size_t(160 * 1024) / groups_per_cu) & ~size_t(511);
+    if (share > lds) lds = share;
+  }
   uint32_t grid = (n + lanes - 1) / lanes;
   if (max_groups && grid > max_groups) grid = max_groups;
   hipLaunchKernelGGL(lzgpu_decode_lds_kernel<W>, dim3(grid), dim3(lanes), lds, stream, d_descs,
@@ -100,19 +107,19 @@ extern "C" int lzgpu_launch_decode_lds(const LzmaGpuStreamDesc* d_descs, const u
                                        uint32_t n, const uint8_t* d_src, uint8_t* d_dst,
                                        uint16_t* d_ws, LzmaGpuResult* d_results, uint32_t lanes,
                                        uint32_t stride, uint32_t waves_per_simd,
-                                       uint32_t max_groups, uint32_t* d_queue,
-                                       hipStream_t stream) {
+                                       uint32_t groups_per_cu, uint32_t max_groups,
+                                       uint32_t* d_queue, hipStream_t stream) {
   if (n == 0) return 0;
   switch (waves_per_simd) {
     case 8:
       return launch_lds<8>(d_descs, d_order, n, d_src, d_dst, d_ws, d_results, lanes, stride,
-                           max_groups, d_queue, stream);
+                           groups_per_cu, max_groups, d_queue, stream);
     case 6:
       return launch_lds<6>(d_descs, d_order, n, d_src, d_dst, d_ws, d_results, lanes, stride,
-                           max_groups, d_queue, stream);
+                           groups_per_cu, max_groups, d_queue, stream);
     default:
       return launch_lds<4>(d_descs, d_order, n, d_src, d_dst, d_ws, d_results, lanes, stride,
-                           max_groups, d_queue, stream);
+                           groups_per_cu, max_groups, d_queue, stream);
   }
 }
 
