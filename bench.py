@@ -1,6 +1,6 @@
 """bench.py -- batch LZMA decode throughput on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg3|cfg2|cfg5]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg3|cfg2|cfg4]
 
 One "step" = one launch of the batch decode kernel over the whole per-GPU
 batch (inputs already resident in HBM, outputs written to HBM).  Default
@@ -16,6 +16,11 @@ kernel (HIP events on the launch stream) and the CPU baseline: the oracle
 restatement (oracle/liboracle.so, a checker, never the measured product)
 timed on this host's cores over a bounded sample of the same workload.
 Every timed batch is verified bit-exact against its plaintext afterwards.
+
+--config cfg4: 1 MiB LZMA2 dict-reset blocks, 1024
+per GPU, one compressed file on rank 0 scattered to the peers over RCCL
+(grouped point-to-point, the only data exchange of the path), one block per
+lane; the scatter is timed and reported separately.
 """
 import argparse
 import ctypes
@@ -165,6 +170,213 @@ def measure_crc(L, torch, descs, d_desc, d_res, d_dst, plain, count, n, stream, 
             "verified": bool(np.array_equal(got, want))}
 
 
+# ---------------------------------------------------------------- config 4
+
+CFG4_BLOCK = 1 << 20     # 1 MiB dict-reset blocks (Lzma2Enc.c MT layout)
+CFG4_PROP = 16           # LZMA2 dict prop: 1 MiB
+CFG4_UNIQUE = 64         # distinct blocks generated; the file repeats them
+
+
+def _compress_lzma2_block(i):
+    import native
+    data = native.gen("text", 50000 + i, CFG4_BLOCK)
+    f = [{"id": lzma.FILTER_LZMA2, "dict_size": CFG4_BLOCK, "lc": 3, "lp": 0, "pb": 2,
+          "preset": 6}]
+    c = lzma.compress(data, format=lzma.FORMAT_RAW, filters=f)
+    assert c[-1] == 0
+    return i, c[:-1], zlib_crc(data)
+
+
+def zlib_crc(b):
+    import zlib
+    return zlib.crc32(b)
+
+
+def build_cfg4_unique(workers):
+    tmp = os.environ.get("TMPDIR", "/tmp")
+    path = os.path.join(tmp, f"lzgpu_cfg4_u{CFG4_UNIQUE}_v1.npz")
+    if os.path.exists(path):
+        z = np.load(path)
+        comp, lens, crcs = z["comp"], z["lens"], z["crcs"]
+        parts, o = [], 0
+        for ln in lens:
+            parts.append(comp[o:o + int(ln)].tobytes())
+            o += int(ln)
+        return parts, [int(c) for c in crcs]
+    t0 = time.time()
+    parts, crcs = [None] * CFG4_UNIQUE, [0] * CFG4_UNIQUE
+    with mp.get_context("fork").Pool(workers) as pool:
+        for i, c, crc in pool.imap_unordered(_compress_lzma2_block, range(CFG4_UNIQUE)):
+            parts[i], crcs[i] = c, crc
+    np.savez(path, comp=np.frombuffer(b"".join(parts), dtype=np.uint8),
+             lens=np.array([len(c) for c in parts], dtype=np.uint64),
+             crcs=np.array(crcs, dtype=np.uint64))
+    log(f"[rank 0] compressed {CFG4_UNIQUE} LZMA2 blocks in {time.time() - t0:.1f}s")
+    return parts, crcs
+
+
+def run_cfg4(args):
+    import dist_bench as D
+    world, rank, local_rank = D.world_info()
+    cpus = os.cpu_count() or 8
+    workers = max(1, min(16, cpus // max(1, world)))
+    B = args.blocks
+    parts = crcs = None
+    if rank == 0:
+        parts, crcs = build_cfg4_unique(workers)  # before the GPU is touched (fork pool)
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    import lzmagpu as L
+    # rank 0: the whole file (world x B blocks + EOS) and its block table
+    meta = [None]
+    if rank == 0:
+        seq = [b % CFG4_UNIQUE for b in range(world * B)]
+        blob = b"".join(parts[u] for u in seq) + b"\0"
+        blocks = L.split_lzma2_blocks(blob)  # host header walk, O(#chunks)
+        assert len(blocks) == world * B
+        ranges = [(int(blocks[r * B][0]), int(blocks[(r + 1) * B - 1][0] + blocks[(r + 1) * B - 1][1]))
+                  for r in range(world)]
+        table = [[(int(o), int(ln), int(u)) for o, ln, u in blocks[r * B:(r + 1) * B]]
+                 for r in range(world)]
+        meta = [(ranges, table, [crcs[u] for u in seq], len(blob))]
+        d_file = torch.frombuffer(bytearray(blob), dtype=torch.uint8).to(dev)
+    if world > 1:
+        dist.broadcast_object_list(meta, src=0)
+    ranges, table, crc_seq, file_bytes = meta[0]
+    lo, hi = ranges[rank]
+    mine = table[rank]
+    d_src = torch.empty(max(hi - lo, 16) + 16, dtype=torch.uint8, device=dev)
+    if world == 1:
+        d_src[:hi - lo].copy_(d_file[lo:hi])
+    items, doff = [], 0
+    for o, ln, u in mine:
+        items.append(dict(src_off=o - lo, src_len=ln, dst_off=doff, dst_cap=u,
+                          props=bytes([CFG4_PROP]), finish=0, kind=L.KIND_LZMA2))
+        doff += u
+    descs = L.make_descs(items)
+    plan, order = L.plan_ex(descs)
+    d_dst = torch.empty(doff + 16, dtype=torch.uint8, device=dev)
+    d_ws = torch.empty(max(int(plan.workspace_bytes), 16), dtype=torch.uint8, device=dev)
+    d_desc = torch.frombuffer(bytearray(bytes(descs)), dtype=torch.uint8).to(dev)
+    d_order = torch.frombuffer(bytearray(bytes(order)), dtype=torch.uint8).to(dev)
+    d_res = torch.empty(B * 24, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    sh = stream.cuda_stream
+    out_view = d_src[:hi - lo]
+
+    def scatter():
+        if world > 1:
+            D.scatter_ranges(d_file if rank == 0 else None, ranges, out_view, rank, world)
+
+    def decode():
+        r = L.decode_batch_device_ex(plan, d_desc.data_ptr(), d_order.data_ptr(), d_src.data_ptr(),
+                                     d_dst.data_ptr(), d_ws.data_ptr(), d_res.data_ptr(), sh)
+        if r != 0:
+            raise RuntimeError("LzmaGpu_DecodeBatchEx failed: " + L.last_error())
+
+    for _ in range(args.warmup):
+        scatter()
+        decode()
+    torch.cuda.synchronize()
+    D.barrier()
+    torch.cuda.synchronize()
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ev[i][0].record(stream)
+        scatter()
+        ev[i][1].record(stream)
+        decode()
+        ev[i][2].record(stream)
+    torch.cuda.synchronize()
+    D.barrier()
+    torch.cuda.synchronize()
+    elapsed = D.reduce_max(time.perf_counter() - t0, dev)
+    scat_ms = float(np.mean([a.elapsed_time(b) for a, b, _ in ev]))
+    dec_ms = float(np.mean([b.elapsed_time(c) for _, b, c in ev]))
+    scat_ms = D.reduce_max(scat_ms, dev)
+
+    # verify: per-block results and the CRC of every decoded block (on the GPU)
+    res = np.frombuffer(d_res.cpu().numpy().tobytes(), dtype=np.dtype(
+        [("res", "<i4"), ("status", "<i4"), ("dest_len", "<u8"), ("src_len", "<u8")]))
+    ok = bool((res["res"] == 0).all() and (res["status"] == 2).all() and
+              (res["dest_len"] == np.array([u for _, _, u in mine])).all() and
+              (res["src_len"] == np.array([ln for _, ln, _ in mine])).all())
+    base, crange, total = L.crc32_plan_decoded(descs)
+    d_base = torch.frombuffer(bytearray(base), dtype=torch.uint8).to(dev)
+    d_range = torch.frombuffer(bytearray(crange), dtype=torch.uint8).to(dev)
+    d_chunks = torch.empty(max(total, 1) * 4, dtype=torch.uint8, device=dev)
+    d_crc = torch.empty(B * 4, dtype=torch.uint8, device=dev)
+    assert L.crc32_batch_decoded(d_desc.data_ptr(), d_res.data_ptr(), B, d_dst.data_ptr(),
+                                 d_base.data_ptr(), d_range.data_ptr(), total,
+                                 d_chunks.data_ptr(), d_crc.data_ptr(), sh) == 0
+    got = np.frombuffer(d_crc.cpu().numpy().tobytes(), dtype="<u4")
+    ok = ok and bool(np.array_equal(got, np.array(crc_seq[rank * B:(rank + 1) * B],
+                                                  dtype=np.uint32)))
+    ok = D.all_true(ok, dev)
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cfg4_cpu_baseline(parts, min(cpus, 16))
+    total_bytes = world * B * CFG4_BLOCK * args.steps
+    value = total_bytes / elapsed / 1e6
+    comp_bytes = hi - lo
+    alg = comp_bytes + B * CFG4_BLOCK
+    achieved = alg / (dec_ms * 1e-3) / 1e9
+    if rank == 0:
+        print(json.dumps({
+            "metric": "decompressed MB/s (whole node), config 4: 1 MiB LZMA2 dict-reset blocks",
+            "value": round(value, 2), "unit": "MB/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+            "data": f"synthetic text, {CFG4_UNIQUE} distinct liblzma LZMA2 blocks repeated",
+            "config": {"workload": f"{B} x 1 MiB LZMA2 blocks per GPU (lc3/lp0/pb2, dict 1 MiB), "
+                                   "one file on rank 0 scattered over RCCL",
+                       "blocks_per_gpu": B, "compressed_bytes_per_gpu": comp_bytes,
+                       "file_bytes": file_bytes,
+                       "kernel_plan": {"lds_streams": int(plan.n_lds),
+                                       "streams_per_workgroup": int(plan.lanes_per_group),
+                                       "workgroups_per_cu": int(plan.groups_per_cu)},
+                       "exchange": {"collective": "grouped P2P isend/irecv from rank 0"
+                                    if world > 1 else "none (1 GPU)",
+                                    "scatter_ms": round(scat_ms, 4),
+                                    "bytes_per_peer": comp_bytes}},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
+                         "traffic": None, "kernel": "lzgpu_decode_lds_kernel",
+                         "kernel_avg_ms": round(dec_ms, 4), "alg_bytes_per_launch": alg},
+            "cpu_baseline": cpu, "verified": ok}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    if not ok:
+        sys.exit(3)
+
+
+def cfg4_cpu_baseline(parts, threads):
+    """Oracle LZMA2 decode of distinct blocks on a thread pool (ctypes drops the GIL)."""
+    import native
+    from concurrent.futures import ThreadPoolExecutor
+    orc = native.oracle()
+    sample = parts[:min(len(parts), 2 * threads)]
+
+    def one(c):
+        r = native.lzma2_decode(orc, "orc", c, CFG4_PROP, CFG4_BLOCK, 0)
+        return r[0] == 0 and r[2] == CFG4_BLOCK
+
+    t0 = time.perf_counter()
+    with ThreadPoolExecutor(threads) as ex:
+        oks = list(ex.map(one, sample))
+    dt = time.perf_counter() - t0
+    return {"value": round(len(sample) * CFG4_BLOCK / dt / 1e6, 2), "unit": "MB/s",
+            "cores": threads, "kind": "port",
+            "sample": f"{len(sample)} distinct 1 MiB blocks, {threads} threads, {dt:.2f}s",
+            "errors": int(len(oks) - sum(oks))}
+
+
 def cpu_baseline(comp, lens, offs, n, props, threads, sample_streams):
     """The oracle restatement (CPU port of LzmaDec) on a bounded sample."""
     import native
@@ -191,10 +403,13 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="cfg3", choices=sorted(CONFIGS))
+    ap.add_argument("--config", default="cfg3", choices=sorted(CONFIGS) + ["cfg4"])
+    ap.add_argument("--blocks", type=int, default=1024, help="cfg4: LZMA2 blocks per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-crc", action="store_true", help="skip the CRC-32 (8(f) row 1) leg")
     args = ap.parse_args()
+    if args.config == "cfg4":
+        return run_cfg4(args)
 
     import dist_bench as D
     world, rank, local_rank = D.world_info()

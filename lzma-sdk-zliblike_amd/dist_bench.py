@@ -5,6 +5,11 @@ of a global batch with no data-path collective.  The only collectives are the
 timing/verification reductions (barrier, MAX of elapsed time, MIN of the
 verified flag), which work on both backends: "nccl" (RCCL over xGMI, CUDA
 tensors) on the GPU box and "gloo" (CPU tensors) in the CPU test-suite.
+
+Config 4 (LZMA2 dict-reset blocks) has the one real exchange:
+the compressed file sits on rank 0 and each peer receives the byte range of its
+blocks (and its block table) by point-to-point sends -- RCCL over xGMI on the
+box, one link per peer, all sends posted as one group.
 """
 import os
 
@@ -80,3 +85,27 @@ def barrier():
     import torch.distributed as dist
     if dist.is_initialized() and dist.get_world_size() > 1:
         dist.barrier()
+
+
+def scatter_ranges(src, ranges, out, rank, world):
+    """Rank 0 sends src[lo:hi] of ranges[r] = (lo, hi) to rank r; every rank
+    gets its own range in `out` (rank 0 copies locally).  src is only read on
+    rank 0 (None elsewhere); out has hi - lo elements on each rank.  All
+    transfers are posted as one batch (grouped point-to-point)."""
+    import torch.distributed as dist
+    lo, hi = ranges[rank]
+    if rank == 0:
+        out.copy_(src[lo:hi])
+    if world == 1:
+        return
+    ops = []
+    if rank == 0:
+        for r in range(1, world):
+            a, b = ranges[r]
+            if b > a:
+                ops.append(dist.P2POp(dist.isend, src[a:b], r))
+    elif hi > lo:
+        ops.append(dist.P2POp(dist.irecv, out, 0))
+    if ops:
+        for req in dist.batch_isend_irecv(ops):
+            req.wait()

@@ -79,6 +79,58 @@ def test_two_rank_gloo_sharding_and_reductions():
     assert eq == [(0, 19), (19, 18)]
 
 
+def _scatter_worker(rank, world, port, q):
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    sys.path.insert(0, os.path.join(ROOT, "lzma-sdk-zliblike_amd"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import lzma
+    import torch
+    import torch.distributed as dist
+    import dist_bench as D
+    import native
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        # config-4 shape: rank 0 holds an LZMA2 stream of dict-reset blocks
+        # (the MT-encoder layout) and scatters each rank's block range
+        per_rank, plain = 3, [native.gen("text", 4400 + i, 20000 + 777 * i) for i in range(6)]
+        f = [{"id": lzma.FILTER_LZMA2, "dict_size": 1 << 16, "lc": 3, "lp": 0, "pb": 2}]
+        comps = [lzma.compress(b, format=lzma.FORMAT_RAW, filters=f)[:-1] for b in plain]
+        offs = [0]
+        for c in comps:
+            offs.append(offs[-1] + len(c))
+        ranges = [(offs[r * per_rank], offs[(r + 1) * per_rank]) for r in range(world)]
+        src = torch.frombuffer(bytearray(b"".join(comps)), dtype=torch.uint8) if rank == 0 else None
+        lo, hi = ranges[rank]
+        out = torch.empty(hi - lo, dtype=torch.uint8)
+        D.scatter_ranges(src, ranges, out, rank, world)
+        mine = out.numpy().tobytes()
+        orc = native.oracle()
+        ok = True
+        for k in range(per_rank):
+            b = rank * per_rank + k
+            blk = mine[offs[b] - lo:offs[b + 1] - lo]
+            res, st, dl, sl, data = native.lzma2_decode(orc, "orc", blk, 16, len(plain[b]), 0)
+            ok = ok and (res, st, dl, sl) == (0, 2, len(plain[b]), len(blk)) and data == plain[b]
+        q.put((rank, len(mine), ok))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_gloo_lzma2_block_scatter():
+    world = 2
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_scatter_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = sorted(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(ok and n > 0 for _, n, ok in out)
+
+
 def test_shard_helpers_single_process():
     sys.path.insert(0, os.path.join(ROOT, "lzma-sdk-zliblike_amd"))
     import dist_bench as D
