@@ -720,9 +720,10 @@ SRes LzmaGpu_PlanBatchEx(LzmaGpuStreamDesc* descs, size_t n, uint32_t* order,
     stride = (stride + 3) & ~3u;  // 8-byte aligned per-lane slices
     const uint32_t lds_per_cu = 160 * 1024;
     const uint32_t per_cu = std::max<uint32_t>(1, lds_per_cu / (stride * 2));  // streams/CU
-    uint32_t occ = 4;
+    uint32_t occ = 4;  // register budget while sizing; re-derived below
     const int occ_over = env_int("LZGPU_OCC", 0);
-    if (occ_over == 4 || occ_over == 6 || occ_over == 8) occ = uint32_t(occ_over);
+    if (occ_over == 1 || occ_over == 2 || occ_over == 4 || occ_over == 6 || occ_over == 8)
+      occ = uint32_t(occ_over);
     // Measured (r01 A/B, 64K x 4 KiB): about 12-16
     // streams per wave (the literal batching keeps lanes converged), as many
     // waves as LDS allows, and a power-of-two workgroup count per CU so the
@@ -734,13 +735,17 @@ SRes LzmaGpu_PlanBatchEx(LzmaGpuStreamDesc* descs, size_t n, uint32_t* order,
     // small batches: spread the streams over every CU before stacking lanes
     const uint64_t spread = (plan->n_lds + uint64_t(kPlanCUs) * 4 - 1) / (uint64_t(kPlanCUs) * 4);
     if (!over && spread < lanes) lanes = std::max<uint32_t>(1, uint32_t(spread));
-    uint32_t groups = std::min<uint32_t>(per_cu / lanes, 4 * occ);
+    uint32_t groups = std::min<uint32_t>(per_cu / lanes, occ_over ? 4 * occ : 16u);
     while (groups & (groups - 1)) groups &= groups - 1;  // 4, 8 or 16 (12 measured slow)
     const int g_over = env_int("LZGPU_GROUPS", 0);
     if (g_over > 0 && uint32_t(g_over) * lanes <= per_cu) groups = uint32_t(g_over);
     plan->lanes_per_group = lanes;
     plan->lds_cells_per_lane = stride;
     plan->groups_per_cu = std::max<uint32_t>(1, groups);
+    // register budget = the waves per SIMD that are actually resident (one
+    // wave per workgroup): 8 workgroups per CU -> 2 waves/SIMD -> 256 VGPRs,
+    // enough for the decoder state without spills
+    if (!occ_over) occ = std::max<uint32_t>(1, (plan->groups_per_cu + 3) / 4);
     plan->waves_per_simd = occ;
     plan->persistent = env_int("LZGPU_PERSIST", 1) ? 1u : 0u;
   }

@@ -188,6 +188,11 @@ typedef __attribute__((address_space(1))) uint32_t gu32;
 #ifndef LZGPU_LIT_BATCH
 #define LZGPU_LIT_BATCH 6
 #endif
+//   LZGPU_UNIFORM_EXIT the literal batch loop exits only when every lane of
+//                      the wave is done (lanes drop out by a flag)
+#ifndef LZGPU_UNIFORM_EXIT
+#define LZGPU_UNIFORM_EXIT 1
+#endif
 
 // Per-lane decoder state (CLzmaDec fields, LzmaDec.h:50-69).  lo = the LDS
 // table (pointer type Lo: lds_u16*; or gu16* aliasing gl when everything is
@@ -626,6 +631,54 @@ __device__ __forceinline__ uint32_t lit_bit(Rc<Rd>& rc, const Tab<M, Lo>& T, uin
   }
 }
 
+// One literal (LzmaDec.c:161-196): plain tree for state < 7, matched tree
+// against the byte at rep0 otherwise; writes the byte, updates state.
+template <uint32_t M, class Lo, class Rd>
+__device__ __forceinline__ void lz_literal(Rc<Rd>& rc, const Tab<M, Lo>& T, uint32_t& st,
+                                           uint32_t& prev, uint32_t& total, uint32_t full,
+                                           uint32_t lc, uint32_t lp_mask, gbyte* dic,
+                                           uint64_t& pos, uint64_t cap, uint32_t r0
+#if LZGPU_MB_PF
+                                           , uint32_t mb_pf
+#endif
+) {
+  uint32_t sym = 1;
+  uint32_t ctx = 0;
+  if (full != 0 || total != 0) ctx = ((total & lp_mask) << lc) + (prev >> (8 - lc));
+  if (st < 7) {
+    st = (st < 4) ? 0 : st - 3;
+    sym = 0x100u | rc.template tree<8>(T.template at<S_LITP>(ctx << 8));
+  } else {
+#if LZGPU_MB_PF
+    uint32_t mbyte = mb_pf;
+#else
+    uint32_t mbyte = dic[ring_back(pos, r0, cap)];
+#endif
+    uint32_t offs = 0x100;
+    st = (st < 10) ? st - 3 : st - 6;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      mbyte <<= 1;
+      const uint32_t mbit = mbyte & offs;
+      const uint32_t b = lit_bit(rc, T, ctx, offs + mbit, sym);
+      sym = (sym << 1) | b;
+      offs = b ? (offs & mbit) : (offs & ~mbit);
+    }
+  }
+  prev = sym & 0xFFu;
+  dic[pos++] = uint8_t(prev);
+  total++;
+}
+
+// any lane of the wave (the lane itself in the host emulation)
+__device__ __forceinline__ bool lz_any(bool v) {
+#ifdef LZGPU_HOST_EMU
+  return v;
+#else
+  return __builtin_amdgcn_ballot_w64(v) != 0;
+#endif
+}
+
 // Decode symbols until pos reaches `limit` or the reader index reaches
 // `in_limit` (checked after each whole symbol; the first is always decoded).
 // State is written back only on success, as LzmaDec_DecodeReal does.
@@ -661,6 +714,33 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
     // that sit in literal runs keep decoding together instead of idling
     // behind a neighbour's match path on every symbol.
     bool is_match = false, stop = false;
+#if LZGPU_UNIFORM_EXIT
+    // lanes leave the batch by clearing lit_on, the loop itself exits only
+    // when the whole wave is done: no divergent exit, so no per-iteration
+    // copies of the lane state into exit registers
+    bool lit_on = true;
+#pragma unroll 1
+    for (int lit = 0; lit < LZGPU_LIT_BATCH; ++lit) {
+      if (lit_on) {
+        ps = total & pb_mask;
+        if (rc.bit(T.template at<S_MATCH>((st << pb) + ps))) {
+          is_match = true;
+          lit_on = false;
+        } else {
+          lz_literal<M>(rc, T, st, prev, total, full, lc, lp_mask, dic, pos, cap, r0
+#if LZGPU_MB_PF
+                        , mb_pf
+#endif
+          );
+          if (!(pos < limit && rd.idx < in_limit)) {
+            stop = true;
+            lit_on = false;
+          }
+        }
+      }
+      if (!lz_any(lit_on)) break;
+    }
+#else
 #pragma unroll 1
     for (int lit = 0; lit < LZGPU_LIT_BATCH; ++lit) {
       ps = total & pb_mask;
@@ -668,37 +748,17 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
         is_match = true;
         break;
       }
-      uint32_t sym = 1;
-      uint32_t ctx = 0;
-      if (full != 0 || total != 0) ctx = ((total & lp_mask) << lc) + (prev >> (8 - lc));
-      if (st < 7) {
-        st = (st < 4) ? 0 : st - 3;
-        sym = 0x100u | rc.template tree<8>(T.template at<S_LITP>(ctx << 8));
-      } else {
+      lz_literal<M>(rc, T, st, prev, total, full, lc, lp_mask, dic, pos, cap, r0
 #if LZGPU_MB_PF
-        uint32_t mbyte = mb_pf;
-#else
-        uint32_t mbyte = dic[ring_back(pos, r0, cap)];
+                    , mb_pf
 #endif
-        uint32_t offs = 0x100;
-        st = (st < 10) ? st - 3 : st - 6;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          mbyte <<= 1;
-          const uint32_t mbit = mbyte & offs;
-          const uint32_t b = lit_bit(rc, T, ctx, offs + mbit, sym);
-          sym = (sym << 1) | b;
-          offs = b ? (offs & mbit) : (offs & ~mbit);
-        }
-      }
-      prev = sym & 0xFFu;
-      dic[pos++] = uint8_t(prev);
-      total++;
+      );
       if (!(pos < limit && rd.idx < in_limit)) {
         stop = true;
         break;
       }
     }
+#endif
     if (stop) break;
     if (!is_match) continue;
     if (!rc.bit(T.template at<S_REP>(st))) {

@@ -117,6 +117,12 @@ extern "C" int lzgpu_launch_decode_lds(const LzmaGpuStreamDesc* d_descs, const u
     case 6:
       return launch_lds<6>(d_descs, d_order, n, d_src, d_dst, d_ws, d_results, lanes, stride,
                            groups_per_cu, max_groups, d_queue, stream);
+    case 2:
+      return launch_lds<2>(d_descs, d_order, n, d_src, d_dst, d_ws, d_results, lanes, stride,
+                           groups_per_cu, max_groups, d_queue, stream);
+    case 1:
+      return launch_lds<1>(d_descs, d_order, n, d_src, d_dst, d_ws, d_results, lanes, stride,
+                           groups_per_cu, max_groups, d_queue, stream);
     default:
       return launch_lds<4>(d_descs, d_order, n, d_src, d_dst, d_ws, d_results, lanes, stride,
                            groups_per_cu, max_groups, d_queue, stream);

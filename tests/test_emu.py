@@ -26,6 +26,7 @@ EMU_VARIANTS = {
     "full_lds": "-DLZGPU_LDS_MASK=0x3FF",
     "copy_v2": "-DLZGPU_COPY_V2=1",
     "lit_batch": "-DLZGPU_LIT_BATCH=3",
+    "uniform_exit": "-DLZGPU_UNIFORM_EXIT=1",
 }
 
 
