@@ -149,12 +149,13 @@ typedef __attribute__((address_space(1))) uint32_t gu32;
 
 // Build-time code-shape switches (A/B'd on MI355X):
 //   LZGPU_NORM_BRANCHLESS  NORMALIZE as selects instead of a skip-able branch
-//   LZGPU_BIT_MASK         decision/update as mask arithmetic instead of if/else
+//   LZGPU_BIT_MASK         decision/update: 0 if/else, 1 mask arithmetic, 2 selects
+//                          with the shared-form update p - ((p - m) >> 5) (default)
 #ifndef LZGPU_NORM_BRANCHLESS
 #define LZGPU_NORM_BRANCHLESS 0
 #endif
 #ifndef LZGPU_BIT_MASK
-#define LZGPU_BIT_MASK 0
+#define LZGPU_BIT_MASK 2
 #endif
 //   LZGPU_TREE_PF      bit-trees read both children of the next level (one
 //                      32-bit read) while the current decision resolves
@@ -432,7 +433,17 @@ struct Rc {
     const uint32_t p = *prob;
     norm();
     const uint32_t bound = (range >> 11) * p;
-#if LZGPU_BIT_MASK
+#if LZGPU_BIT_MASK == 2
+    // selects only: with b = (code >= bound),
+    //   UPDATE_0: p + ((2048 - p) >> 5) == p - ((p - 2017) >> 5)  (arithmetic >>)
+    //   UPDATE_1: p - (p >> 5)          == p - ((p - 0) >> 5)
+    const bool b = code >= bound;
+    const int32_t m = b ? 0 : int32_t(kProbOne - 31);
+    *prob = uint16_t(int32_t(p) - ((int32_t(p) - m) >> 5));
+    range = b ? range - bound : bound;
+    code = b ? code - bound : code;
+    return b ? 1u : 0u;
+#elif LZGPU_BIT_MASK
     // mask arithmetic: lanes of a wave sit on different symbol paths, and the
     // compiler otherwise turns the two updates into a divergent if/else
     const uint32_t mask = 0u - uint32_t(code >= bound);

@@ -27,6 +27,8 @@ EMU_VARIANTS = {
     "copy_v2": "-DLZGPU_COPY_V2=1",
     "lit_batch": "-DLZGPU_LIT_BATCH=3",
     "uniform_exit": "-DLZGPU_UNIFORM_EXIT=1",
+    "bit_select_rd4": "-DLZGPU_BIT_MASK=2 -DLZGPU_READER16=0",
+    "bit_branchy": "-DLZGPU_BIT_MASK=0",
 }
 
 
