@@ -187,7 +187,13 @@ typedef __attribute__((address_space(1))) uint32_t gu32;
 //   LZGPU_LIT_BATCH    literals decoded per pass of the symbol loop before a
 //                      lane's match path runs (1 = one symbol per pass)
 #ifndef LZGPU_LIT_BATCH
-#define LZGPU_LIT_BATCH 6
+#define LZGPU_LIT_BATCH 8
+#endif
+//   LZGPU_MLIT_PF      matched literal with the matched-tree cells in global
+//                      memory: load the eight cells of the all-match path at
+//                      once (one round trip instead of up to eight)
+#ifndef LZGPU_MLIT_PF
+#define LZGPU_MLIT_PF 1
 #endif
 //   LZGPU_UNIFORM_EXIT the literal batch loop exits only when every lane of
 //                      the wave is done (lanes drop out by a flag)
@@ -468,6 +474,14 @@ struct Rc {
   __device__ __forceinline__ uint32_t bit_v(uint32_t p, P prob) {
     norm();
     const uint32_t bound = (range >> 11) * p;
+#if LZGPU_BIT_MASK == 2
+    const bool b = code >= bound;
+    const int32_t m = b ? 0 : int32_t(kProbOne - 31);
+    *prob = uint16_t(int32_t(p) - ((int32_t(p) - m) >> 5));
+    range = b ? range - bound : bound;
+    code = b ? code - bound : code;
+    return b ? 1u : 0u;
+#endif
     if (code < bound) {
       range = bound;
       *prob = uint16_t(p + ((kProbOne - p) >> 5));
@@ -665,15 +679,43 @@ __device__ __forceinline__ void lz_literal(Rc<Rd>& rc, const Tab<M, Lo>& T, uint
 #else
     uint32_t mbyte = dic[ring_back(pos, r0, cap)];
 #endif
-    uint32_t offs = 0x100;
     st = (st < 10) ? st - 3 : st - 6;
+    constexpr bool p_lds = ((M >> S_LITP) & 1u) != 0u, m_lds = ((M >> S_LITM) & 1u) != 0u;
+    if constexpr (LZGPU_MLIT_PF && p_lds && !m_lds) {
+      // While the decoded bits equal the match byte's, the cell of bit k is
+      // fixed by the match byte alone (offs stays 0x100, symbol = its top k
+      // bits under a leading 1): load all eight matched-tree cells at once
+      // instead of one dependent global round trip per bit.  After the first
+      // mismatch the walk continues in the plain tree (LDS), as the
+      // reference's offs = 0 does.
+      const uint32_t mb = mbyte & 0xFFu;
+      auto lm = T.template at<S_LITM>(ctx << 9);
+      uint32_t pk[8];
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      mbyte <<= 1;
-      const uint32_t mbit = mbyte & offs;
-      const uint32_t b = lit_bit(rc, T, ctx, offs + mbit, sym);
-      sym = (sym << 1) | b;
-      offs = b ? (offs & mbit) : (offs & ~mbit);
+      for (int k = 0; k < 8; ++k)
+        pk[k] = lm[(((mb >> (7 - k)) & 1u) << 8) + ((1u << k) | (mb >> (8 - k)))];
+      bool matched = true;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const uint32_t mk = (mb >> (7 - k)) & 1u;
+        uint32_t b;
+        if (matched)
+          b = rc.bit_v(pk[k], lm + ((mk << 8) + sym));
+        else
+          b = rc.bit(T.template at<S_LITP>((ctx << 8) + sym));
+        matched = matched && (b == mk);
+        sym = (sym << 1) | b;
+      }
+    } else {
+      uint32_t offs = 0x100;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        mbyte <<= 1;
+        const uint32_t mbit = mbyte & offs;
+        const uint32_t b = lit_bit(rc, T, ctx, offs + mbit, sym);
+        sym = (sym << 1) | b;
+        offs = b ? (offs & mbit) : (offs & ~mbit);
+      }
     }
   }
   prev = sym & 0xFFu;

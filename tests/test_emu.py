@@ -28,7 +28,7 @@ EMU_VARIANTS = {
     "lit_batch": "-DLZGPU_LIT_BATCH=3",
     "uniform_exit": "-DLZGPU_UNIFORM_EXIT=1",
     "bit_select_rd4": "-DLZGPU_BIT_MASK=2 -DLZGPU_READER16=0",
-    "bit_branchy": "-DLZGPU_BIT_MASK=0",
+    "bit_branchy": "-DLZGPU_BIT_MASK=0 -DLZGPU_MLIT_PF=0",
 }
 
 
