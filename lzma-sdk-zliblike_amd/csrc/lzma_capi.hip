@@ -724,19 +724,33 @@ SRes LzmaGpu_PlanBatchEx(LzmaGpuStreamDesc* descs, size_t n, uint32_t* order,
     const int occ_over = env_int("LZGPU_OCC", 0);
     if (occ_over == 1 || occ_over == 2 || occ_over == 4 || occ_over == 6 || occ_over == 8)
       occ = uint32_t(occ_over);
-    // Measured (r01 A/B, 64K x 4 KiB): about 12-16
-    // streams per wave (the literal batching keeps lanes converged), as many
-    // waves as LDS allows, and a power-of-two workgroup count per CU so the
-    // four SIMDs carry equal loads (6, 10 or 12 workgroups per CU ran 10-30 %
-    // slower; profiles/r01_variants/v17, v18).
-    uint32_t lanes = std::min<uint32_t>(16, std::max<uint32_t>(1, per_cu / 4));
+    // Two regimes (profiles/r01_variants v17-v28):
+    //  * throughput -- LDS holds >= 64 streams per CU and the batch fills them:
+    //    16 streams per wave (the literal batching keeps them converged), as
+    //    many waves as LDS allows (64K x 4 KiB: 16 lanes x 8 waves per CU);
+    //  * latency -- few streams per CU (small batches, or wide lc+lp tables):
+    //    one stream per wave, 16 waves per CU (config 2: 5.8 GB/s vs 2.5 GB/s
+    //    with 4 lanes x 4 waves).
+    // Workgroups per CU stay a power of two so the four SIMDs carry equal
+    // loads (6, 10 or 12 ran 10-30 % slower).
+    auto pow2floor = [](uint32_t v) {
+      while (v & (v - 1)) v &= v - 1;
+      return v;
+    };
+    const uint64_t per_cu_batch = (plan->n_lds + kPlanCUs - 1) / kPlanCUs;
+    uint32_t lanes = 1, groups = 16;
+    if (per_cu >= 64 && per_cu_batch >= 64) {
+      lanes = std::min<uint32_t>(16, pow2floor(per_cu / 8));
+      groups = pow2floor(std::min<uint32_t>(per_cu / lanes, 16));
+    } else {
+      groups = pow2floor(std::min<uint32_t>(per_cu, 16));
+    }
     const int over = env_int("LZGPU_LANES", 0);
-    if (over > 0 && over <= 64 && uint32_t(over) * stride * 2 <= lds_per_cu) lanes = uint32_t(over);
-    // small batches: spread the streams over every CU before stacking lanes
-    const uint64_t spread = (plan->n_lds + uint64_t(kPlanCUs) * 4 - 1) / (uint64_t(kPlanCUs) * 4);
-    if (!over && spread < lanes) lanes = std::max<uint32_t>(1, uint32_t(spread));
-    uint32_t groups = std::min<uint32_t>(per_cu / lanes, occ_over ? 4 * occ : 16u);
-    while (groups & (groups - 1)) groups &= groups - 1;  // 4, 8 or 16 (12 measured slow)
+    if (over > 0 && over <= 64 && uint32_t(over) * stride * 2 <= lds_per_cu) {
+      lanes = uint32_t(over);
+      groups = pow2floor(std::min<uint32_t>(per_cu / lanes, 16));
+    }
+    if (occ_over) groups = std::min<uint32_t>(groups, 4 * occ);
     const int g_over = env_int("LZGPU_GROUPS", 0);
     if (g_over > 0 && uint32_t(g_over) * lanes <= per_cu) groups = uint32_t(g_over);
     plan->lanes_per_group = lanes;
