@@ -264,6 +264,44 @@ SRes LzmaGpu_DecodeBatchHost(const LzmaGpuStreamDesc *descs, size_t n, const Byt
 size_t Lzma2Gpu_SplitBlocks(const Byte *src, size_t src_len, uint64_t *src_off,
                             uint64_t *block_src_len, uint64_t *unpack, size_t max_blocks);
 
+/* ---------------------------------------------------------------- streaming sessions */
+
+/* A device-resident decoder: the CLzmaDec state (LzmaDec.h:50-69) plus one
+ * call's arguments and results.  Many concurrent zlib-like streams (the fork's
+ * SzDecodeLzmaToFileWithBuf pattern, 7zDec.c:567-648) advance by one batched
+ * launch per round of calls; the state stays in device memory between calls.
+ * All pointers are device memory. */
+typedef struct LzmaGpuSession {
+  uint32_t lc, lp, pb, dict_size;          /* CLzmaProps */
+  uint16_t *probs;                         /* LzmaGpu_SessionProbsBytes() bytes */
+  Byte *dic;                               /* dictionary (a ring for DecodeToBuf) */
+  const Byte *in;                          /* this call: input */
+  uint64_t dic_buf_size, dic_pos, dic_limit, in_len, in_used;
+  uint32_t range, code, processed_pos, check_dic_size, state;
+  uint32_t reps[4];
+  uint32_t remain_len, need_flush, need_init_state, temp_buf_size;
+  int32_t finish_mode, res, status;        /* this call: finish mode; results */
+  int32_t mode;                            /* 0: DecodeToDic(dic_limit), 1: DecodeToBuf */
+  Byte temp_buf[LZMA_REQUIRED_INPUT_MAX];
+  Byte _pad[4];
+  Byte *out;                               /* DecodeToBuf: destination */
+  uint64_t out_len;                        /* DecodeToBuf: in = room, out = bytes written */
+} LzmaGpuSession;
+
+/* Device bytes a session's probability table needs for these props (0 on bad props). */
+size_t LzmaGpu_SessionProbsBytes(const Byte *props, unsigned propsSize);
+/* Host-side LzmaDec_Allocate + LzmaDec_Init on a session struct (LzmaDec.c:950-970,
+ * 685-705): parses props, binds the caller's device probs / dictionary
+ * (dic_buf_size >= 1; LzmaDec_Allocate uses the props' dictionary size). */
+SRes LzmaGpu_SessionInit(LzmaGpuSession *s, const Byte *props, unsigned propsSize,
+                         uint16_t *d_probs, Byte *d_dic, size_t dic_buf_size);
+/* One call per session, all in one launch: for mode 0 exactly
+ * LzmaDec_DecodeToDic(s, dic_limit, in, &in_len -> in_used, finish_mode, &status),
+ * for mode 1 exactly LzmaDec_DecodeToBuf(s, out, &out_len, in, &in_len -> in_used,
+ * finish_mode, &status); res / status / in_used / out_len and the decoder state are
+ * written back into each d_sessions[i].  Asynchronous on `stream`. */
+SRes LzmaGpu_SessionDecodeBatch(LzmaGpuSession *d_sessions, size_t n, void *stream);
+
 /* ---------------------------------------------------------------- CRC-32 */
 
 /* Drop-ins for 7zCrc.h (poly 0xEDB88320, 7zCrc.c:7):

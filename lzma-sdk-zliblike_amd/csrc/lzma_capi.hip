@@ -138,22 +138,23 @@ SRes gpu_decode_to_dic(CLzmaDec* p, SizeT dicLimit, const Byte* src, SizeT* srcL
   q.probs = static_cast<uint16_t*>(d_probs);
   q.dic = static_cast<uint8_t*>(d_dic);
   q.in = static_cast<const uint8_t*>(d_src);
-  q.cap = p->dicBufSize;
-  q.pos = p->dicPos;
+  q.dic_buf_size = p->dicBufSize;
+  q.dic_pos = p->dicPos;
   q.dic_limit = dicLimit;
   q.in_len = in_size;
   q.range = p->range;
   q.code = p->code;
-  q.total = p->processedPos;
-  q.full = p->checkDicSize;
-  q.st = p->state;
-  for (int i = 0; i < 4; ++i) q.rep[i] = p->reps[i];
-  q.pending = p->remainLen;
-  q.need_rc_init = p->needFlush ? 1 : 0;
-  q.need_state_init = p->needInitState ? 1 : 0;
-  q.tmp_n = p->tempBufSize;
-  memcpy(q.tmp, p->tempBuf, LZMA_REQUIRED_INPUT_MAX);
+  q.processed_pos = p->processedPos;
+  q.check_dic_size = p->checkDicSize;
+  q.state = p->state;
+  for (int i = 0; i < 4; ++i) q.reps[i] = p->reps[i];
+  q.remain_len = p->remainLen;
+  q.need_flush = p->needFlush ? 1 : 0;
+  q.need_init_state = p->needInitState ? 1 : 0;
+  q.temp_buf_size = p->tempBufSize;
+  memcpy(q.temp_buf, p->tempBuf, LZMA_REQUIRED_INPUT_MAX);
   q.finish_mode = finishMode;
+  q.mode = 0;
   const SizeT pos0 = p->dicPos;
 
   if (!hip_ok(hipMemcpy(d_sess, &q, sizeof q, hipMemcpyHostToDevice), "upload session"))
@@ -168,24 +169,24 @@ SRes gpu_decode_to_dic(CLzmaDec* p, SizeT dicLimit, const Byte* src, SizeT* srcL
       !hip_ok(hipMemcpy(p->probs, d_probs, size_t(nprobs) * 2, hipMemcpyDeviceToHost),
               "download probs"))
     return SZ_ERROR_FAIL;
-  if (q.pos > pos0 &&
-      !hip_ok(hipMemcpy(p->dic + pos0, static_cast<uint8_t*>(d_dic) + pos0, q.pos - pos0,
+  if (q.dic_pos > pos0 &&
+      !hip_ok(hipMemcpy(p->dic + pos0, static_cast<uint8_t*>(d_dic) + pos0, q.dic_pos - pos0,
                         hipMemcpyDeviceToHost),
               "download dic"))
     return SZ_ERROR_FAIL;
 
-  p->dicPos = q.pos;
+  p->dicPos = q.dic_pos;
   p->range = q.range;
   p->code = q.code;
-  p->processedPos = q.total;
-  p->checkDicSize = q.full;
-  p->state = q.st;
-  for (int i = 0; i < 4; ++i) p->reps[i] = q.rep[i];
-  p->remainLen = q.pending;
-  p->needFlush = int(q.need_rc_init);
-  p->needInitState = int(q.need_state_init);
-  p->tempBufSize = q.tmp_n;
-  memcpy(p->tempBuf, q.tmp, LZMA_REQUIRED_INPUT_MAX);
+  p->processedPos = q.processed_pos;
+  p->checkDicSize = q.check_dic_size;
+  p->state = q.state;
+  for (int i = 0; i < 4; ++i) p->reps[i] = q.reps[i];
+  p->remainLen = q.remain_len;
+  p->needFlush = int(q.need_flush);
+  p->needInitState = int(q.need_init_state);
+  p->tempBufSize = q.temp_buf_size;
+  memcpy(p->tempBuf, q.temp_buf, LZMA_REQUIRED_INPUT_MAX);
   p->buf = src + q.in_used;
   *srcLen = q.in_used;
   *status = ELzmaStatus(q.status);
@@ -917,6 +918,52 @@ size_t Lzma2Gpu_SplitBlocks(const Byte* src, size_t src_len, uint64_t* src_off,
   if (pos > src_len) return size_t(-1);
   close_block(src_len);  // no EOS byte: the last block runs to the end
   return nb;
+}
+
+// ------------------------------------------------------------------ streaming sessions
+
+static_assert(sizeof(LzmaGpuSession) == 192, "LzmaGpuSession layout");
+
+size_t LzmaGpu_SessionProbsBytes(const Byte* props, unsigned propsSize) {
+  CLzmaProps pr;
+  if (LzmaProps_Decode(&pr, props, propsSize) != SZ_OK) return 0;
+  return size_t(lzgpu::table_cells(pr.lc, pr.lp, pr.pb)) * 2;
+}
+
+SRes LzmaGpu_SessionInit(LzmaGpuSession* s, const Byte* props, unsigned propsSize,
+                         uint16_t* d_probs, Byte* d_dic, size_t dic_buf_size) {
+  if (!s) return SZ_ERROR_PARAM;
+  CLzmaProps pr;
+  const SRes r = LzmaProps_Decode(&pr, props, propsSize);
+  if (r != SZ_OK) return r;
+  if (!d_probs || !d_dic || dic_buf_size == 0) return SZ_ERROR_PARAM;
+  memset(s, 0, sizeof *s);
+  s->lc = pr.lc;
+  s->lp = pr.lp;
+  s->pb = pr.pb;
+  s->dict_size = pr.dicSize;
+  s->probs = d_probs;
+  s->dic = d_dic;
+  s->dic_buf_size = dic_buf_size;
+  // LzmaDec_Init (LzmaDec.c:701-705): dicPos = 0, InitDicAndState(True, True)
+  s->dic_pos = 0;
+  s->need_flush = 1;
+  s->remain_len = 0;
+  s->temp_buf_size = 0;
+  s->processed_pos = 0;
+  s->check_dic_size = 0;
+  s->need_init_state = 1;
+  return SZ_OK;
+}
+
+SRes LzmaGpu_SessionDecodeBatch(LzmaGpuSession* d_sessions, size_t n, void* stream) {
+  if (!ensure_device()) return SZ_ERROR_FAIL;
+  if (n > 0xFFFFFFFFull) return SZ_ERROR_PARAM;
+  if (lzgpu_launch_session(d_sessions, uint32_t(n), static_cast<hipStream_t>(stream)) != 0) {
+    set_error("session kernel launch failed");
+    return SZ_ERROR_FAIL;
+  }
+  return SZ_OK;
 }
 
 // ------------------------------------------------------------------ CRC-32

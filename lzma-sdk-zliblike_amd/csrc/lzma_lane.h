@@ -12,21 +12,9 @@
 #include "lzma2_device.h"
 #include "lzma_device.h"
 
-// Device-resident decoder state for one DecodeToDic call (the CLzmaDec
-// fields of LzmaDec.h:50-69 plus the call's arguments and results).
-struct LzgpuSession {
-  uint32_t lc, lp, pb, dict_size;
-  uint16_t* probs;
-  uint8_t* dic;
-  const uint8_t* in;
-  uint64_t cap, pos, dic_limit, in_len, in_used;
-  uint32_t range, code, total, full, st;
-  uint32_t rep[4];
-  uint32_t pending, need_rc_init, need_state_init, tmp_n;
-  int32_t finish_mode, res, status, _pad;
-  uint8_t tmp[20];
-  uint8_t _pad2[4];
-};
+// Device-resident decoder state for one DecodeToDic / DecodeToBuf call: the
+// public LzmaGpuSession of include/lzma_gpu.h.
+typedef LzmaGpuSession LzgpuSession;
 
 namespace lzgpu {
 
@@ -166,9 +154,11 @@ __device__ __forceinline__ LzmaGpuResult lane_decode_lds(const LzmaGpuStreamDesc
   return r;
 }
 
-// One LzmaDec_DecodeToDic call on a device-resident decoder (compact layout,
-// all sections in q.probs, for the current lc/lp/pb).
-__device__ __forceinline__ void lane_session(LzgpuSession& q) {
+// One LzmaDec_DecodeToDic call (LzmaDec.c:719-838) on a device-resident
+// decoder (compact layout, all sections in q.probs, for the current lc/lp/pb).
+__device__ __forceinline__ int session_to_dic(LzgpuSession& q, uint64_t dic_limit,
+                                              const gbyte* in, uint64_t& in_len, int fin,
+                                              int& status) {
   LzStateT<gu16*> s;
   s.lc = q.lc;
   s.lp = q.lp;
@@ -177,43 +167,86 @@ __device__ __forceinline__ void lane_session(LzgpuSession& q) {
   s.gl = (gu16*)q.probs;
   s.lo = s.gl;
   s.dic = (gbyte*)q.dic;
-  s.cap = q.cap;
-  s.pos = q.pos;
+  s.cap = q.dic_buf_size;
+  s.pos = q.dic_pos;
   s.range = q.range;
   s.code = q.code;
-  s.total = q.total;
-  s.full = q.full;
-  s.st = q.st;
-  s.rep0 = q.rep[0];
-  s.rep1 = q.rep[1];
-  s.rep2 = q.rep[2];
-  s.rep3 = q.rep[3];
-  s.pending = q.pending;
-  s.need_rc_init = q.need_rc_init;
-  s.need_state_init = q.need_state_init;
-  s.tmp_n = q.tmp_n;
-  for (int i = 0; i < int(kLookahead); ++i) s.tmp[i] = q.tmp[i];
-  uint64_t sl = q.in_len;
-  int status = kStNone;
-  int res = lz_decode_to_dic<true, 0u>(s, q.dic_limit, (const gbyte*)q.in, sl, q.finish_mode, status);
-  q.pos = s.pos;
+  s.total = q.processed_pos;
+  s.full = q.check_dic_size;
+  s.st = q.state;
+  s.rep0 = q.reps[0];
+  s.rep1 = q.reps[1];
+  s.rep2 = q.reps[2];
+  s.rep3 = q.reps[3];
+  s.pending = q.remain_len;
+  s.need_rc_init = q.need_flush;
+  s.need_state_init = q.need_init_state;
+  s.tmp_n = q.temp_buf_size;
+  for (int i = 0; i < int(kLookahead); ++i) s.tmp[i] = q.temp_buf[i];
+  const int res = lz_decode_to_dic<true, 0u>(s, dic_limit, in, in_len, fin, status);
+  q.dic_pos = s.pos;
   q.range = s.range;
   q.code = s.code;
-  q.total = s.total;
-  q.full = s.full;
-  q.st = s.st;
-  q.rep[0] = s.rep0;
-  q.rep[1] = s.rep1;
-  q.rep[2] = s.rep2;
-  q.rep[3] = s.rep3;
-  q.pending = s.pending;
-  q.need_rc_init = s.need_rc_init;
-  q.need_state_init = s.need_state_init;
-  q.tmp_n = s.tmp_n;
-  for (int i = 0; i < int(kLookahead); ++i) q.tmp[i] = s.tmp[i];
+  q.processed_pos = s.total;
+  q.check_dic_size = s.full;
+  q.state = s.st;
+  q.reps[0] = s.rep0;
+  q.reps[1] = s.rep1;
+  q.reps[2] = s.rep2;
+  q.reps[3] = s.rep3;
+  q.remain_len = s.pending;
+  q.need_flush = s.need_rc_init;
+  q.need_init_state = s.need_state_init;
+  q.temp_buf_size = s.tmp_n;
+  for (int i = 0; i < int(kLookahead); ++i) q.temp_buf[i] = s.tmp[i];
+  return res;
+}
+
+// One call on a session: mode 0 = LzmaDec_DecodeToDic(dic_limit), mode 1 =
+// LzmaDec_DecodeToBuf (LzmaDec.c:840-878: the dictionary is a ring of
+// dic_buf_size bytes; each pass decodes up to the ring end or the caller's
+// remaining room, copies the new bytes to `out`, and stops on an error, on a
+// pass that produced nothing, or when `out` is full).
+__device__ __forceinline__ void lane_session(LzgpuSession& q) {
+  int status = kStNone;
+  if (q.mode != 1) {
+    uint64_t sl = q.in_len;
+    q.res = session_to_dic(q, q.dic_limit, (const gbyte*)q.in, sl, q.finish_mode, status);
+    q.status = status;
+    q.in_used = sl;
+    return;
+  }
+  uint64_t out_left = q.out_len, in_left = q.in_len, in_done = 0, out_done = 0;
+  const gbyte* in = (const gbyte*)q.in;
+  gbyte* out = (gbyte*)q.out;
+  int res = kOk;
+  for (;;) {
+    if (q.dic_pos == q.dic_buf_size) q.dic_pos = 0;
+    const uint64_t start = q.dic_pos;
+    uint64_t lim;
+    int fin;
+    if (out_left > q.dic_buf_size - start) {
+      lim = q.dic_buf_size;
+      fin = kFinAny;
+    } else {
+      lim = start + out_left;
+      fin = q.finish_mode;
+    }
+    uint64_t in_cur = in_left;
+    res = session_to_dic(q, lim, in + in_done, in_cur, fin, status);
+    in_done += in_cur;
+    in_left -= in_cur;
+    const uint64_t produced = q.dic_pos - start;
+    const gbyte* from = (const gbyte*)q.dic + start;
+    for (uint64_t i = 0; i < produced; ++i) out[out_done + i] = from[i];
+    out_done += produced;
+    out_left -= produced;
+    if (res != kOk || produced == 0 || out_left == 0) break;
+  }
   q.res = res;
   q.status = status;
-  q.in_used = sl;
+  q.in_used = in_done;
+  q.out_len = out_done;
 }
 
 }  // namespace lzgpu

@@ -80,7 +80,26 @@ class Plan(ctypes.Structure):
                 ("persistent", ctypes.c_uint32), ("reserved", ctypes.c_uint32 * 5)]
 
 
+class Session(ctypes.Structure):
+    """LzmaGpuSession: a device-resident decoder (include/lzma_gpu.h)."""
+    _fields_ = [("lc", ctypes.c_uint32), ("lp", ctypes.c_uint32), ("pb", ctypes.c_uint32),
+                ("dict_size", ctypes.c_uint32), ("probs", ctypes.c_void_p),
+                ("dic", ctypes.c_void_p), ("in_", ctypes.c_void_p),
+                ("dic_buf_size", ctypes.c_uint64), ("dic_pos", ctypes.c_uint64),
+                ("dic_limit", ctypes.c_uint64), ("in_len", ctypes.c_uint64),
+                ("in_used", ctypes.c_uint64), ("range", ctypes.c_uint32),
+                ("code", ctypes.c_uint32), ("processed_pos", ctypes.c_uint32),
+                ("check_dic_size", ctypes.c_uint32), ("state", ctypes.c_uint32),
+                ("reps", ctypes.c_uint32 * 4), ("remain_len", ctypes.c_uint32),
+                ("need_flush", ctypes.c_uint32), ("need_init_state", ctypes.c_uint32),
+                ("temp_buf_size", ctypes.c_uint32), ("finish_mode", ctypes.c_int32),
+                ("res", ctypes.c_int32), ("status", ctypes.c_int32), ("mode", ctypes.c_int32),
+                ("temp_buf", ctypes.c_ubyte * 20), ("_pad", ctypes.c_ubyte * 4),
+                ("out", ctypes.c_void_p), ("out_len", ctypes.c_uint64)]
+
+
 assert ctypes.sizeof(StreamDesc) == 48 and ctypes.sizeof(Result) == 24
+assert ctypes.sizeof(Session) == 192
 assert ctypes.sizeof(CLzmaDec) == 136
 
 _P = ctypes.c_void_p
@@ -108,6 +127,9 @@ _sig = {
     "LzmaGpu_DecodeBatchEx": (ctypes.c_int, [ctypes.POINTER(Plan), _P, _P, _P, _P, _P, _P, _P]),
     "LzmaGpu_DecodeBatchHost": (ctypes.c_int, [ctypes.POINTER(StreamDesc), ctypes.c_size_t, _P, ctypes.c_size_t, _P, ctypes.c_size_t, ctypes.POINTER(Result)]),
     "Lzma2Gpu_SplitBlocks": (ctypes.c_size_t, [_P, ctypes.c_size_t, _P, _P, _P, ctypes.c_size_t]),
+    "LzmaGpu_SessionProbsBytes": (ctypes.c_size_t, [ctypes.c_char_p, ctypes.c_uint]),
+    "LzmaGpu_SessionInit": (ctypes.c_int, [ctypes.POINTER(Session), ctypes.c_char_p, ctypes.c_uint, _P, _P, ctypes.c_size_t]),
+    "LzmaGpu_SessionDecodeBatch": (ctypes.c_int, [_P, ctypes.c_size_t, _P]),
     "CrcGenerateTable": (None, []),
     "CrcUpdate": (ctypes.c_uint32, [ctypes.c_uint32, _P, ctypes.c_size_t]),
     "CrcCalc": (ctypes.c_uint32, [_P, ctypes.c_size_t]),
@@ -356,3 +378,22 @@ def crc32_batch_decoded(d_descs, d_results, n, d_dst, d_base, d_range, n_chunks,
     """LzmaGpu_Crc32Batch over raw device pointers (ints)."""
     return _lib.LzmaGpu_Crc32Batch(d_descs, d_results, n, d_dst, d_base, d_range, n_chunks,
                                    d_chunk_crc, d_crc, stream or None)
+
+
+# ---------------------------------------------------------------- streaming sessions
+
+def session_probs_bytes(props):
+    return _lib.LzmaGpu_SessionProbsBytes(bytes(props), len(props))
+
+
+def session_init(props, d_probs, d_dic, dic_buf_size):
+    """Host-side LzmaDec_Allocate + LzmaDec_Init on a fresh Session (device pointers in)."""
+    s = Session()
+    r = _lib.LzmaGpu_SessionInit(ctypes.byref(s), bytes(props), len(props), d_probs, d_dic,
+                                 dic_buf_size)
+    return r, s
+
+
+def session_decode_batch(d_sessions, n, stream=0):
+    """LzmaGpu_SessionDecodeBatch over a device array of n Sessions."""
+    return _lib.LzmaGpu_SessionDecodeBatch(d_sessions, n, stream or None)

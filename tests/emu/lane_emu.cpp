@@ -34,10 +34,13 @@ void emu_decode_batch_lds(const LzmaGpuStreamDesc* descs, size_t n, const uint8_
 }
 
 // zlib-like DecodeToBuf loop driven through lane_session (the session
-// kernel's body), same contract as orc_lzma_stream_decode.
-int emu_stream_decode(const uint8_t* props, const uint8_t* src, size_t src_total, uint8_t* out,
-                      size_t out_total, size_t in_chunk, size_t out_chunk, int finish_mode,
-                      long long* trace, int max_calls, size_t* out_len, size_t* in_used) {
+// kernel's body), same contract as orc_lzma_stream_decode.  buf_mode 1: each
+// DecodeToBuf call is one session call in mode 1 (the device ring loop);
+// buf_mode 0: the ring loop runs here over mode-0 (DecodeToDic) calls.
+static int stream_decode(const uint8_t* props, const uint8_t* src, size_t src_total, uint8_t* out,
+                         size_t out_total, size_t in_chunk, size_t out_chunk, int finish_mode,
+                         long long* trace, int max_calls, size_t* out_len, size_t* in_used,
+                         int buf_mode) {
   uint32_t lc, lp, pb, dict;
   int r = lz_props_parse(props, 5, lc, lp, pb, dict);
   if (r != kOk) { *out_len = 0; *in_used = 0; return -r; }
@@ -46,34 +49,45 @@ int emu_stream_decode(const uint8_t* props, const uint8_t* src, size_t src_total
   q.lc = lc; q.lp = lp; q.pb = pb; q.dict_size = dict;
   q.probs = (uint16_t*)malloc(size_t(num_probs(lc, lp)) * 2);
   q.dic = (uint8_t*)malloc(dict);
-  q.cap = dict;
-  q.pos = 0;
-  q.need_rc_init = 1; q.need_state_init = 1; q.pending = 0; q.tmp_n = 0;
+  q.dic_buf_size = dict;
+  q.dic_pos = 0;
+  q.need_flush = 1; q.need_init_state = 1; q.remain_len = 0; q.temp_buf_size = 0;
   size_t in_pos = 0, out_pos = 0;
   int calls = 0;
   while (calls < max_calls) {
     size_t sl = src_total - in_pos, dl = out_total - out_pos;
     if (sl > in_chunk) sl = in_chunk;
     if (dl > out_chunk) dl = out_chunk;
-    // ---- LzmaDec_DecodeToBuf (LzmaDec.c:840-878) over lane_session
-    size_t out_left = dl, in_left = sl, got_in = 0, got_out = 0;
-    const uint8_t* s = src + in_pos;
-    uint8_t* d = out + out_pos;
+    size_t got_in = 0, got_out = 0;
     int res = 0, st = -1;
-    for (;;) {
-      if (q.pos == q.cap) q.pos = 0;
-      uint64_t start = q.pos, lim;
-      int fin;
-      if (out_left > q.cap - start) { lim = q.cap; fin = 0; } else { lim = start + out_left; fin = finish_mode; }
-      q.in = s; q.in_len = in_left; q.dic_limit = lim; q.finish_mode = fin;
+    if (buf_mode) {
+      q.mode = 1;
+      q.in = src + in_pos; q.in_len = sl; q.out = out + out_pos; q.out_len = dl;
+      q.finish_mode = finish_mode;
       lane_session(q);
-      res = q.res; st = q.status;
-      s += q.in_used; in_left -= q.in_used; got_in += q.in_used;
-      size_t produced = q.pos - start;
-      memcpy(d, q.dic + start, produced);
-      d += produced; out_left -= produced; got_out += produced;
-      if (res != 0) break;
-      if (produced == 0 || out_left == 0) break;
+      res = q.res; st = q.status; got_in = q.in_used; got_out = q.out_len;
+    } else {
+      // ---- LzmaDec_DecodeToBuf (LzmaDec.c:840-878) over mode-0 calls
+      size_t out_left = dl, in_left = sl;
+      const uint8_t* s = src + in_pos;
+      uint8_t* d = out + out_pos;
+      q.mode = 0;
+      for (;;) {
+        if (q.dic_pos == q.dic_buf_size) q.dic_pos = 0;
+        uint64_t start = q.dic_pos, lim;
+        int fin;
+        if (out_left > q.dic_buf_size - start) { lim = q.dic_buf_size; fin = 0; }
+        else { lim = start + out_left; fin = finish_mode; }
+        q.in = s; q.in_len = in_left; q.dic_limit = lim; q.finish_mode = fin;
+        lane_session(q);
+        res = q.res; st = q.status;
+        s += q.in_used; in_left -= q.in_used; got_in += q.in_used;
+        size_t produced = q.dic_pos - start;
+        memcpy(d, q.dic + start, produced);
+        d += produced; out_left -= produced; got_out += produced;
+        if (res != 0) break;
+        if (produced == 0 || out_left == 0) break;
+      }
     }
     trace[4 * calls + 0] = res;
     trace[4 * calls + 1] = st;
@@ -89,6 +103,21 @@ int emu_stream_decode(const uint8_t* props, const uint8_t* src, size_t src_total
   *out_len = out_pos;
   *in_used = in_pos;
   return calls;
+}
+
+int emu_stream_decode(const uint8_t* props, const uint8_t* src, size_t src_total, uint8_t* out,
+                      size_t out_total, size_t in_chunk, size_t out_chunk, int finish_mode,
+                      long long* trace, int max_calls, size_t* out_len, size_t* in_used) {
+  return stream_decode(props, src, src_total, out, out_total, in_chunk, out_chunk, finish_mode,
+                       trace, max_calls, out_len, in_used, 1);
+}
+
+int emu_stream_decode_dic(const uint8_t* props, const uint8_t* src, size_t src_total,
+                          uint8_t* out, size_t out_total, size_t in_chunk, size_t out_chunk,
+                          int finish_mode, long long* trace, int max_calls, size_t* out_len,
+                          size_t* in_used) {
+  return stream_decode(props, src, src_total, out, out_total, in_chunk, out_chunk, finish_mode,
+                       trace, max_calls, out_len, in_used, 0);
 }
 
 // CRC-32 kernels' per-lane code (crc_chunk per chunk slot, then crc_fold),

@@ -45,12 +45,12 @@ def emu(request):
     lib.emu_decode_batch.restype = None
     lib.emu_decode_batch.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_char_p,
                                      ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
-    f = lib.emu_stream_decode
-    f.restype = ctypes.c_int
-    f.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p,
-                  ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int,
-                  ctypes.POINTER(ctypes.c_longlong), ctypes.c_int, native.size_t_p,
-                  native.size_t_p]
+    for f in (lib.emu_stream_decode, lib.emu_stream_decode_dic):
+        f.restype = ctypes.c_int
+        f.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p,
+                      ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int,
+                      ctypes.POINTER(ctypes.c_longlong), ctypes.c_int, native.size_t_p,
+                      native.size_t_p]
     return lib
 
 
@@ -130,14 +130,18 @@ def test_emu_golden_lzma2_batch(emu, lds):
         assert G.sha(dst[:res[0].dest_len]) == e["sha256"]
 
 
-def test_emu_golden_streaming(emu):
+@pytest.mark.parametrize("device_ring", [True, False])
+def test_emu_golden_streaming(emu, device_ring):
+    """DecodeToBuf traces: the session's device ring loop (mode 1) and the
+    host ring loop over DecodeToDic calls (mode 0)."""
     d = G.load()
+    fn = emu.emu_stream_decode if device_ring else emu.emu_stream_decode_dic
     for i, c in G.cases("stream"):
         s = G.case_input(d, c)
         out = ctypes.create_string_buffer(max(c["out_total"], 1))
         trace = (ctypes.c_longlong * 400000)()
         ol, iu = ctypes.c_size_t(0), ctypes.c_size_t(0)
-        calls = emu.emu_stream_decode(bytes.fromhex(c["props"]), s, len(s), out, c["out_total"],
+        calls = fn(bytes.fromhex(c["props"]), s, len(s), out, c["out_total"],
                                       c["in_chunk"], c["out_chunk"], c["finish"], trace, 100000,
                                       ctypes.byref(ol), ctypes.byref(iu))
         tr = [tuple(trace[4 * k:4 * k + 4]) for k in range(calls)]
