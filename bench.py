@@ -1,6 +1,6 @@
 """bench.py -- batch LZMA decode throughput on MI355X (BASELINE.json metric).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg3|cfg2|cfg4]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg3|cfg2|cfg4|cfg5]
 
 One "step" = one launch of the batch decode kernel over the whole per-GPU
 batch (inputs already resident in HBM, outputs written to HBM).  Default
@@ -356,6 +356,206 @@ def run_cfg4(args):
         sys.exit(3)
 
 
+# ---------------------------------------------------------------- config 5
+
+CFG5_STREAMS = 32768
+CFG5_DICTS = (4096, 16384, 65536, 262144, 1 << 20)
+
+
+def _cfg5_stream(i):
+    """Stream i of config 5: props, dict, length and finish mode
+    drawn from a generator seeded by (5, i); liblzma-encoded synthetic text."""
+    import random
+    import native
+    rng = random.Random(5 * 1000003 + i)
+    while True:
+        lc, lp = rng.randrange(5), rng.randrange(3)
+        if lc + lp <= 4:
+            break
+    pb = rng.randrange(5)
+    dsz = rng.choice(CFG5_DICTS)
+    n = int(round(1024 * 2 ** rng.uniform(0, 8)))  # log-uniform 1 KiB .. 256 KiB
+    fin = rng.randrange(2)  # half stop at the end marker (END), half at destLen (ANY)
+    data = native.gen("text", 70000 + i, n)
+    f = [{"id": lzma.FILTER_LZMA1, "dict_size": dsz, "lc": lc, "lp": lp, "pb": pb, "preset": 6}]
+    c = lzma.compress(data, format=lzma.FORMAT_RAW, filters=f)
+    props = bytes([(pb * 5 + lp) * 9 + lc]) + dsz.to_bytes(4, "little")
+    return i, c, props, n, fin, zlib_crc(data)
+
+
+def build_cfg5(workers, first, count):
+    tmp = os.environ.get("TMPDIR", "/tmp")
+    path = os.path.join(tmp, f"lzgpu_cfg5_{first}_{count}_v1.npz")
+    if os.path.exists(path):
+        z = np.load(path)
+        return (z["comp"], z["lens"], z["props"], z["n"], z["fin"], z["crc"])
+    t0 = time.time()
+    out = [None] * count
+    with mp.get_context("fork").Pool(workers) as pool:
+        for i, c, props, n, fin, crc in pool.imap_unordered(
+                _cfg5_stream, range(first, first + count), chunksize=64):
+            out[i - first] = (c, props, n, fin, crc)
+    comp = np.frombuffer(b"".join(o[0] for o in out), dtype=np.uint8)
+    lens = np.array([len(o[0]) for o in out], dtype=np.uint64)
+    props = np.frombuffer(b"".join(o[1] for o in out), dtype=np.uint8).reshape(count, 5)
+    n = np.array([o[2] for o in out], dtype=np.uint64)
+    fin = np.array([o[3] for o in out], dtype=np.uint8)
+    crc = np.array([o[4] for o in out], dtype=np.uint32)
+    np.savez(path, comp=comp, lens=lens, props=props, n=n, fin=fin, crc=crc)
+    log(f"[cfg5] compressed {count} mixed streams in {time.time() - t0:.1f}s")
+    return comp, lens, props, n, fin, crc
+
+
+def run_cfg5(args):
+    """Config 5: 32,768 streams of mixed lc/lp/pb, dictionaries and lengths per
+    GPU (weak scaling), one batch launch set per step (one LDS launch per
+    table-width class), verified by per-stream results and GPU CRC-32."""
+    import dist_bench as D
+    world, rank, local_rank = D.world_info()
+    cpus = os.cpu_count() or 8
+    workers = max(1, min(16, cpus // max(1, world)))
+    count = args.streams or CFG5_STREAMS
+    comp, lens, props, nout, fin, crcs = build_cfg5(workers, rank * count, count)
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    import lzmagpu as L
+    descs = (L.StreamDesc * count)()
+    arr = np.frombuffer(descs, dtype=np.uint8).reshape(count, 48)
+    u64 = arr[:, :40].view(np.uint64)
+    src_off = np.zeros(count, dtype=np.uint64)
+    src_off[1:] = np.cumsum(lens)[:-1]
+    dst_off = np.zeros(count, dtype=np.uint64)
+    dst_off[1:] = np.cumsum(nout)[:-1]
+    u64[:, 0], u64[:, 1], u64[:, 2], u64[:, 3] = src_off, lens, dst_off, nout
+    arr[:, 40:45] = props
+    arr[:, 45] = 5
+    arr[:, 46] = fin
+    arr[:, 47] = L.KIND_LZMA
+    plan, order = L.plan_ex(descs)
+    total_out = int(nout.sum())
+    d_src = torch.from_numpy(np.concatenate([comp, np.zeros(16, np.uint8)])).to(dev)
+    d_dst = torch.empty(total_out + 16, dtype=torch.uint8, device=dev)
+    d_ws = torch.empty(max(int(plan.workspace_bytes), 16), dtype=torch.uint8, device=dev)
+    d_desc = torch.frombuffer(bytearray(bytes(descs)), dtype=torch.uint8).to(dev)
+    d_order = torch.frombuffer(bytearray(bytes(order)), dtype=torch.uint8).to(dev)
+    d_res = torch.empty(count * 24, dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    sh = stream.cuda_stream
+
+    def step():
+        r = L.decode_batch_device_ex(plan, d_desc.data_ptr(), d_order.data_ptr(), d_src.data_ptr(),
+                                     d_dst.data_ptr(), d_ws.data_ptr(), d_res.data_ptr(), sh)
+        if r != 0:
+            raise RuntimeError("LzmaGpu_DecodeBatchEx failed: " + L.last_error())
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    D.barrier()
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for a, b in evs:
+        a.record(stream)
+        step()
+        b.record(stream)
+    torch.cuda.synchronize()
+    D.barrier()
+    torch.cuda.synchronize()
+    elapsed = D.reduce_max(time.perf_counter() - t0, dev)
+    dec_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    res = np.frombuffer(d_res.cpu().numpy().tobytes(), dtype=np.dtype(
+        [("res", "<i4"), ("status", "<i4"), ("dest_len", "<u8"), ("src_len", "<u8")]))
+    want_status = np.where(fin == 1, 1, 2)
+    ok = bool((res["res"] == 0).all() and (res["status"] == want_status).all() and
+              (res["dest_len"] == nout).all() and
+              (res["src_len"][fin == 1] == lens[fin == 1]).all())
+    base, crange, total = L.crc32_plan_decoded(descs)
+    d_base = torch.frombuffer(bytearray(base), dtype=torch.uint8).to(dev)
+    d_range = torch.frombuffer(bytearray(crange), dtype=torch.uint8).to(dev)
+    d_chunks = torch.empty(max(total, 1) * 4, dtype=torch.uint8, device=dev)
+    d_crc = torch.empty(count * 4, dtype=torch.uint8, device=dev)
+    assert L.crc32_batch_decoded(d_desc.data_ptr(), d_res.data_ptr(), count, d_dst.data_ptr(),
+                                 d_base.data_ptr(), d_range.data_ptr(), total,
+                                 d_chunks.data_ptr(), d_crc.data_ptr(), sh) == 0
+    got = np.frombuffer(d_crc.cpu().numpy().tobytes(), dtype="<u4")
+    ok = D.all_true(ok and bool(np.array_equal(got, crcs)), dev)
+    value = world * total_out * args.steps / elapsed / 1e6
+    alg = int(lens.sum()) + 5 * count + total_out
+    achieved = alg / (dec_ms * 1e-3) / 1e9
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        thr = min(cpus, 16)
+        m = min(count, 2048)
+        orc_n = nout[:m]
+        v, dt, mm, errs = cpu_baseline_mixed(comp, lens, src_off, orc_n, props, fin, thr, m)
+        cpu = {"value": round(v, 2), "unit": "MB/s", "cores": thr, "kind": "port",
+               "sample": f"first {mm} streams of the batch, {thr} threads, {dt:.2f}s",
+               "errors": int(errs)}
+    if rank == 0:
+        cls = [{"streams": int(c.n), "streams_per_workgroup": int(c.lanes_per_group),
+                "lds_bytes_per_stream": int(c.lds_cells_per_lane) * 2,
+                "workgroups_per_cu": int(c.groups_per_cu)}
+               for c in list(plan.classes)[:int(plan.n_classes)]]
+        print(json.dumps({
+            "metric": "decompressed MB/s (whole node), config 5: 32K mixed-props streams",
+            "value": round(value, 2), "unit": "MB/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic text, liblzma-encoded (lc 0-4, lp 0-2, pb 0-4, dict 4K-1M)",
+            "config": {"workload": f"{count} streams, log-uniform 1 KiB-256 KiB, mixed props, "
+                                   "half FINISH_END / half FINISH_ANY",
+                       "decompressed_bytes_per_gpu": total_out,
+                       "compressed_bytes_per_gpu": int(lens.sum()),
+                       "kernel_plan": {"lds_streams": int(plan.n_lds), "classes": cls}},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
+                         "traffic": None, "kernel": "lzgpu_decode_lds_kernel",
+                         "kernel_avg_ms": round(dec_ms, 4), "alg_bytes_per_launch": alg},
+            "cpu_baseline": cpu, "verified": ok}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    if not ok:
+        sys.exit(3)
+
+
+def cpu_baseline_mixed(comp, lens, offs, nout, props, fin, threads, m):
+    """The oracle restatement over the first m streams of a mixed batch."""
+    import native
+    orc = native.oracle()
+    src_off = np.ascontiguousarray(offs[:m], dtype=np.uint64)
+    src_len = np.ascontiguousarray(lens[:m], dtype=np.uint64)
+    dst_cap = np.ascontiguousarray(nout[:m], dtype=np.uint64)
+    dst_off = np.zeros(m, dtype=np.uint64)
+    dst_off[1:] = np.cumsum(dst_cap)[:-1]
+    dst = np.zeros(int(dst_cap.sum()) + 1, dtype=np.uint8)
+    res = np.zeros(m, np.int32)
+    st = np.zeros(m, np.int32)
+    dl = np.zeros(m, np.uint64)
+    sl = np.zeros(m, np.uint64)
+    errs = 0
+    t0 = time.perf_counter()
+    for f in (0, 1):  # the oracle batch helper takes one finish mode per call
+        sel = np.nonzero(fin[:m] == f)[0]
+        if len(sel) == 0:
+            continue
+        # keep every argument array referenced until the call returns
+        so, sn, do, dc = (np.ascontiguousarray(x[sel]) for x in (src_off, src_len, dst_off,
+                                                                 dst_cap))
+        pp = np.ascontiguousarray(props[:m][sel]).reshape(-1)
+        errs += orc.orc_lzma_decode_batch(
+            comp.ctypes.data, so.ctypes.data, sn.ctypes.data, pp.ctypes.data, dst.ctypes.data,
+            do.ctypes.data, dc.ctypes.data, f, res.ctypes.data, st.ctypes.data,
+            dl.ctypes.data, sl.ctypes.data, len(sel), threads)
+    dt = time.perf_counter() - t0
+    return float(dst_cap.sum()) / dt / 1e6, dt, m, errs
+
+
 def cfg4_cpu_baseline(parts, threads):
     """Oracle LZMA2 decode of distinct blocks on a thread pool (ctypes drops the GIL)."""
     import native
@@ -403,13 +603,16 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="cfg3", choices=sorted(CONFIGS) + ["cfg4"])
+    ap.add_argument("--config", default="cfg3", choices=sorted(CONFIGS) + ["cfg4", "cfg5"])
+    ap.add_argument("--streams", type=int, default=0, help="cfg5: streams per GPU (32768)")
     ap.add_argument("--blocks", type=int, default=1024, help="cfg4: LZMA2 blocks per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-crc", action="store_true", help="skip the CRC-32 (8(f) row 1) leg")
     args = ap.parse_args()
     if args.config == "cfg4":
         return run_cfg4(args)
+    if args.config == "cfg5":
+        return run_cfg5(args)
 
     import dist_bench as D
     world, rank, local_rank = D.world_info()

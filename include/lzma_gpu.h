@@ -211,26 +211,40 @@ typedef struct LzmaGpuResult {
 size_t LzmaGpu_PlanBatch(LzmaGpuStreamDesc *descs, size_t n, uint32_t *order);
 
 /* Launch plan for LzmaGpu_DecodeBatchEx (filled by LzmaGpu_PlanBatchEx).
- * The lane order is partitioned: order[0, n_lds) runs on the LDS kernel
- * (per-stream probability tables in LDS, lanes_per_group streams per
- * workgroup, lds_cells_per_lane cells each); order[n_lds, n) runs on the
- * generic kernel (tables in the global workspace: LZMA2 ranges, lc+lp too
- * wide for LDS).  Environment overrides for experiments:
- * LZGPU_KERNEL=global|lds, LZGPU_LANES=<streams per workgroup>,
- * LZGPU_OCC=<4|6|8 waves per SIMD>, LZGPU_PERSIST=0 (one stream per lane).
- * workspace_bytes includes the LDS kernel's 4-byte work counter at
- * queue_offset (zeroed by every DecodeBatchEx launch on its stream). */
-typedef struct LzmaGpuPlan {
-  uint64_t workspace_bytes;
+ * The lane order is partitioned: order[0, n_lds) runs on the LDS kernel in
+ * n_classes launches by table width (class k: classes[k].n consecutive lanes,
+ * per-stream probability tables in LDS, lanes_per_group streams per
+ * workgroup); order[n_lds, n) runs on the generic kernel (tables in the
+ * global workspace: lc + lp too wide for LDS).  Environment overrides for
+ * experiments: LZGPU_KERNEL=global|lds, LZGPU_LANES=<streams per workgroup>,
+ * LZGPU_GROUPS=<workgroups per CU>, LZGPU_OCC=<1|2|4|6|8 waves per SIMD>,
+ * LZGPU_PERSIST=0 (one stream per lane), LZGPU_CLASSES=1 (one LDS launch).
+ * workspace_bytes includes the LDS launches' work counters at queue_offset
+ * (zeroed by every DecodeBatchEx launch on its stream). */
+#define LZMA_GPU_MAX_CLASSES 4
+/* One LDS-kernel launch: `n` consecutive lanes of the order, tables of at most
+ * lds_cells_per_lane cells, lanes_per_group streams per workgroup,
+ * groups_per_cu workgroups per CU, register budget waves_per_simd. */
+typedef struct LzmaGpuLdsClass {
   uint64_t n;
-  uint64_t n_lds;
   uint32_t lanes_per_group;
   uint32_t lds_cells_per_lane;
   uint32_t groups_per_cu;
-  uint32_t waves_per_simd; /* LDS kernel register budget: 4, 6 or 8 waves per SIMD */
-  uint64_t queue_offset;   /* byte offset in the workspace of the LDS kernel's work counter */
-  uint32_t persistent;     /* 1: grid = resident workgroups, lanes pull streams from the queue */
-  uint32_t reserved[5];
+  uint32_t waves_per_simd;
+} LzmaGpuLdsClass;
+
+typedef struct LzmaGpuPlan {
+  uint64_t workspace_bytes;
+  uint64_t n;
+  uint64_t n_lds;           /* lanes on the LDS kernel: sum of classes[k].n */
+  uint32_t lanes_per_group; /* the class with the most streams (summary) */
+  uint32_t lds_cells_per_lane;
+  uint32_t groups_per_cu;
+  uint32_t waves_per_simd;
+  uint64_t queue_offset;    /* class k's work counter at queue_offset + 64 k */
+  uint32_t persistent;      /* 1: grid = resident workgroups, lanes pull streams from the queue */
+  uint32_t n_classes;       /* LDS launches, by table width (mixed lc/lp/pb batches) */
+  LzmaGpuLdsClass classes[LZMA_GPU_MAX_CLASSES];
 } LzmaGpuPlan;
 
 SRes LzmaGpu_PlanBatchEx(LzmaGpuStreamDesc *descs, size_t n, uint32_t *order, LzmaGpuPlan *plan);

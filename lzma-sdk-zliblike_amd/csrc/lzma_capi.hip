@@ -679,6 +679,68 @@ size_t LzmaGpu_PlanBatch(LzmaGpuStreamDesc* descs, size_t n, uint32_t* order) {
 // CUs the planner sizes for (MI355X: 256; LZGPU_CUS overrides)
 static const uint32_t kPlanCUs = uint32_t(env_int("LZGPU_CUS", 256));
 
+// Launch shape of one LDS class: `stride` cells per stream, `count` streams.
+static LzmaGpuLdsClass plan_lds_class(uint32_t stride, uint64_t count) {
+  LzmaGpuLdsClass c;
+  memset(&c, 0, sizeof c);
+  stride = (stride + 3) & ~3u;  // 8-byte aligned per-lane slices
+  const uint32_t lds_per_cu = 160 * 1024;
+  const uint32_t per_cu = std::max<uint32_t>(1, lds_per_cu / (stride * 2));  // streams/CU
+  uint32_t occ = 4;
+  const int occ_over = env_int("LZGPU_OCC", 0);
+  if (occ_over == 1 || occ_over == 2 || occ_over == 4 || occ_over == 6 || occ_over == 8)
+    occ = uint32_t(occ_over);
+  // Two regimes (profiles/r01_variants v17-v28):
+  //  * throughput -- LDS holds >= 64 streams per CU and the batch fills them:
+  //    16 streams per wave (the literal batching keeps them converged), as
+  //    many waves as LDS allows (64K x 4 KiB: 16 lanes x 8 waves per CU);
+  //  * latency -- few streams per CU (small batches, or wide lc+lp tables):
+  //    one stream per wave and 16 waves per CU, more lanes only once there
+  //    are 32+ streams per CU to place (config 2: 1 lane x 16 waves 5.8 GB/s
+  //    vs 4 lanes x 4 waves 2.5 GB/s).
+  // Workgroups per CU stay a power of two so the four SIMDs carry equal
+  // loads (6, 10 or 12 ran 10-30 % slower).
+  auto pow2floor = [](uint32_t v) {
+    while (v & (v - 1)) v &= v - 1;
+    return v;
+  };
+  const uint64_t per_cu_batch = (count + kPlanCUs - 1) / kPlanCUs;
+  uint32_t lanes = 1, groups = 16;
+  if (per_cu >= 64 && per_cu_batch >= 64) {
+    lanes = std::min<uint32_t>(16, pow2floor(per_cu / 8));
+    groups = pow2floor(std::min<uint32_t>(per_cu / lanes, 16));
+  } else {
+    lanes = std::max<uint32_t>(1, pow2floor(uint32_t(std::min<uint64_t>(per_cu, per_cu_batch) / 16)));
+    groups = pow2floor(std::min<uint32_t>(per_cu / lanes, 16));
+  }
+  const int over = env_int("LZGPU_LANES", 0);
+  if (over > 0 && over <= 64 && uint32_t(over) * stride * 2 <= lds_per_cu) {
+    lanes = uint32_t(over);
+    groups = pow2floor(std::min<uint32_t>(per_cu / lanes, 16));
+  }
+  if (occ_over) groups = std::min<uint32_t>(groups, 4 * occ);
+  const int g_over = env_int("LZGPU_GROUPS", 0);
+  if (g_over > 0 && uint32_t(g_over) * lanes <= per_cu) groups = uint32_t(g_over);
+  c.n = count;
+  c.lanes_per_group = lanes;
+  c.lds_cells_per_lane = stride;
+  c.groups_per_cu = std::max<uint32_t>(1, groups);
+  // register budget = the waves per SIMD that are actually resident (one
+  // wave per workgroup): 8 workgroups per CU -> 2 waves/SIMD -> 256 VGPRs,
+  // enough for the decoder state without spills
+  c.waves_per_simd = occ_over ? occ : std::max<uint32_t>(1, (c.groups_per_cu + 3) / 4);
+  return c;
+}
+
+// LDS class of a stream by its table width (cells): narrow tables share a
+// launch with many streams per CU, wide ones (lc + lp >= 3) get their own.
+static int lds_bucket(uint32_t cells) {
+  if (cells <= 768) return 0;
+  if (cells <= 1536) return 1;
+  if (cells <= 3072) return 2;
+  return 3;
+}
+
 SRes LzmaGpu_PlanBatchEx(LzmaGpuStreamDesc* descs, size_t n, uint32_t* order,
                          LzmaGpuPlan* plan) {
   if (!order || !plan) return SZ_ERROR_PARAM;
@@ -691,12 +753,14 @@ SRes LzmaGpu_PlanBatchEx(LzmaGpuStreamDesc* descs, size_t n, uint32_t* order,
   const int force = env_int("LZGPU_KERNEL_GLOBAL", 0);
   const char* kv = getenv("LZGPU_KERNEL");
   const bool global_only = force || (kv && strcmp(kv, "global") == 0);
-  uint32_t stride = 0;
-  std::vector<uint32_t> lds_idx, glob_idx;
+  const bool one_class = env_int("LZGPU_CLASSES", 0) == 1;
+  std::vector<uint32_t> bucket_idx[LZMA_GPU_MAX_CLASSES], glob_idx;
+  uint32_t bucket_stride[LZMA_GPU_MAX_CLASSES] = {0, 0, 0, 0};
   for (size_t i = 0; i < n; ++i) {
     if (!global_only && w[i] != 0 && w[i] <= kMaxLdsCells) {
-      lds_idx.push_back(uint32_t(i));
-      stride = std::max(stride, w[i]);
+      const int b = one_class ? 0 : lds_bucket(w[i]);
+      bucket_idx[b].push_back(uint32_t(i));
+      bucket_stride[b] = std::max(bucket_stride[b], w[i]);
     } else {
       glob_idx.push_back(uint32_t(i));
     }
@@ -711,62 +775,29 @@ SRes LzmaGpu_PlanBatchEx(LzmaGpuStreamDesc* descs, size_t n, uint32_t* order,
     if (wa != wb) return wa > wb;
     return w[a] > w[b];
   };
-  std::stable_sort(lds_idx.begin(), lds_idx.end(), by_len);
-  std::stable_sort(glob_idx.begin(), glob_idx.end(), by_len);
   size_t k = 0;
-  for (uint32_t i : lds_idx) order[k++] = i;
-  for (uint32_t i : glob_idx) order[k++] = i;
-  plan->n_lds = lds_idx.size();
-  if (plan->n_lds) {
-    stride = (stride + 3) & ~3u;  // 8-byte aligned per-lane slices
-    const uint32_t lds_per_cu = 160 * 1024;
-    const uint32_t per_cu = std::max<uint32_t>(1, lds_per_cu / (stride * 2));  // streams/CU
-    uint32_t occ = 4;  // register budget while sizing; re-derived below
-    const int occ_over = env_int("LZGPU_OCC", 0);
-    if (occ_over == 1 || occ_over == 2 || occ_over == 4 || occ_over == 6 || occ_over == 8)
-      occ = uint32_t(occ_over);
-    // Two regimes (profiles/r01_variants v17-v28):
-    //  * throughput -- LDS holds >= 64 streams per CU and the batch fills them:
-    //    16 streams per wave (the literal batching keeps them converged), as
-    //    many waves as LDS allows (64K x 4 KiB: 16 lanes x 8 waves per CU);
-    //  * latency -- few streams per CU (small batches, or wide lc+lp tables):
-    //    one stream per wave, 16 waves per CU (config 2: 5.8 GB/s vs 2.5 GB/s
-    //    with 4 lanes x 4 waves).
-    // Workgroups per CU stay a power of two so the four SIMDs carry equal
-    // loads (6, 10 or 12 ran 10-30 % slower).
-    auto pow2floor = [](uint32_t v) {
-      while (v & (v - 1)) v &= v - 1;
-      return v;
-    };
-    const uint64_t per_cu_batch = (plan->n_lds + kPlanCUs - 1) / kPlanCUs;
-    uint32_t lanes = 1, groups = 16;
-    if (per_cu >= 64 && per_cu_batch >= 64) {
-      lanes = std::min<uint32_t>(16, pow2floor(per_cu / 8));
-      groups = pow2floor(std::min<uint32_t>(per_cu / lanes, 16));
-    } else {
-      groups = pow2floor(std::min<uint32_t>(per_cu, 16));
+  uint64_t best = 0;
+  for (int b = 0; b < LZMA_GPU_MAX_CLASSES; ++b) {
+    if (bucket_idx[b].empty()) continue;
+    std::stable_sort(bucket_idx[b].begin(), bucket_idx[b].end(), by_len);
+    for (uint32_t i : bucket_idx[b]) order[k++] = i;
+    const LzmaGpuLdsClass c = plan_lds_class(bucket_stride[b], bucket_idx[b].size());
+    plan->classes[plan->n_classes++] = c;
+    plan->n_lds += c.n;
+    if (c.n > best) {
+      best = c.n;
+      plan->lanes_per_group = c.lanes_per_group;
+      plan->lds_cells_per_lane = c.lds_cells_per_lane;
+      plan->groups_per_cu = c.groups_per_cu;
+      plan->waves_per_simd = c.waves_per_simd;
     }
-    const int over = env_int("LZGPU_LANES", 0);
-    if (over > 0 && over <= 64 && uint32_t(over) * stride * 2 <= lds_per_cu) {
-      lanes = uint32_t(over);
-      groups = pow2floor(std::min<uint32_t>(per_cu / lanes, 16));
-    }
-    if (occ_over) groups = std::min<uint32_t>(groups, 4 * occ);
-    const int g_over = env_int("LZGPU_GROUPS", 0);
-    if (g_over > 0 && uint32_t(g_over) * lanes <= per_cu) groups = uint32_t(g_over);
-    plan->lanes_per_group = lanes;
-    plan->lds_cells_per_lane = stride;
-    plan->groups_per_cu = std::max<uint32_t>(1, groups);
-    // register budget = the waves per SIMD that are actually resident (one
-    // wave per workgroup): 8 workgroups per CU -> 2 waves/SIMD -> 256 VGPRs,
-    // enough for the decoder state without spills
-    if (!occ_over) occ = std::max<uint32_t>(1, (plan->groups_per_cu + 3) / 4);
-    plan->waves_per_simd = occ;
-    plan->persistent = env_int("LZGPU_PERSIST", 1) ? 1u : 0u;
   }
-  // the LDS kernel's work counter, after the probability slices
+  std::stable_sort(glob_idx.begin(), glob_idx.end(), by_len);
+  for (uint32_t i : glob_idx) order[k++] = i;
+  plan->persistent = env_int("LZGPU_PERSIST", 1) ? 1u : 0u;
+  // the LDS launches' work counters, after the probability slices
   plan->queue_offset = (plan->workspace_bytes + 63) & ~uint64_t(63);
-  plan->workspace_bytes = plan->queue_offset + 64;
+  plan->workspace_bytes = plan->queue_offset + 64 * LZMA_GPU_MAX_CLASSES;
   return SZ_OK;
 }
 
@@ -774,30 +805,36 @@ SRes LzmaGpu_DecodeBatchEx(const LzmaGpuPlan* plan, const LzmaGpuStreamDesc* d_d
                            const uint32_t* d_order, const Byte* d_src, Byte* d_dst,
                            void* d_workspace, LzmaGpuResult* d_results, void* stream) {
   if (!ensure_device()) return SZ_ERROR_FAIL;
-  if (!plan || !d_order || plan->n > 0xFFFFFFFFull || plan->n_lds > plan->n) return SZ_ERROR_PARAM;
+  if (!plan || !d_order || plan->n > 0xFFFFFFFFull || plan->n_lds > plan->n ||
+      plan->n_classes > LZMA_GPU_MAX_CLASSES)
+    return SZ_ERROR_PARAM;
   hipStream_t st = static_cast<hipStream_t>(stream);
   uint16_t* ws = static_cast<uint16_t*>(d_workspace);
-  const uint32_t n_lds = uint32_t(plan->n_lds), n_glob = uint32_t(plan->n - plan->n_lds);
-  uint32_t max_groups = 0;
-  if (plan->persistent) {
-    static int cus = 0;
-    if (cus == 0) {
-      int dev = 0, v = 0;
-      (void)hipGetDevice(&dev);
-      if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
-        cus = v;
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0, v = 0;
+    (void)hipGetDevice(&dev);
+    cus = (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
+              ? v
+              : int(kPlanCUs);
+  }
+  uint64_t first = 0;
+  for (uint32_t k = 0; k < plan->n_classes; ++k) {
+    const LzmaGpuLdsClass& c = plan->classes[k];
+    if (c.n == 0) continue;
+    if (first + c.n > plan->n_lds) return SZ_ERROR_PARAM;
+    const uint32_t max_groups = plan->persistent ? uint32_t(cus) * c.groups_per_cu : 0u;
+    uint32_t* queue = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(d_workspace) +
+                                                  plan->queue_offset + 64 * k);
+    if (lzgpu_launch_decode_lds(d_descs, d_order + first, uint32_t(c.n), d_src, d_dst, ws,
+                                d_results, c.lanes_per_group, c.lds_cells_per_lane,
+                                c.waves_per_simd, c.groups_per_cu, max_groups, queue, st) != 0) {
+      set_error("LDS decode kernel launch failed");
+      return SZ_ERROR_FAIL;
     }
-    max_groups = uint32_t(cus) * plan->groups_per_cu;
+    first += c.n;
   }
-  uint32_t* queue = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(d_workspace) +
-                                                plan->queue_offset);
-  if (n_lds && lzgpu_launch_decode_lds(d_descs, d_order, n_lds, d_src, d_dst, ws, d_results,
-                                       plan->lanes_per_group, plan->lds_cells_per_lane,
-                                       plan->waves_per_simd, plan->groups_per_cu, max_groups,
-                                       queue, st) != 0) {
-    set_error("LDS decode kernel launch failed");
-    return SZ_ERROR_FAIL;
-  }
+  const uint32_t n_lds = uint32_t(plan->n_lds), n_glob = uint32_t(plan->n - plan->n_lds);
   if (n_glob && lzgpu_launch_decode_batch(d_descs, d_order + n_lds, n_glob, d_src, d_dst, ws,
                                           d_results, st) != 0) {
     set_error("generic decode kernel launch failed");
@@ -923,6 +960,7 @@ size_t Lzma2Gpu_SplitBlocks(const Byte* src, size_t src_len, uint64_t* src_off,
 // ------------------------------------------------------------------ streaming sessions
 
 static_assert(sizeof(LzmaGpuSession) == 192, "LzmaGpuSession layout");
+static_assert(sizeof(LzmaGpuPlan) == 152, "LzmaGpuPlan layout");
 
 size_t LzmaGpu_SessionProbsBytes(const Byte* props, unsigned propsSize) {
   CLzmaProps pr;

@@ -72,12 +72,19 @@ class Result(ctypes.Structure):
                 ("dest_len", ctypes.c_uint64), ("src_len", ctypes.c_uint64)]
 
 
+class LdsClass(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_uint64), ("lanes_per_group", ctypes.c_uint32),
+                ("lds_cells_per_lane", ctypes.c_uint32), ("groups_per_cu", ctypes.c_uint32),
+                ("waves_per_simd", ctypes.c_uint32)]
+
+
 class Plan(ctypes.Structure):
     _fields_ = [("workspace_bytes", ctypes.c_uint64), ("n", ctypes.c_uint64),
                 ("n_lds", ctypes.c_uint64), ("lanes_per_group", ctypes.c_uint32),
                 ("lds_cells_per_lane", ctypes.c_uint32), ("groups_per_cu", ctypes.c_uint32),
                 ("waves_per_simd", ctypes.c_uint32), ("queue_offset", ctypes.c_uint64),
-                ("persistent", ctypes.c_uint32), ("reserved", ctypes.c_uint32 * 5)]
+                ("persistent", ctypes.c_uint32), ("n_classes", ctypes.c_uint32),
+                ("classes", LdsClass * 4)]
 
 
 class Session(ctypes.Structure):
@@ -99,7 +106,7 @@ class Session(ctypes.Structure):
 
 
 assert ctypes.sizeof(StreamDesc) == 48 and ctypes.sizeof(Result) == 24
-assert ctypes.sizeof(Session) == 192
+assert ctypes.sizeof(Session) == 192 and ctypes.sizeof(Plan) == 152
 assert ctypes.sizeof(CLzmaDec) == 136
 
 _P = ctypes.c_void_p

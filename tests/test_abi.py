@@ -130,6 +130,10 @@ def test_plan_batch_workspace_and_order():
     plan, order2 = L.plan_ex(descs)
     assert plan.n == 3 and plan.n_lds == 2 and list(order2) == [1, 0, 2]
     # LDS slice = sections of the default placement (LZGPU_LDS_MASK 0x1BF: all but
-    # SpecPos, matched-literal and LenHigh trees) = 56 * 2^pb + 324 + 0x100 << (lc+lp),
-    # sized for the largest LDS-resident stream of the batch (here lc3/pb2)
-    assert plan.lds_cells_per_lane == (56 * 4 + 324 + (256 << 3) + 3) // 4 * 4
+    # SpecPos, matched-literal and LenHigh trees) = 56 * 2^pb + 324 + 0x100 << (lc+lp);
+    # one LDS launch per table-width class, in the lane order
+    assert plan.n_classes == 2
+    c0, c1 = plan.classes[0], plan.classes[1]
+    assert (c0.n, c0.lds_cells_per_lane) == (1, 56 + 324 + 256)
+    assert (c1.n, c1.lds_cells_per_lane) == (1, (56 * 4 + 324 + (256 << 3) + 3) // 4 * 4)
+    assert plan.queue_offset % 64 == 0 and plan.workspace_bytes >= plan.queue_offset + 256
