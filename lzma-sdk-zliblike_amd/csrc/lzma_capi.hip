@@ -695,9 +695,8 @@ static LzmaGpuLdsClass plan_lds_class(uint32_t stride, uint64_t count) {
   //    16 streams per wave (the literal batching keeps them converged), as
   //    many waves as LDS allows (64K x 4 KiB: 16 lanes x 8 waves per CU);
   //  * latency -- few streams per CU (small batches, or wide lc+lp tables):
-  //    one stream per wave and 16 waves per CU, more lanes only once there
-  //    are 32+ streams per CU to place (config 2: 1 lane x 16 waves 5.8 GB/s
-  //    vs 4 lanes x 4 waves 2.5 GB/s).
+  //    one stream per wave, 16 waves per CU (config 2: 5.8 GB/s vs 2.5 GB/s
+  //    with 4 lanes x 4 waves; config 5: 2.6 GB/s vs 2.2 GB/s with 2 lanes).
   // Workgroups per CU stay a power of two so the four SIMDs carry equal
   // loads (6, 10 or 12 ran 10-30 % slower).
   auto pow2floor = [](uint32_t v) {
@@ -710,8 +709,7 @@ static LzmaGpuLdsClass plan_lds_class(uint32_t stride, uint64_t count) {
     lanes = std::min<uint32_t>(16, pow2floor(per_cu / 8));
     groups = pow2floor(std::min<uint32_t>(per_cu / lanes, 16));
   } else {
-    lanes = std::max<uint32_t>(1, pow2floor(uint32_t(std::min<uint64_t>(per_cu, per_cu_batch) / 16)));
-    groups = pow2floor(std::min<uint32_t>(per_cu / lanes, 16));
+    groups = pow2floor(std::min<uint32_t>(per_cu, 16));
   }
   const int over = env_int("LZGPU_LANES", 0);
   if (over > 0 && over <= 64 && uint32_t(over) * stride * 2 <= lds_per_cu) {
