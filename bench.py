@@ -679,6 +679,17 @@ def main():
         log(f"[rank {rank}] VERIFY FAILED: res={np.unique(res['res'])} "
             f"status={np.unique(res['status'])}")
 
+    if hasattr(L.lib, "LzmaGpu_ProfileRead"):  # profiling variant builds only
+        buf = (ctypes.c_ulonglong * 8)()
+        L.lib.LzmaGpu_ProfileRead(buf, 0)
+        lanes = max(1, buf[7])
+        names = ("literal_batches", "match_decode", "copy_tail", "decode_to_dic_total",
+                 "refills")
+        prof = {k: buf[i] / lanes for i, k in enumerate(names)}
+        prof["other_in_decode_to_dic"] = prof["decode_to_dic_total"] - sum(
+            prof[k] for k in names[:3])  # refills overlap the first three regions
+        log("PROF cycles per stream (lane-summed wave time): " + json.dumps(
+            {k: round(v) for k, v in prof.items()}))
     crc = measure_crc(L, torch, descs, d_desc, d_res, d_dst, plain, count, n, stream, dev,
                       args.steps) if not args.no_crc else None
     if crc is not None:

@@ -195,6 +195,14 @@ typedef __attribute__((address_space(1))) uint32_t gu32;
 #ifndef LZGPU_MLIT_PF
 #define LZGPU_MLIT_PF 1
 #endif
+//   LZGPU_TAIL_LIT     decode the symbol after a match at the end of the match
+//                      path (a matched literal there, not in the plain batch)
+#ifndef LZGPU_TAIL_LIT
+#define LZGPU_TAIL_LIT 0
+#endif
+#ifndef LZGPU_PROF
+#define LZGPU_PROF 0
+#endif
 //   LZGPU_UNIFORM_EXIT the literal batch loop exits only when every lane of
 //                      the wave is done (lanes drop out by a flag)
 #ifndef LZGPU_UNIFORM_EXIT
@@ -221,6 +229,9 @@ struct LzStateT {
   uint32_t need_rc_init, need_state_init;
   uint32_t tmp_n;
   uint8_t tmp[kLookahead];
+#if LZGPU_PROF
+  uint64_t prof[5];  // cycles: literal batches, match decode, copies + tail, calls, refills
+#endif
 };
 
 // Section accessor for placement mask M (compile-time): at<S>(i) is a pointer to
@@ -357,7 +368,13 @@ struct GlobalReader16 {
     if (!avail) nb = 0;
   }
   __device__ __forceinline__ uint32_t peek() const { return uint32_t(win) & 0xFFu; }
+#if LZGPU_PROF && !defined(LZGPU_HOST_EMU)
+  uint64_t prof = 0;
+#endif
   __device__ __forceinline__ void refill() {
+#if LZGPU_PROF && !defined(LZGPU_HOST_EMU)
+    const uint64_t t0 = __builtin_amdgcn_s_memtime();
+#endif
     if (half == 0) {
       win = nlo;
       half = 1;
@@ -367,6 +384,9 @@ struct GlobalReader16 {
       half = 0;
     }
     nb = 8;
+#if LZGPU_PROF && !defined(LZGPU_HOST_EMU)
+    prof += __builtin_amdgcn_s_memtime() - t0;
+#endif
   }
   __device__ __forceinline__ void advance(bool n) {
     if (n) {
@@ -723,6 +743,20 @@ __device__ __forceinline__ void lz_literal(Rc<Rd>& rc, const Tab<M, Lo>& T, uint
   total++;
 }
 
+// Region timing for profiling builds (-DLZGPU_PROF=1, never the default):
+// wave-uniform cycle stamps around the symbol loop's regions.
+#if LZGPU_PROF && !defined(LZGPU_HOST_EMU)
+__device__ __forceinline__ uint64_t lz_clock() { return __builtin_amdgcn_s_memtime(); }
+#define LZ_PROF_MARK(s, k, t)            \
+  do {                                   \
+    const uint64_t now_ = lz_clock();    \
+    (s).prof[k] += now_ - (t);           \
+    (t) = now_;                          \
+  } while (0)
+#else
+#define LZ_PROF_MARK(s, k, t) ((void)0)
+#endif
+
 // any lane of the wave (the lane itself in the host emulation)
 __device__ __forceinline__ bool lz_any(bool v) {
 #ifdef LZGPU_HOST_EMU
@@ -759,19 +793,27 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
   uint32_t mb_pf = (st >= 7) ? uint32_t(dic[ring_back(pos, r0, cap)]) : 0u;
 #endif
 
+  uint32_t ps = 0;
+#if LZGPU_PROF && !defined(LZGPU_HOST_EMU)
+  uint64_t t_prof = lz_clock();
+#endif
+  // LZGPU_TAIL_LIT: the symbol after a match was started at the end of the
+  // previous pass (its IsMatch bit said "match"): skip straight to the match
+  // path, the symbol must complete whatever the limits say now
+  bool pend_match = false;
   do {
-    uint32_t ps;
     uint32_t lcoder_is_rep;
     // Up to LZGPU_LIT_BATCH symbols per pass of this loop while they are
     // literals: a lane's symbol sequence is unchanged, but lanes of a wave
     // that sit in literal runs keep decoding together instead of idling
     // behind a neighbour's match path on every symbol.
-    bool is_match = false, stop = false;
+    bool is_match = pend_match, stop = false;
+    pend_match = false;
 #if LZGPU_UNIFORM_EXIT
     // lanes leave the batch by clearing lit_on, the loop itself exits only
     // when the whole wave is done: no divergent exit, so no per-iteration
     // copies of the lane state into exit registers
-    bool lit_on = true;
+    bool lit_on = !is_match;
 #pragma unroll 1
     for (int lit = 0; lit < LZGPU_LIT_BATCH; ++lit) {
       if (lit_on) {
@@ -795,7 +837,7 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
     }
 #else
 #pragma unroll 1
-    for (int lit = 0; lit < LZGPU_LIT_BATCH; ++lit) {
+    for (int lit = 0; lit < LZGPU_LIT_BATCH && !is_match; ++lit) {
       ps = total & pb_mask;
       if (rc.bit(T.template at<S_MATCH>((st << pb) + ps))) {
         is_match = true;
@@ -812,6 +854,7 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
       }
     }
 #endif
+    LZ_PROF_MARK(s, 0, t_prof);
     if (stop) break;
     if (!is_match) continue;
     if (!rc.bit(T.template at<S_REP>(st))) {
@@ -912,6 +955,7 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
       st = (st < 19) ? 7 : 10;
     }
     len += 2;
+    LZ_PROF_MARK(s, 1, t_prof);
     if (limit == pos) return kErrData;
     {
       const uint64_t room = limit - pos;
@@ -925,7 +969,27 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
       mb_pf = dic[ring_back(pos, r0, cap)];
 #endif
     }
+    LZ_PROF_MARK(s, 2, t_prof);
+#if LZGPU_TAIL_LIT
+    // The symbol after a match, decoded here while only the lanes that
+    // matched are active: if it is a literal it is a matched one (state >= 7),
+    // which would otherwise diverge from the plain literals of the batch.
+    if (pos < limit && rd.idx < in_limit) {
+      ps = total & pb_mask;
+      if (rc.bit(T.template at<S_MATCH>((st << pb) + ps))) {
+        pend_match = true;
+      } else {
+        lz_literal<M>(rc, T, st, prev, total, full, lc, lp_mask, dic, pos, cap, r0
+#if LZGPU_MB_PF
+                      , mb_pf
+#endif
+        );
+      }
+    }
+  } while ((pos < limit && rd.idx < in_limit) || pend_match);
+#else
   } while (pos < limit && rd.idx < in_limit);
+#endif
 
   rc.norm();
   s.range = rc.range;
@@ -1203,7 +1267,13 @@ __device__ __forceinline__ int lz_decode_to_dic(LzStateT<Lo>& s, uint64_t dic_li
       }
       BulkReader rd;
       rd.init(src, avail);
+#if LZGPU_PROF && !defined(LZGPU_HOST_EMU) && LZGPU_READER16
+      const int rr = lz_run_split<M>(s, dic_limit, rd, in_limit);
+      s.prof[4] += rd.prof;
+      if (rr != kOk) return kErrData;
+#else
       if (lz_run_split<M>(s, dic_limit, rd, in_limit) != kOk) return kErrData;
+#endif
       const uint32_t used = rd.idx;
       src_len += used;
       src += used;

@@ -136,3 +136,17 @@ extern "C" int lzgpu_launch_session(LzgpuSession* d_sess, uint32_t n, hipStream_
   hipLaunchKernelGGL(lzgpu_session_kernel, dim3(grid), dim3(block), 0, stream, d_sess, n);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
+
+#if LZGPU_PROF
+// profiling builds: read (and optionally clear) the region cycle sums
+extern "C" int LzmaGpu_ProfileRead(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(lzgpu::g_lz_prof), 8 * sizeof(unsigned long long)) !=
+      hipSuccess)
+    return -1;
+  if (reset) {
+    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(lzgpu::g_lz_prof), z, sizeof z) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#endif

@@ -18,6 +18,11 @@ typedef LzmaGpuSession LzgpuSession;
 
 namespace lzgpu {
 
+#if LZGPU_PROF && !defined(LZGPU_HOST_EMU)
+// per-region cycle sums over lanes (profiling builds only)
+__device__ unsigned long long g_lz_prof[8];
+#endif
+
 // One batch item with the whole probability table in global memory (the
 // generic kernel: any lc/lp/pb, LZMA or LZMA2).  The item's workspace slice
 // holds table_cells() cells: lo first, hi behind it.
@@ -144,8 +149,17 @@ __device__ __forceinline__ LzmaGpuResult lane_decode_lds(const LzmaGpuStreamDesc
   lz_init_dic_state(s, true, true);
   uint64_t sl = d.src_len;
   int status = kStNone;
+#if LZGPU_PROF && !defined(LZGPU_HOST_EMU)
+  for (int k = 0; k < 5; ++k) s.prof[k] = 0;
+  const uint64_t t0 = lz_clock();
+#endif
   int res = lz_decode_to_dic<false, LZGPU_LDS_MASK>(s, d.dst_cap, (const gbyte*)(src + d.src_off), sl,
                                     d.finish_mode, status);
+#if LZGPU_PROF && !defined(LZGPU_HOST_EMU)
+  s.prof[3] = lz_clock() - t0;
+  for (int k = 0; k < 5; ++k) atomicAdd(&g_lz_prof[k], (unsigned long long)s.prof[k]);
+  atomicAdd(&g_lz_prof[7], 1ull);
+#endif
   if (res == kOk && status == kStMoreInput) res = kErrInputEof;
   r.res = res;
   r.status = status;

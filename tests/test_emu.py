@@ -29,6 +29,8 @@ EMU_VARIANTS = {
     "uniform_exit": "-DLZGPU_UNIFORM_EXIT=1",
     "bit_select_rd4": "-DLZGPU_BIT_MASK=2 -DLZGPU_READER16=0",
     "bit_branchy": "-DLZGPU_BIT_MASK=0 -DLZGPU_MLIT_PF=0",
+    "tail_lit": "-DLZGPU_TAIL_LIT=1",
+    "tail_lit_divergent": "-DLZGPU_TAIL_LIT=1 -DLZGPU_UNIFORM_EXIT=0 -DLZGPU_LIT_BATCH=2",
 }
 
 
