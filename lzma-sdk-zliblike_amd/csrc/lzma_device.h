@@ -300,6 +300,7 @@ struct GlobalReader {
     pend = fetch();
   }
   __device__ __forceinline__ uint32_t peek() const { return uint32_t(win) & 0xFFu; }
+  __device__ __forceinline__ uint32_t used() const { return idx; }
   // consume the peeked byte when n is set
   __device__ __forceinline__ void advance(bool n) {
     win = n ? (win >> 8) : win;
@@ -329,7 +330,7 @@ struct GlobalReader16 {
   uint32_t half;   // 0: nxt untouched, 1: nxt low half already taken
   uint64_t win;
   uint64_t nlo, nhi;
-  uint32_t idx;
+  uint32_t taken;  // bytes moved into win since init (consumed = taken - nb)
 
   __device__ __forceinline__ void fetch() {
     // unconditional load (no phi on the loaded registers)
@@ -353,7 +354,6 @@ struct GlobalReader16 {
     const uint64_t blocks = avail ? (((a + avail + 15) & ~uintptr_t(15)) - a0) >> 4 : 0;
     wp = (const gu32*)a0;
     left = blocks > 0xFFFFFFF0ull ? 0xFFFFFFF0u : uint32_t(blocks);
-    idx = 0;
     fetch();  // first block: nlo/nhi
     if (skip < 8) {
       win = nlo >> (8 * skip);
@@ -366,7 +366,9 @@ struct GlobalReader16 {
       half = 0;
     }
     if (!avail) nb = 0;
+    taken = nb;
   }
+  __device__ __forceinline__ uint32_t used() const { return taken - nb; }
   __device__ __forceinline__ uint32_t peek() const { return uint32_t(win) & 0xFFu; }
 #if LZGPU_PROF && !defined(LZGPU_HOST_EMU)
   uint64_t prof = 0;
@@ -384,6 +386,7 @@ struct GlobalReader16 {
       half = 0;
     }
     nb = 8;
+    taken += 8;
 #if LZGPU_PROF && !defined(LZGPU_HOST_EMU)
     prof += __builtin_amdgcn_s_memtime() - t0;
 #endif
@@ -392,7 +395,6 @@ struct GlobalReader16 {
     if (n) {
       win >>= 8;
       --nb;
-      ++idx;
       if (nb == 0) refill();
     }
   }
@@ -400,7 +402,6 @@ struct GlobalReader16 {
     const uint32_t b = peek();
     win >>= 8;
     --nb;
-    ++idx;
     if (nb == 0) refill();
     return b;
   }
@@ -417,6 +418,7 @@ struct LocalReader {
   const uint8_t* p;
   uint32_t idx;
   __device__ __forceinline__ void init(const uint8_t* q) { p = q; idx = 0; }
+  __device__ __forceinline__ uint32_t used() const { return idx; }
   __device__ __forceinline__ uint32_t peek() const { return p[idx]; }
   __device__ __forceinline__ void advance(bool n) { idx += n ? 1u : 0u; }
   __device__ __forceinline__ uint32_t next() { return p[idx++]; }
@@ -827,7 +829,7 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
                         , mb_pf
 #endif
           );
-          if (!(pos < limit && rd.idx < in_limit)) {
+          if (!(pos < limit && rd.used() < in_limit)) {
             stop = true;
             lit_on = false;
           }
@@ -848,7 +850,7 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
                     , mb_pf
 #endif
       );
-      if (!(pos < limit && rd.idx < in_limit)) {
+      if (!(pos < limit && rd.used() < in_limit)) {
         stop = true;
         break;
       }
@@ -974,7 +976,7 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
     // The symbol after a match, decoded here while only the lanes that
     // matched are active: if it is a literal it is a matched one (state >= 7),
     // which would otherwise diverge from the plain literals of the batch.
-    if (pos < limit && rd.idx < in_limit) {
+    if (pos < limit && rd.used() < in_limit) {
       ps = total & pb_mask;
       if (rc.bit(T.template at<S_MATCH>((st << pb) + ps))) {
         pend_match = true;
@@ -986,9 +988,9 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
         );
       }
     }
-  } while ((pos < limit && rd.idx < in_limit) || pend_match);
+  } while ((pos < limit && rd.used() < in_limit) || pend_match);
 #else
-  } while (pos < limit && rd.idx < in_limit);
+  } while (pos < limit && rd.used() < in_limit);
 #endif
 
   rc.norm();
@@ -1031,7 +1033,7 @@ __device__ __forceinline__ int lz_run_split(LzStateT<Lo>& s, uint64_t limit, Rd&
     if (lz_run<M>(s, lim, rd, in_limit) != kOk) return kErrData;
     if (s.total >= s.dict_size) s.full = s.dict_size;
     lz_flush_pending(s, limit);
-  } while (s.pos < limit && rd.idx < in_limit && s.pending < kLenDone);
+  } while (s.pos < limit && rd.used() < in_limit && s.pending < kLenDone);
   if (s.pending > kLenDone) s.pending = kLenDone;
   return kOk;
 }
@@ -1274,7 +1276,7 @@ __device__ __forceinline__ int lz_decode_to_dic(LzStateT<Lo>& s, uint64_t dic_li
 #else
       if (lz_run_split<M>(s, dic_limit, rd, in_limit) != kOk) return kErrData;
 #endif
-      const uint32_t used = rd.idx;
+      const uint32_t used = rd.used();
       src_len += used;
       src += used;
       avail -= used;
@@ -1294,7 +1296,7 @@ __device__ __forceinline__ int lz_decode_to_dic(LzStateT<Lo>& s, uint64_t dic_li
       LocalReader rd;
       rd.init(s.tmp);
       if (lz_run_split<M>(s, dic_limit, rd, 0) != kOk) return kErrData;
-      taken -= (have - rd.idx);
+      taken -= (have - rd.used());
       src_len += taken;
       src += taken;
       avail -= taken;
