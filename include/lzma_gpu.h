@@ -231,6 +231,8 @@ typedef struct LzmaGpuLdsClass {
   uint32_t lds_cells_per_lane;
   uint32_t groups_per_cu;
   uint32_t waves_per_simd;
+  uint32_t lds_mask;      /* which probability sections live in LDS */
+  uint32_t reserved;
 } LzmaGpuLdsClass;
 
 typedef struct LzmaGpuPlan {

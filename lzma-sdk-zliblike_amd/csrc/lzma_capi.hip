@@ -639,20 +639,24 @@ SRes Lzma2Decode(Byte* dest, SizeT* destLen, const Byte* src, SizeT* srcLen, Byt
 // Workspace: each item gets a 16-byte aligned slice of table_cells() cells
 // (LZMA2 ranges: the lc+lp=4, pb=4 maximum).  Returns per-item lo-table
 // widths (0 = not LDS-eligible) through lo_w when given.
-static uint64_t plan_workspace(LzmaGpuStreamDesc* descs, size_t n, std::vector<uint32_t>* lo_w) {
+static uint64_t plan_workspace(LzmaGpuStreamDesc* descs, size_t n, std::vector<uint32_t>* lo_w,
+                               std::vector<uint32_t>* lat_w = nullptr) {
   uint64_t off = 0;
   if (lo_w) lo_w->assign(n, 0);
+  if (lat_w) lat_w->assign(n, 0);
   for (size_t i = 0; i < n; ++i) {
     LzmaGpuStreamDesc& d = descs[i];
     uint32_t np = 0;
     if (d.kind == LZMA_GPU_KIND_LZMA2) {
       np = lzgpu::table_cells(4, 0, 4);
       if (lo_w && d.props[0] <= 40) (*lo_w)[i] = lzgpu::lzma2_lds_cells(LZGPU_LDS_MASK);
+      if (lat_w && d.props[0] <= 40) (*lat_w)[i] = lzgpu::lzma2_lds_cells(LZGPU_LDS_MASK_LAT);
     } else {
       uint32_t lc, lp, pb, dict;
       if (lzgpu::lz_props_parse(d.props, d.props_size, lc, lp, pb, dict) == SZ_OK) {
         np = lzgpu::table_cells(lc, lp, pb);
         if (lo_w) (*lo_w)[i] = lzgpu::make_layout(lc, lp, pb, LZGPU_LDS_MASK).lds_cells;
+        if (lat_w) (*lat_w)[i] = lzgpu::make_layout(lc, lp, pb, LZGPU_LDS_MASK_LAT).lds_cells;
       }
     }
     d.probs_off = off;
@@ -680,9 +684,11 @@ size_t LzmaGpu_PlanBatch(LzmaGpuStreamDesc* descs, size_t n, uint32_t* order) {
 static const uint32_t kPlanCUs = uint32_t(env_int("LZGPU_CUS", 256));
 
 // Launch shape of one LDS class: `stride` cells per stream, `count` streams.
-static LzmaGpuLdsClass plan_lds_class(uint32_t stride, uint64_t count) {
+static LzmaGpuLdsClass plan_lds_class(uint32_t stride, uint64_t count, uint32_t mask,
+                                      bool* latency = nullptr) {
   LzmaGpuLdsClass c;
   memset(&c, 0, sizeof c);
+  c.lds_mask = mask;
   stride = (stride + 3) & ~3u;  // 8-byte aligned per-lane slices
   const uint32_t lds_per_cu = 160 * 1024;
   const uint32_t per_cu = std::max<uint32_t>(1, lds_per_cu / (stride * 2));  // streams/CU
@@ -705,6 +711,7 @@ static LzmaGpuLdsClass plan_lds_class(uint32_t stride, uint64_t count) {
   };
   const uint64_t per_cu_batch = (count + kPlanCUs - 1) / kPlanCUs;
   uint32_t lanes = 1, groups = 16;
+  if (latency) *latency = !(per_cu >= 64 && per_cu_batch >= 64);
   if (per_cu >= 64 && per_cu_batch >= 64) {
     lanes = std::min<uint32_t>(16, pow2floor(per_cu / 8));
     groups = pow2floor(std::min<uint32_t>(per_cu / lanes, 16));
@@ -743,8 +750,8 @@ SRes LzmaGpu_PlanBatchEx(LzmaGpuStreamDesc* descs, size_t n, uint32_t* order,
                          LzmaGpuPlan* plan) {
   if (!order || !plan) return SZ_ERROR_PARAM;
   memset(plan, 0, sizeof *plan);
-  std::vector<uint32_t> w;
-  plan->workspace_bytes = plan_workspace(descs, n, &w);
+  std::vector<uint32_t> w, w_lat;
+  plan->workspace_bytes = plan_workspace(descs, n, &w, &w_lat);
   plan->n = n;
   // LDS-eligible: lo table <= 16384 cells (32 KiB, >= 5 streams per CU)
   const uint32_t kMaxLdsCells = 16384;
@@ -779,7 +786,18 @@ SRes LzmaGpu_PlanBatchEx(LzmaGpuStreamDesc* descs, size_t n, uint32_t* order,
     if (bucket_idx[b].empty()) continue;
     std::stable_sort(bucket_idx[b].begin(), bucket_idx[b].end(), by_len);
     for (uint32_t i : bucket_idx[b]) order[k++] = i;
-    const LzmaGpuLdsClass c = plan_lds_class(bucket_stride[b], bucket_idx[b].size());
+    // throughput placement first; a class that lands in the latency regime is
+    // re-planned with the latency placement (more tables in LDS, few streams)
+    bool lat = false;
+    LzmaGpuLdsClass c = plan_lds_class(bucket_stride[b], bucket_idx[b].size(), LZGPU_LDS_MASK,
+                                       &lat);
+    const int mask_over = env_int("LZGPU_MASK", 0);  // 1: throughput, 2: latency placement
+    if ((lat && mask_over != 1) || mask_over == 2) {
+      uint32_t stride_lat = 0;
+      for (uint32_t i : bucket_idx[b]) stride_lat = std::max(stride_lat, w_lat[i]);
+      if (stride_lat <= kMaxLdsCells)
+        c = plan_lds_class(stride_lat, bucket_idx[b].size(), LZGPU_LDS_MASK_LAT);
+    }
     plan->classes[plan->n_classes++] = c;
     plan->n_lds += c.n;
     if (c.n > best) {
@@ -826,7 +844,8 @@ SRes LzmaGpu_DecodeBatchEx(const LzmaGpuPlan* plan, const LzmaGpuStreamDesc* d_d
                                                   plan->queue_offset + 64 * k);
     if (lzgpu_launch_decode_lds(d_descs, d_order + first, uint32_t(c.n), d_src, d_dst, ws,
                                 d_results, c.lanes_per_group, c.lds_cells_per_lane,
-                                c.waves_per_simd, c.groups_per_cu, max_groups, queue, st) != 0) {
+                                c.waves_per_simd, c.groups_per_cu, max_groups, queue, c.lds_mask,
+                                st) != 0) {
       set_error("LDS decode kernel launch failed");
       return SZ_ERROR_FAIL;
     }
@@ -958,7 +977,7 @@ size_t Lzma2Gpu_SplitBlocks(const Byte* src, size_t src_len, uint64_t* src_off,
 // ------------------------------------------------------------------ streaming sessions
 
 static_assert(sizeof(LzmaGpuSession) == 192, "LzmaGpuSession layout");
-static_assert(sizeof(LzmaGpuPlan) == 152, "LzmaGpuPlan layout");
+static_assert(sizeof(LzmaGpuPlan) == 184, "LzmaGpuPlan layout");
 
 size_t LzmaGpu_SessionProbsBytes(const Byte* props, unsigned propsSize) {
   CLzmaProps pr;

@@ -125,10 +125,18 @@ __host__ __device__ inline uint32_t num_probs(uint32_t lc, uint32_t lp) {
 }
 
 // Placement used by the fast kernel (build-time; A/B'd on MI355X):
-// default = everything in LDS except SpecPos, the matched-literal trees and the
-// LenHigh trees (1272 B per lc0/pb0 stream, 128 resident streams per CU).
+// default = only the per-symbol tables in LDS -- IsMatch, IsRep/G0/G1/G2 and the
+// plain literal tree (632 B per lc0/pb0 stream: 256 resident streams per CU,
+// 16 lanes x 4 waves per SIMD); the match path's tables live in global memory
+// (+31 % over keeping them in LDS at half the resident streams).
 #ifndef LZGPU_LDS_MASK
-#define LZGPU_LDS_MASK 0x1BFu
+#define LZGPU_LDS_MASK 0x105u
+#endif
+// Placement for the latency regime (few streams per CU, one per wave): LDS is
+// not the limit there, the match path's round trips are -- everything but
+// SpecPos, the matched-literal trees and LenHigh stays in LDS.
+#ifndef LZGPU_LDS_MASK_LAT
+#define LZGPU_LDS_MASK_LAT 0x1BFu
 #endif
 
 // Explicit address spaces: LDS (3) for the lo table of the fast kernel, global

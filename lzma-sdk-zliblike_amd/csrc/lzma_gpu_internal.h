@@ -16,7 +16,8 @@ extern "C" int lzgpu_launch_decode_lds(const LzmaGpuStreamDesc* d_descs, const u
                                        uint16_t* d_ws, LzmaGpuResult* d_results, uint32_t lanes,
                                        uint32_t stride, uint32_t waves_per_simd,
                                        uint32_t groups_per_cu, uint32_t max_groups,
-                                       uint32_t* d_queue, hipStream_t stream);
+                                       uint32_t* d_queue, uint32_t lds_mask,
+                                       hipStream_t stream);
 extern "C" int lzgpu_launch_crc_arrays(const uint8_t* d_data, const uint64_t* d_off,
                                        const uint64_t* d_len, uint32_t n,
                                        const uint32_t* d_chunk_base,

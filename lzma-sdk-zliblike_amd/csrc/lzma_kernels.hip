@@ -39,7 +39,7 @@ __global__ void __launch_bounds__(64) lzgpu_decode_batch_kernel(
 // launcher zeroes), so no lane idles behind a slower neighbour in its wave
 // and the chip drains without a partial last round of workgroups.  Every
 // lane exits once the queue passes n.
-template <int W>
+template <int W, uint32_t M>
 __global__ void __launch_bounds__(64, W) lzgpu_decode_lds_kernel(
     const LzmaGpuStreamDesc* __restrict__ descs, const uint32_t* __restrict__ order, uint32_t n,
     const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, uint16_t* __restrict__ ws,
@@ -51,7 +51,7 @@ __global__ void __launch_bounds__(64, W) lzgpu_decode_lds_kernel(
   while (idx < n) {
     const uint32_t id = order ? order[idx] : idx;
     const LzmaGpuStreamDesc d = descs[id];
-    results[id] = lane_decode_lds(d, src, dst, ws, lo, stride);
+    results[id] = lane_decode_lds<M>(d, src, dst, ws, lo, stride);
     idx = lanes_total + atomicAdd(queue, 1u);
   }
 }
@@ -76,7 +76,7 @@ extern "C" int lzgpu_launch_decode_batch(const LzmaGpuStreamDesc* d_descs, const
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-template <int W>
+template <int W, uint32_t M>
 static int launch_lds(const LzmaGpuStreamDesc* d_descs, const uint32_t* d_order, uint32_t n,
                       const uint8_t* d_src, uint8_t* d_dst, uint16_t* d_ws,
                       LzmaGpuResult* d_results, uint32_t lanes, uint32_t stride,
@@ -84,7 +84,7 @@ static int launch_lds(const LzmaGpuStreamDesc* d_descs, const uint32_t* d_order,
                       hipStream_t stream) {
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(lzgpu_decode_lds_kernel<W>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(lzgpu_decode_lds_kernel<W, M>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
   }
@@ -98,9 +98,26 @@ static int launch_lds(const LzmaGpuStreamDesc* d_descs, const uint32_t* d_order,
   }
   uint32_t grid = (n + lanes - 1) / lanes;
   if (max_groups && grid > max_groups) grid = max_groups;
-  hipLaunchKernelGGL(lzgpu_decode_lds_kernel<W>, dim3(grid), dim3(lanes), lds, stream, d_descs,
+  auto kfn = lzgpu_decode_lds_kernel<W, M>;
+  hipLaunchKernelGGL(kfn, dim3(grid), dim3(lanes), lds, stream, d_descs,
                      d_order, n, d_src, d_dst, d_ws, d_results, stride, d_queue);
   return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+template <uint32_t M>
+static int launch_lds_w(const LzmaGpuStreamDesc* d_descs, const uint32_t* d_order, uint32_t n,
+                        const uint8_t* d_src, uint8_t* d_dst, uint16_t* d_ws,
+                        LzmaGpuResult* d_results, uint32_t lanes, uint32_t stride,
+                        uint32_t waves_per_simd, uint32_t groups_per_cu, uint32_t max_groups,
+                        uint32_t* d_queue, hipStream_t stream) {
+  if (waves_per_simd <= 1)
+    return launch_lds<1, M>(d_descs, d_order, n, d_src, d_dst, d_ws, d_results, lanes, stride,
+                            groups_per_cu, max_groups, d_queue, stream);
+  if (waves_per_simd == 2)
+    return launch_lds<2, M>(d_descs, d_order, n, d_src, d_dst, d_ws, d_results, lanes, stride,
+                            groups_per_cu, max_groups, d_queue, stream);
+  return launch_lds<4, M>(d_descs, d_order, n, d_src, d_dst, d_ws, d_results, lanes, stride,
+                          groups_per_cu, max_groups, d_queue, stream);
 }
 
 extern "C" int lzgpu_launch_decode_lds(const LzmaGpuStreamDesc* d_descs, const uint32_t* d_order,
@@ -108,25 +125,17 @@ extern "C" int lzgpu_launch_decode_lds(const LzmaGpuStreamDesc* d_descs, const u
                                        uint16_t* d_ws, LzmaGpuResult* d_results, uint32_t lanes,
                                        uint32_t stride, uint32_t waves_per_simd,
                                        uint32_t groups_per_cu, uint32_t max_groups,
-                                       uint32_t* d_queue, hipStream_t stream) {
+                                       uint32_t* d_queue, uint32_t lds_mask, hipStream_t stream) {
   if (n == 0) return 0;
-  switch (waves_per_simd) {
-    case 8:
-      return launch_lds<8>(d_descs, d_order, n, d_src, d_dst, d_ws, d_results, lanes, stride,
-                           groups_per_cu, max_groups, d_queue, stream);
-    case 6:
-      return launch_lds<6>(d_descs, d_order, n, d_src, d_dst, d_ws, d_results, lanes, stride,
-                           groups_per_cu, max_groups, d_queue, stream);
-    case 2:
-      return launch_lds<2>(d_descs, d_order, n, d_src, d_dst, d_ws, d_results, lanes, stride,
-                           groups_per_cu, max_groups, d_queue, stream);
-    case 1:
-      return launch_lds<1>(d_descs, d_order, n, d_src, d_dst, d_ws, d_results, lanes, stride,
-                           groups_per_cu, max_groups, d_queue, stream);
-    default:
-      return launch_lds<4>(d_descs, d_order, n, d_src, d_dst, d_ws, d_results, lanes, stride,
-                           groups_per_cu, max_groups, d_queue, stream);
-  }
+  if (lds_mask == LZGPU_LDS_MASK)
+    return launch_lds_w<LZGPU_LDS_MASK>(d_descs, d_order, n, d_src, d_dst, d_ws, d_results, lanes,
+                                        stride, waves_per_simd, groups_per_cu, max_groups,
+                                        d_queue, stream);
+  if (lds_mask == LZGPU_LDS_MASK_LAT)
+    return launch_lds_w<LZGPU_LDS_MASK_LAT>(d_descs, d_order, n, d_src, d_dst, d_ws, d_results,
+                                            lanes, stride, waves_per_simd, groups_per_cu,
+                                            max_groups, d_queue, stream);
+  return -1;  // no kernel built for this placement
 }
 
 extern "C" int lzgpu_launch_session(LzgpuSession* d_sess, uint32_t n, hipStream_t stream) {

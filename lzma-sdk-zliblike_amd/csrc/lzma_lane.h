@@ -97,6 +97,7 @@ __host__ __device__ __forceinline__ uint32_t lzma2_lds_cells(uint32_t m) {
 // One LZMA (or LZMA2) batch item with the LDS-placed sections (LZGPU_LDS_MASK)
 // in the lane's LDS slice (lo_cap cells) and the others in its global
 // workspace slice.  The planner only routes items here whose LDS part fits.
+template <uint32_t M = LZGPU_LDS_MASK>
 __device__ __forceinline__ LzmaGpuResult lane_decode_lds(const LzmaGpuStreamDesc& d,
                                                          const uint8_t* __restrict__ src,
                                                          uint8_t* __restrict__ dst,
@@ -108,7 +109,7 @@ __device__ __forceinline__ LzmaGpuResult lane_decode_lds(const LzmaGpuStreamDesc
   r.src_len = 0;
   if (d.kind == LZMA_GPU_KIND_LZMA2) {
     // chunks may switch lc/lp/pb (lc + lp <= 4): the slice holds the widest layout
-    if (d.probs_off == LZMA_GPU_NO_WORKSPACE || lzma2_lds_cells(LZGPU_LDS_MASK) > lo_cap) {
+    if (d.probs_off == LZMA_GPU_NO_WORKSPACE || lzma2_lds_cells(M) > lo_cap) {
       r.res = (d.props[0] > 40) ? kErrUnsupported : kErrMem;
       return r;
     }
@@ -118,7 +119,7 @@ __device__ __forceinline__ LzmaGpuResult lane_decode_lds(const LzmaGpuStreamDesc
     if (r.res != kOk) return r;
     uint64_t sl = d.src_len;
     int status = kStNone;
-    r.res = lz2_decode_to_dic<LZGPU_LDS_MASK>(p, d.dst_cap, (const gbyte*)(src + d.src_off), sl,
+    r.res = lz2_decode_to_dic<M>(p, d.dst_cap, (const gbyte*)(src + d.src_off), sl,
                                               d.finish_mode, status);
     r.status = status;
     r.dest_len = p.dec.pos;
@@ -133,7 +134,7 @@ __device__ __forceinline__ LzmaGpuResult lane_decode_lds(const LzmaGpuStreamDesc
   r.res = lz_props_parse(d.props, d.props_size, s.lc, s.lp, s.pb, s.dict_size);
   if (r.res != kOk) return r;
   if (d.probs_off == LZMA_GPU_NO_WORKSPACE ||
-      make_layout(s.lc, s.lp, s.pb, LZGPU_LDS_MASK).lds_cells > lo_cap) {
+      make_layout(s.lc, s.lp, s.pb, M).lds_cells > lo_cap) {
     r.res = kErrMem;
     return r;
   }
@@ -153,7 +154,7 @@ __device__ __forceinline__ LzmaGpuResult lane_decode_lds(const LzmaGpuStreamDesc
   for (int k = 0; k < 5; ++k) s.prof[k] = 0;
   const uint64_t t0 = lz_clock();
 #endif
-  int res = lz_decode_to_dic<false, LZGPU_LDS_MASK>(s, d.dst_cap, (const gbyte*)(src + d.src_off), sl,
+  int res = lz_decode_to_dic<false, M>(s, d.dst_cap, (const gbyte*)(src + d.src_off), sl,
                                     d.finish_mode, status);
 #if LZGPU_PROF && !defined(LZGPU_HOST_EMU)
   s.prof[3] = lz_clock() - t0;

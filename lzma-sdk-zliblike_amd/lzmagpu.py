@@ -75,7 +75,8 @@ class Result(ctypes.Structure):
 class LdsClass(ctypes.Structure):
     _fields_ = [("n", ctypes.c_uint64), ("lanes_per_group", ctypes.c_uint32),
                 ("lds_cells_per_lane", ctypes.c_uint32), ("groups_per_cu", ctypes.c_uint32),
-                ("waves_per_simd", ctypes.c_uint32)]
+                ("waves_per_simd", ctypes.c_uint32), ("lds_mask", ctypes.c_uint32),
+                ("reserved", ctypes.c_uint32)]
 
 
 class Plan(ctypes.Structure):
@@ -106,7 +107,7 @@ class Session(ctypes.Structure):
 
 
 assert ctypes.sizeof(StreamDesc) == 48 and ctypes.sizeof(Result) == 24
-assert ctypes.sizeof(Session) == 192 and ctypes.sizeof(Plan) == 152
+assert ctypes.sizeof(Session) == 192 and ctypes.sizeof(Plan) == 184
 assert ctypes.sizeof(CLzmaDec) == 136
 
 _P = ctypes.c_void_p

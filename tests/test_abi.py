@@ -129,11 +129,20 @@ def test_plan_batch_workspace_and_order():
                 assert cells(lc, lp, pb) <= 1846 + (768 << (lc + lp))
     plan, order2 = L.plan_ex(descs)
     assert plan.n == 3 and plan.n_lds == 2 and list(order2) == [1, 0, 2]
-    # LDS slice = sections of the default placement (LZGPU_LDS_MASK 0x1BF: all but
-    # SpecPos, matched-literal and LenHigh trees) = 56 * 2^pb + 324 + 0x100 << (lc+lp);
-    # one LDS launch per table-width class, in the lane order
+    # one LDS launch per table-width class, in the lane order.  A one-stream class
+    # is in the latency regime: placement 0x1BF (all but SpecPos, matched-literal
+    # and LenHigh trees in LDS) = 56 * 2^pb + 324 + 0x100 << (lc+lp) cells
     assert plan.n_classes == 2
     c0, c1 = plan.classes[0], plan.classes[1]
-    assert (c0.n, c0.lds_cells_per_lane) == (1, 56 + 324 + 256)
-    assert (c1.n, c1.lds_cells_per_lane) == (1, (56 * 4 + 324 + (256 << 3) + 3) // 4 * 4)
+    assert (c0.n, c0.lds_cells_per_lane, c0.lds_mask) == (1, 56 + 324 + 256, 0x1BF)
+    assert (c1.n, c1.lds_cells_per_lane, c1.lds_mask) == (1, 56 * 4 + 324 + (256 << 3), 0x1BF)
+    assert (c0.lanes_per_group, c0.groups_per_cu) == (1, 16)
+    # a full-size batch is in the throughput regime: placement 0x105 (IsMatch,
+    # IsRep/G0/G1/G2, plain literal tree) = 12 * 2^pb + 48 + 0x100 << (lc+lp) cells
+    big = L.make_descs([dict(src_off=0, src_len=1000, dst_off=4096 * i, dst_cap=4096,
+                             props=b"\x00\x00\x10\x00\x00") for i in range(65536)])
+    pb_, _ = L.plan_ex(big)
+    cb = pb_.classes[0]
+    assert (pb_.n_classes, cb.n, cb.lds_cells_per_lane, cb.lds_mask) == (1, 65536, 316, 0x105)
+    assert (cb.lanes_per_group, cb.groups_per_cu, cb.waves_per_simd) == (16, 16, 4)
     assert plan.queue_offset % 64 == 0 and plan.workspace_bytes >= plan.queue_offset + 256

@@ -24,6 +24,7 @@ EMU_VARIANTS = {
     "litm_global": "-DLZGPU_LDS_MASK=0x1FF -DLZGPU_MB_PF=0 -DLZGPU_READER16=0",
     "hot_only_lds": "-DLZGPU_LDS_MASK=0x107",
     "full_lds": "-DLZGPU_LDS_MASK=0x3FF",
+    "latency_mask": "-DLZGPU_LDS_MASK=0x1BF",
     "copy_v2": "-DLZGPU_COPY_V2=1",
     "lit_batch": "-DLZGPU_LIT_BATCH=3",
     "uniform_exit": "-DLZGPU_UNIFORM_EXIT=1",
