@@ -211,6 +211,12 @@ typedef __attribute__((address_space(1))) uint32_t gu32;
 #ifndef LZGPU_PROF
 #define LZGPU_PROF 0
 #endif
+//   LZGPU_TREE_GPF     bit trees in global memory (length, slot, SpecPos, Align
+//                      under the default placement) read three levels per load
+//                      batch instead of one dependent round trip per bit
+#ifndef LZGPU_TREE_GPF
+#define LZGPU_TREE_GPF 1
+#endif
 //   LZGPU_UNIFORM_EXIT the literal batch loop exits only when every lane of
 //                      the wave is done (lanes drop out by a flag)
 #ifndef LZGPU_UNIFORM_EXIT
@@ -542,6 +548,24 @@ struct Rc {
     for (int k = 0; k < BITS; ++k) m = (m << 1) | bit(probs + m);
 #endif
     return m - (1u << BITS);
+  }
+  // Three levels of a bit tree below node `root` (cells root, 2root + {0,1},
+  // 4root + {0..3}) with all seven probabilities loaded in one batch: one
+  // memory round trip instead of three dependent ones when the tree lives in
+  // global memory.  Returns the node 8 * root + (the three bits, MSB first).
+  template <class P>
+  __device__ __forceinline__ uint32_t sub3(P probs, uint32_t root) {
+    const uint32_t r2 = root * 2, r4 = root * 4;
+    const uint32_t c0 = probs[root], c10 = probs[r2], c11 = probs[r2 + 1];
+    const uint32_t c20 = probs[r4], c21 = probs[r4 + 1], c22 = probs[r4 + 2],
+                   c23 = probs[r4 + 3];
+    const uint32_t b0 = bit_v(c0, probs + root);
+    uint32_t m = r2 + b0;
+    const uint32_t b1 = bit_v(b0 ? c11 : c10, probs + m);
+    m = 2 * m + b1;
+    const uint32_t p2 = b0 ? (b1 ? c23 : c22) : (b1 ? c21 : c20);
+    const uint32_t b2 = bit_v(p2, probs + m);
+    return 2 * m + b2;
   }
   // fixed-probability bit in the reference's exact arithmetic (LzmaDec.c:325-334)
   __device__ __forceinline__ void direct(uint32_t& v) {
@@ -910,17 +934,36 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
       auto lbase = [&]() {
         if constexpr (len_lds) return T.lo + lsec_o; else return T.gl + lsec_o;
       }();
-      if (!rc.bit(lbase))
-        len = rc.template tree<3>(lbase + 2 + (ps << 3));
-      else if (!rc.bit(lbase + 1))
-        len = 8 + rc.template tree<3>(lbase + 2 + (8u << pb) + (ps << 3));
-      else
-        len = 16 + rc.template tree<8>(T.template at<S_LENHI>(lcoder_is_rep << 8));
+      if constexpr (!len_lds && LZGPU_TREE_GPF) {
+        // global length coder: the choice bits and the low tree load together,
+        // the mid tree only behind choice = 1
+        const uint32_t ch = lbase[0];
+        auto lo_t = lbase + 2 + (ps << 3);
+        if (!rc.bit_v(ch, lbase))
+          len = rc.sub3(lo_t, 1) - 8;
+        else if (!rc.bit(lbase + 1))
+          len = 8 + rc.sub3(lbase + 2 + (8u << pb) + (ps << 3), 1) - 8;
+        else
+          len = 16 + rc.template tree<8>(T.template at<S_LENHI>(lcoder_is_rep << 8));
+      } else {
+        if (!rc.bit(lbase))
+          len = rc.template tree<3>(lbase + 2 + (ps << 3));
+        else if (!rc.bit(lbase + 1))
+          len = 8 + rc.template tree<3>(lbase + 2 + (8u << pb) + (ps << 3));
+        else
+          len = 16 + rc.template tree<8>(T.template at<S_LENHI>(lcoder_is_rep << 8));
+      }
     }
 
     if (st >= 12) {
       const uint32_t lstate = len < 4 ? len : 3;
-      uint32_t dist = rc.template tree<6>(T.template at<S_SLOT>(lstate << 6));
+      uint32_t dist;
+      if constexpr (((M >> S_SLOT) & 1u) == 0u && LZGPU_TREE_GPF) {
+        auto sl_t = T.template at<S_SLOT>(lstate << 6);
+        dist = rc.sub3(sl_t, rc.sub3(sl_t, 1)) - 64;
+      } else {
+        dist = rc.template tree<6>(T.template at<S_SLOT>(lstate << 6));
+      }
       if (dist >= 4) {
         const uint32_t slot = dist;
         uint32_t nbits = (slot >> 1) - 1;
@@ -929,22 +972,39 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
           dist <<= nbits;
           uint32_t mask = 1, node = 1;
           const uint32_t sp = dist - slot - 1;
-          do {
+          if constexpr (((M >> S_SPEC) & 1u) == 0u && LZGPU_TREE_GPF) {
+            if (nbits >= 3) {
+              // first three reverse-tree bits in one load batch
+              node = rc.sub3(T.template at<S_SPEC>(sp), 1);
+              dist |= ((node >> 2) & 1u) | (((node >> 1) & 1u) << 1) | ((node & 1u) << 2);
+              mask = 8;
+              nbits -= 3;
+            }
+          }
+          while (nbits != 0) {
             uint32_t b = rc.bit(T.template at<S_SPEC>(sp + node));
             node = (node << 1) | b;
             dist |= b ? mask : 0u;
             mask <<= 1;
-          } while (--nbits != 0);
+            --nbits;
+          }
         } else {
           nbits -= 4;
           do rc.direct(dist); while (--nbits != 0);
           dist <<= 4;
           uint32_t node = 1;
+          if constexpr (((M >> S_ALIGN) & 1u) == 0u && LZGPU_TREE_GPF) {
+            node = rc.sub3(T.template at<S_ALIGN>(0), 1);
+            dist |= ((node >> 2) & 1u) | (((node >> 1) & 1u) << 1) | ((node & 1u) << 2);
+            const uint32_t b = rc.bit(T.template at<S_ALIGN>(node));
+            dist |= b << 3;
+          } else {
 #pragma unroll
-          for (uint32_t k = 0; k < 4; ++k) {
-            uint32_t b = rc.bit(T.template at<S_ALIGN>(node));
-            node = (node << 1) | b;
-            dist |= b << k;
+            for (uint32_t k = 0; k < 4; ++k) {
+              uint32_t b = rc.bit(T.template at<S_ALIGN>(node));
+              node = (node << 1) | b;
+              dist |= b << k;
+            }
           }
           if (dist == 0xFFFFFFFFu) {
             len += kLenDone;

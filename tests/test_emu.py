@@ -25,6 +25,7 @@ EMU_VARIANTS = {
     "hot_only_lds": "-DLZGPU_LDS_MASK=0x107",
     "full_lds": "-DLZGPU_LDS_MASK=0x3FF",
     "latency_mask": "-DLZGPU_LDS_MASK=0x1BF",
+    "no_tree_gpf": "-DLZGPU_TREE_GPF=0",
     "copy_v2": "-DLZGPU_COPY_V2=1",
     "lit_batch": "-DLZGPU_LIT_BATCH=3",
     "uniform_exit": "-DLZGPU_UNIFORM_EXIT=1",
