@@ -680,15 +680,18 @@ def main():
             f"status={np.unique(res['status'])}")
 
     if hasattr(L.lib, "LzmaGpu_ProfileRead"):  # profiling variant builds only
-        buf = (ctypes.c_ulonglong * 8)()
+        buf = (ctypes.c_ulonglong * 24)()
         L.lib.LzmaGpu_ProfileRead(buf, 0)
-        lanes = max(1, buf[7])
+        lanes = max(1, buf[23])
         names = ("literal_batches", "match_decode", "copy_tail", "decode_to_dic_total",
-                 "refills")
+                 "refills", "batch_iters", "lit_lanes", "mlit_lanes", "mixed_iters",
+                 "match_entries", "match_lanes", "live_lanes", "bytes", "matches",
+                 "cyc_ismatch", "cyc_literal", "cyc_lit_tail")
         prof = {k: buf[i] / lanes for i, k in enumerate(names)}
         prof["other_in_decode_to_dic"] = prof["decode_to_dic_total"] - sum(
             prof[k] for k in names[:3])  # refills overlap the first three regions
-        log("PROF cycles per stream (lane-summed wave time): " + json.dumps(
+        log("PROF per stream (cycles: lane-summed wave time; counts: wave-level "
+            "seen by each lane): " + json.dumps(
             {k: round(v) for k, v in prof.items()}))
     crc = measure_crc(L, torch, descs, d_desc, d_res, d_dst, plain, count, n, stream, dev,
                       args.steps) if not args.no_crc else None

@@ -698,8 +698,12 @@ static LzmaGpuLdsClass plan_lds_class(uint32_t stride, uint64_t count, uint32_t 
     occ = uint32_t(occ_over);
   // Two regimes (profiles/r01_variants v17-v28):
   //  * throughput -- LDS holds >= 64 streams per CU and the batch fills them:
-  //    16 streams per wave (the literal batching keeps them converged), as
-  //    many waves as LDS allows (64K x 4 KiB: 16 lanes x 8 waves per CU);
+  //    up to 32 streams per wave with at least 8 waves per CU (64K x 4 KiB:
+  //    32 lanes x 8 waves per CU).  A VALU instruction of a wave whose active
+  //    lanes all sit in its low half costs one pass whether 16 or 32 lanes are
+  //    active, so 32 lanes halve the instructions per stream (ubench:
+  //    scripts/ubench/lit_ubench.hip; v38-v41: 24.6 -> 27.0 GB/s with the
+  //    checkpoint reader);
   //  * latency -- few streams per CU (small batches, or wide lc+lp tables):
   //    one stream per wave, 16 waves per CU (config 2: 5.8 GB/s vs 2.5 GB/s
   //    with 4 lanes x 4 waves; config 5: 2.6 GB/s vs 2.2 GB/s with 2 lanes).
@@ -713,7 +717,7 @@ static LzmaGpuLdsClass plan_lds_class(uint32_t stride, uint64_t count, uint32_t 
   uint32_t lanes = 1, groups = 16;
   if (latency) *latency = !(per_cu >= 64 && per_cu_batch >= 64);
   if (per_cu >= 64 && per_cu_batch >= 64) {
-    lanes = std::min<uint32_t>(16, pow2floor(per_cu / 8));
+    lanes = std::min<uint32_t>(32, pow2floor(per_cu / 8));
     groups = pow2floor(std::min<uint32_t>(per_cu / lanes, 16));
   } else {
     groups = pow2floor(std::min<uint32_t>(per_cu, 16));

@@ -100,7 +100,10 @@ __host__ __device__ __forceinline__ Layout make_layout(uint32_t lc, uint32_t lp,
                                                        uint32_t lds_mask) {
   Layout L;
   uint32_t a = 0, b = 0;
-  for (uint32_t sec = 0; sec < S_NSEC; ++sec) {
+  // literal sections first: every literal tree starts 8-byte aligned in
+  // either table (LZGPU_LIT_2RT reads its cells four at a time)
+  for (uint32_t k = 0; k < S_NSEC; ++k) {
+    const uint32_t sec = k < 2 ? S_LITP + k : (k - 2 < S_LITP ? k - 2 : k);
     const uint32_t n = sec_cells(sec, lc, lp, pb);
     if ((lds_mask >> sec) & 1u) {
       L.o[sec] = a;
@@ -189,6 +192,28 @@ typedef __attribute__((address_space(1))) uint32_t gu32;
 #ifndef LZGPU_READER16
 #define LZGPU_READER16 1
 #endif
+//   LZGPU_READER_SPLIT the 16-byte refill as two 8-byte loads into the two
+//                      halves' own registers
+#ifndef LZGPU_READER_SPLIT
+#define LZGPU_READER_SPLIT 0
+#endif
+//   LZGPU_LIT_2RT      plain literal tree in two memory round trips (levels
+//                      0-3 from one batch of reads, 4-7 from a second)
+#ifndef LZGPU_LIT_2RT
+#define LZGPU_LIT_2RT 0
+#endif
+//   LZGPU_LIT_UNIFIED  plain and matched literals on one instruction path
+//                      (lz_literal_unified) in the literal batch
+#ifndef LZGPU_LIT_UNIFIED
+#define LZGPU_LIT_UNIFIED 0
+#endif
+//   LZGPU_READER_Q     checkpoint reader (GlobalReaderQ): the literal batch's
+//                      IsMatch + literal decisions normalize without refill
+//                      checks; the window is topped up before IsMatch and
+//                      between the literal tree's two halves
+#ifndef LZGPU_READER_Q
+#define LZGPU_READER_Q 1
+#endif
 #ifndef LZGPU_COPY_V2
 #define LZGPU_COPY_V2 0
 #endif
@@ -244,7 +269,11 @@ struct LzStateT {
   uint32_t tmp_n;
   uint8_t tmp[kLookahead];
 #if LZGPU_PROF
-  uint64_t prof[5];  // cycles: literal batches, match decode, copies + tail, calls, refills
+  // [0..4] cycles: literal batches, match decode, copies + tail, calls, refills;
+  // [5..13] wave-level counts: batch iterations, active / matched-literal lanes
+  // per iteration, iterations with both literal kinds, match-path entries and
+  // their lanes, live lanes per iteration, literals, matches (lane-level)
+  uint64_t prof[18];  // [14..16]: IsMatch, literal, batch tail cycles per literal
 #endif
 };
 
@@ -352,6 +381,12 @@ struct GlobalReader16 {
 #ifdef LZGPU_HOST_EMU
     nlo = uint64_t(a[0]) | (uint64_t(a[1]) << 32);
     nhi = uint64_t(a[2]) | (uint64_t(a[3]) << 32);
+#elif LZGPU_READER_SPLIT
+    // two 8-byte loads straight into nlo / nhi: no 16-byte register tuple
+    // that has to be copied (and therefore waited for) at the refill
+    typedef __attribute__((address_space(1))) const uint64_t gu64c;
+    nlo = ((gu64c*)a)[0];
+    nhi = ((gu64c*)a)[1];
 #else
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
     const u32x4 v = *(const __attribute__((address_space(1))) u32x4*)a;
@@ -421,11 +456,132 @@ struct GlobalReader16 {
   }
 };
 
-#if LZGPU_READER16
-typedef GlobalReader16 BulkReader;
-#else
-typedef GlobalReader BulkReader;
+// Checkpoint reader: NORMALIZE takes its byte from `win` without a refill
+// check (take_u), and the decoder tops the window up at checkpoints where a
+// bounded number of decisions follows (topup: nb <= 4 -> nb += 4, so >= 5
+// bytes for the next <= 5 decisions).  The window is fed a 4-byte word at a
+// time from the current 16-byte block (blo:bhi, bw words left); the next block
+// is already loaded (nlo:nhi) when the current one runs out, and only then is
+// the one after requested.  Same contract as GlobalReader16 otherwise:
+// used() = bytes consumed, never loads a block wholly outside [p, p+avail).
+struct GlobalReaderQ {
+  const gu32* wp;  // next 16-byte block to prefetch (as words)
+  uint32_t left;   // blocks with a valid byte still to prefetch
+  uint32_t nb;     // valid bytes in win (0..8)
+  uint32_t bw;     // words left in blo:bhi (1..4)
+  uint64_t win;
+  uint64_t blo, bhi, nlo, nhi;
+  uint32_t taken;  // bytes moved into win since init (consumed = taken - nb)
+#if LZGPU_PROF && !defined(LZGPU_HOST_EMU)
+  uint64_t prof = 0;  // (refills are not timed separately in this reader)
 #endif
+
+  __device__ __forceinline__ void fetch() {
+    const gu32* a = left ? wp : (const gu32*)g_lz_zero_word;
+#ifdef LZGPU_HOST_EMU
+    nlo = uint64_t(a[0]) | (uint64_t(a[1]) << 32);
+    nhi = uint64_t(a[2]) | (uint64_t(a[3]) << 32);
+#else
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 v = *(const __attribute__((address_space(1))) u32x4*)a;
+    nlo = uint64_t(v.x) | (uint64_t(v.y) << 32);
+    nhi = uint64_t(v.z) | (uint64_t(v.w) << 32);
+#endif
+    wp += left ? 4 : 0;
+    left -= left ? 1u : 0u;
+  }
+  // drop the block's lowest word
+  __device__ __forceinline__ void pop_word() {
+    blo = (blo >> 32) | (bhi << 32);
+    bhi >>= 32;
+    if (--bw == 0) {
+      blo = nlo;
+      bhi = nhi;
+      bw = 4;
+      fetch();
+    }
+  }
+  __device__ __forceinline__ void init(const gbyte* p, uint64_t avail) {
+    const uintptr_t a = (uintptr_t)p;
+    const uintptr_t a0 = a & ~uintptr_t(15);
+    const uint64_t blocks = avail ? (((a + avail + 15) & ~uintptr_t(15)) - a0) >> 4 : 0;
+    wp = (const gu32*)a0;
+    left = blocks > 0xFFFFFFF0ull ? 0xFFFFFFF0u : uint32_t(blocks);
+    fetch();
+    blo = nlo;
+    bhi = nhi;
+    bw = 4;
+    fetch();
+    // skip the words of the first block before p, then the bytes of p's word
+    for (uint32_t w = uint32_t(a & 15) >> 2; w != 0; --w) pop_word();
+    const uint32_t sk = uint32_t(a & 3);
+    win = uint64_t(uint32_t(blo)) >> (8 * sk);
+    nb = avail ? 4 - sk : 0;
+    pop_word();
+    taken = nb;
+  }
+  __device__ __forceinline__ uint32_t used() const { return taken - nb; }
+  __device__ __forceinline__ void topup() {
+    if (nb <= 4) {
+      win |= uint64_t(uint32_t(blo)) << (8 * nb);
+      nb += 4;
+      taken += 4;
+      pop_word();
+    }
+  }
+  __device__ __forceinline__ uint32_t peek() const { return uint32_t(win) & 0xFFu; }
+  // next byte, no refill check (a checkpoint guaranteed nb > 0)
+  __device__ __forceinline__ uint32_t take_u() {
+    const uint32_t b = uint32_t(win) & 0xFFu;
+    win >>= 8;
+    --nb;
+    return b;
+  }
+  __device__ __forceinline__ uint32_t next() {
+    if (nb == 0) topup();
+    return take_u();
+  }
+  __device__ __forceinline__ void advance(bool n) {
+    if (n) {
+      win >>= 8;
+      --nb;
+      if (nb == 0) topup();
+    }
+  }
+};
+
+#if LZGPU_READER16
+typedef GlobalReader16 PlainReader;
+#else
+typedef GlobalReader PlainReader;
+#endif
+// Reader of the bulk pass per placement: the checkpoint reader for the
+// throughput placement (many lanes per wave: a refill check in every
+// NORMALIZE fires in some lane almost every decision), the per-byte-checked
+// one elsewhere (one lane per wave: config 2 5.8 vs 5.2 GB/s).
+template <uint32_t M>
+struct BulkReaderFor {
+  typedef PlainReader type;
+};
+#if LZGPU_READER_Q
+template <>
+struct BulkReaderFor<LZGPU_LDS_MASK> {
+  typedef GlobalReaderQ type;
+};
+#endif
+
+// checkpoint hooks for readers without them: every NORMALIZE checks
+template <class Rd>
+__device__ __forceinline__ void rd_topup(Rd& rd) {
+  if constexpr (__is_same(Rd, GlobalReaderQ)) rd.topup();
+}
+template <class Rd>
+__device__ __forceinline__ uint32_t rd_take_u(Rd& rd) {
+  if constexpr (__is_same(Rd, GlobalReaderQ))
+    return rd.take_u();
+  else
+    return rd.next();
+}
 
 // Reader over a lane-private byte array (the tempBuf path).
 struct LocalReader {
@@ -444,10 +600,19 @@ struct LocalReader {
 #ifdef LZGPU_HOST_EMU
 __device__ __forceinline__ const uint32_t* wide(const uint16_t* p) { return (const uint32_t*)p; }
 __device__ __forceinline__ const uint32_t* wide(uint16_t* p) { return (const uint32_t*)p; }
+__device__ __forceinline__ uint64_t ld64(const uint16_t* p) {
+  return uint64_t(p[0]) | (uint64_t(p[1]) << 16) | (uint64_t(p[2]) << 32) |
+         (uint64_t(p[3]) << 48);
+}
 #else
 typedef __attribute__((address_space(3))) uint32_t lds_u32;
+typedef __attribute__((address_space(3))) uint64_t lds_u64;
+typedef __attribute__((address_space(1))) uint64_t gu64;
 __device__ __forceinline__ const lds_u32* wide(lds_u16* p) { return (const lds_u32*)p; }
 __device__ __forceinline__ const gu32* wide(gu16* p) { return (const gu32*)p; }
+// four cells (8-byte aligned) in one read
+__device__ __forceinline__ uint64_t ld64(lds_u16* p) { return *(const lds_u64*)p; }
+__device__ __forceinline__ uint64_t ld64(gu16* p) { return *(const gu64*)p; }
 #endif
 
 template <class Rd>
@@ -468,6 +633,54 @@ struct Rc {
       code = (code << 8) | rd->next();
     }
 #endif
+  }
+  // NORMALIZE after a reader checkpoint: the byte is known to be in the window
+  __device__ __forceinline__ void norm_u() {
+    if (range < kTop) {
+      range <<= 8;
+      code = (code << 8) | rd_take_u(*rd);
+    }
+  }
+  // decision with norm_u (the shared-form update of LZGPU_BIT_MASK 2)
+  template <class P>
+  __device__ __forceinline__ uint32_t bit_u(P prob) {
+#if LZGPU_BIT_MASK == 2 && !LZGPU_NORM_BRANCHLESS
+    const uint32_t p = *prob;
+    norm_u();
+    const uint32_t bound = (range >> 11) * p;
+    const bool b = code >= bound;
+    const int32_t m = b ? 0 : int32_t(kProbOne - 31);
+    *prob = uint16_t(int32_t(p) - ((int32_t(p) - m) >> 5));
+    range = b ? range - bound : bound;
+    code = b ? code - bound : code;
+    return b ? 1u : 0u;
+#else
+    return bit(prob);
+#endif
+  }
+  // decision on a preloaded value p with norm_u
+  template <class P>
+  __device__ __forceinline__ uint32_t bit_vu(uint32_t p, P prob) {
+#if LZGPU_BIT_MASK == 2 && !LZGPU_NORM_BRANCHLESS
+    norm_u();
+    const uint32_t bound = (range >> 11) * p;
+    const bool b = code >= bound;
+    const int32_t m = b ? 0 : int32_t(kProbOne - 31);
+    *prob = uint16_t(int32_t(p) - ((int32_t(p) - m) >> 5));
+    range = b ? range - bound : bound;
+    code = b ? code - bound : code;
+    return b ? 1u : 0u;
+#else
+    return bit_v(p, prob);
+#endif
+  }
+  // BITS levels of an MSB-first tree from node m (no refill checks: at most
+  // 5 levels after a checkpoint); returns the node reached
+  template <int BITS, class P>
+  __device__ __forceinline__ uint32_t tree_u(P probs, uint32_t m) {
+#pragma unroll
+    for (int k = 0; k < BITS; ++k) m = (m << 1) | bit_u(probs + m);
+    return m;
   }
   // one adaptive decision on *prob (any address space), IF_BIT_0/UPDATE_0/1
   template <class P>
@@ -528,6 +741,18 @@ struct Rc {
     *prob = uint16_t(p - (p >> 5));
     return 1;
   }
+  // decision on probability value p; the updated value goes to np (the
+  // caller stores it) -- IF_BIT_0 / UPDATE_0 / UPDATE_1 in the shared form
+  __device__ __forceinline__ uint32_t bit_np(uint32_t p, uint32_t& np) {
+    norm();
+    const uint32_t bound = (range >> 11) * p;
+    const bool b = code >= bound;
+    const int32_t m = b ? 0 : int32_t(kProbOne - 31);
+    np = uint32_t(int32_t(p) - ((int32_t(p) - m) >> 5)) & 0xFFFFu;
+    range = b ? range - bound : bound;
+    code = b ? code - bound : code;
+    return b ? 1u : 0u;
+  }
   // MSB-first bit tree of BITS levels (TREE_DECODE); returns [0, 1 << BITS)
   template <int BITS, class P>
   __device__ __forceinline__ uint32_t tree(P probs) {
@@ -566,6 +791,42 @@ struct Rc {
     const uint32_t p2 = b0 ? (b1 ? c23 : c22) : (b1 ? c21 : c20);
     const uint32_t b2 = bit_v(p2, probs + m);
     return 2 * m + b2;
+  }
+  // 8-level MSB-first tree (a literal, TREE_DECODE of LzmaDec.c:174) in two
+  // memory round trips instead of eight: cells 0..15 (levels 0-3) in four
+  // 8-byte reads, then the 15 cells of the 4-level subtree under the node
+  // reached (m, 2m.., 4m.., 8m..) in one batch; each level's cell is picked
+  // from registers with selects.  probs must be 8-byte aligned.  Returns the
+  // node 0x100 | byte.
+  template <class P>
+  __device__ __forceinline__ uint32_t tree8_2rt(P probs) {
+    const uint64_t q0 = ld64(probs), q1 = ld64(probs + 4), q2 = ld64(probs + 8),
+                   q3 = ld64(probs + 12);
+    auto half = [](uint64_t q, uint32_t j) {  // cell j (0..3) of a 4-cell word
+      return uint32_t(q >> (16 * j)) & 0xFFFFu;
+    };
+    uint32_t b = bit_v(half(q0, 1), probs + 1);
+    uint32_t m = 2 + b;                                   // 2..3
+    b = bit_v(half(q0, m), probs + m);
+    m = 2 * m + b;                                        // 4..7
+    b = bit_v(half(q1, m - 4), probs + m);
+    m = 2 * m + b;                                        // 8..15
+    b = bit_v(half((m & 4) ? q3 : q2, m & 3), probs + m);
+    m = 2 * m + b;                                        // 16..31
+    const uint32_t c0 = probs[m];
+    const uint32_t c1 = *wide(probs + 2 * m);
+    const uint64_t c2 = ld64(probs + 4 * m), c3a = ld64(probs + 8 * m),
+                   c3b = ld64(probs + 8 * m + 4);
+    const uint32_t r = m;
+    b = bit_v(c0, probs + m);
+    m = 2 * m + b;                                        // 2r + j, j < 2
+    b = bit_v((c1 >> (16 * (m - 2 * r))) & 0xFFFFu, probs + m);
+    m = 2 * m + b;                                        // 4r + j, j < 4
+    b = bit_v(half(c2, m - 4 * r), probs + m);
+    m = 2 * m + b;                                        // 8r + j, j < 8
+    const uint32_t j = m - 8 * r;
+    b = bit_v(half((j & 4) ? c3b : c3a, j & 3), probs + m);
+    return 2 * m + b;
   }
   // fixed-probability bit in the reference's exact arithmetic (LzmaDec.c:325-334)
   __device__ __forceinline__ void direct(uint32_t& v) {
@@ -726,7 +987,18 @@ __device__ __forceinline__ void lz_literal(Rc<Rd>& rc, const Tab<M, Lo>& T, uint
   if (full != 0 || total != 0) ctx = ((total & lp_mask) << lc) + (prev >> (8 - lc));
   if (st < 7) {
     st = (st < 4) ? 0 : st - 3;
+#if LZGPU_LIT_2RT
+    sym = rc.tree8_2rt(T.template at<S_LITP>(ctx << 8));
+#elif LZGPU_READER_Q
+    {
+      auto lp = T.template at<S_LITP>(ctx << 8);
+      const uint32_t m = rc.template tree_u<4>(lp, 1);
+      rd_topup(*rc.rd);
+      sym = rc.template tree_u<4>(lp, m);
+    }
+#else
     sym = 0x100u | rc.template tree<8>(T.template at<S_LITP>(ctx << 8));
+#endif
   } else {
 #if LZGPU_MB_PF
     uint32_t mbyte = mb_pf;
@@ -753,10 +1025,18 @@ __device__ __forceinline__ void lz_literal(Rc<Rd>& rc, const Tab<M, Lo>& T, uint
       for (int k = 0; k < 8; ++k) {
         const uint32_t mk = (mb >> (7 - k)) & 1u;
         uint32_t b;
+#if LZGPU_READER_Q
+        if (k == 4) rd_topup(*rc.rd);
+        if (matched)
+          b = rc.bit_vu(pk[k], lm + ((mk << 8) + sym));
+        else
+          b = rc.bit_u(T.template at<S_LITP>((ctx << 8) + sym));
+#else
         if (matched)
           b = rc.bit_v(pk[k], lm + ((mk << 8) + sym));
         else
           b = rc.bit(T.template at<S_LITP>((ctx << 8) + sym));
+#endif
         matched = matched && (b == mk);
         sym = (sym << 1) | b;
       }
@@ -798,6 +1078,56 @@ __device__ __forceinline__ bool lz_any(bool v) {
 #else
   return __builtin_amdgcn_ballot_w64(v) != 0;
 #endif
+}
+
+// One literal (LzmaDec.c:161-196) with plain and matched literals on ONE
+// instruction path (LZGPU_LIT_UNIFIED; plain tree in LDS, matched cells in
+// global memory).  Lanes of a wave decode plain and matched literals side by
+// side in the same batch iteration; as two code paths the wave would run both
+// nearly every iteration.  Per level: the plain cell is read from LDS by
+// every lane; a lane still on the all-match path uses its preloaded matched
+// cell instead, writes the plain cell back unchanged and stores the update to
+// its matched cell (a predicated store, no else-path).  Once a decoded bit
+// differs from the match byte's the lane continues in the plain tree, as the
+// reference's offs = 0 does; a plain literal is that walk from the start.
+template <uint32_t M, class Lo, class Rd>
+__device__ __forceinline__ void lz_literal_unified(Rc<Rd>& rc, const Tab<M, Lo>& T, uint32_t& st,
+                                                   uint32_t& prev, uint32_t& total,
+                                                   uint32_t full, uint32_t lc, uint32_t lp_mask,
+                                                   gbyte* dic, uint64_t& pos, uint32_t mbyte) {
+  uint32_t ctx = 0;
+  if (full != 0 || total != 0) ctx = ((total & lp_mask) << lc) + (prev >> (8 - lc));
+  const bool mlit = st >= 7;
+  st = (st < 4) ? 0 : ((st < 10) ? st - 3 : st - 6);
+  const uint32_t mb = mlit ? (mbyte & 0xFFu) : 0u;
+  auto lp = T.template at<S_LITP>(ctx << 8);
+  auto lm = T.template at<S_LITM>(ctx << 9);
+  uint32_t pk[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) pk[k] = 0;
+  if (lz_any(mlit)) {
+    if (mlit) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        pk[k] = lm[(((mb >> (7 - k)) & 1u) << 8) + ((1u << k) | (mb >> (8 - k)))];
+    }
+  }
+  bool matching = mlit;
+  uint32_t sym = 1;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const uint32_t mk = (mb >> (7 - k)) & 1u;
+    const uint32_t pl = lp[sym];
+    uint32_t np;
+    const uint32_t b = rc.bit_np(matching ? pk[k] : pl, np);
+    lp[sym] = uint16_t(matching ? pl : np);
+    if (matching) lm[(mk << 8) + sym] = uint16_t(np);
+    matching = matching && (b == mk);
+    sym = (sym << 1) | b;
+  }
+  prev = sym & 0xFFu;
+  dic[pos++] = uint8_t(prev);
+  total++;
 }
 
 // Decode symbols until pos reaches `limit` or the reader index reaches
@@ -850,30 +1180,75 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
     bool lit_on = !is_match;
 #pragma unroll 1
     for (int lit = 0; lit < LZGPU_LIT_BATCH; ++lit) {
+#if LZGPU_PROF && !defined(LZGPU_HOST_EMU)
+      {
+        const uint64_t on = __builtin_amdgcn_ballot_w64(lit_on);
+        const uint64_t ml = __builtin_amdgcn_ballot_w64(lit_on && st >= 7);
+        s.prof[5] += 1;
+        s.prof[6] += __builtin_popcountll(on);
+        s.prof[7] += __builtin_popcountll(ml);
+        s.prof[8] += (ml != 0 && ml != on) ? 1 : 0;
+        s.prof[11] += __builtin_popcountll(__builtin_amdgcn_ballot_w64(true));
+      }
+#endif
+#if LZGPU_PROF && !defined(LZGPU_HOST_EMU)
+      const uint64_t tA = lz_clock();
+      uint64_t tB = 0, tC = 0;
+      bool did_lit = false;
+#endif
       if (lit_on) {
         ps = total & pb_mask;
-        if (rc.bit(T.template at<S_MATCH>((st << pb) + ps))) {
+#if LZGPU_READER_Q
+        rd_topup(rd);
+        const uint32_t ism = rc.bit_u(T.template at<S_MATCH>((st << pb) + ps));
+#else
+        const uint32_t ism = rc.bit(T.template at<S_MATCH>((st << pb) + ps));
+#endif
+        if (ism) {
           is_match = true;
           lit_on = false;
         } else {
+#if LZGPU_PROF && !defined(LZGPU_HOST_EMU)
+          tB = lz_clock();
+          did_lit = true;
+#endif
+#if LZGPU_LIT_UNIFIED && LZGPU_MB_PF
+          if constexpr (((M >> S_LITP) & 1u) != 0u && ((M >> S_LITM) & 1u) == 0u)
+            lz_literal_unified<M>(rc, T, st, prev, total, full, lc, lp_mask, dic, pos, mb_pf);
+          else
+#endif
           lz_literal<M>(rc, T, st, prev, total, full, lc, lp_mask, dic, pos, cap, r0
 #if LZGPU_MB_PF
                         , mb_pf
 #endif
           );
+#if LZGPU_PROF && !defined(LZGPU_HOST_EMU)
+          tC = lz_clock();
+#endif
           if (!(pos < limit && rd.used() < in_limit)) {
             stop = true;
             lit_on = false;
           }
         }
       }
+#if LZGPU_PROF && !defined(LZGPU_HOST_EMU)
+      {
+        const uint64_t tD = lz_clock();
+        if (did_lit) {
+          s.prof[14] += tB - tA;
+          s.prof[15] += tC - tB;
+          s.prof[16] += tD - tC;
+        }
+      }
+#endif
       if (!lz_any(lit_on)) break;
     }
 #else
 #pragma unroll 1
     for (int lit = 0; lit < LZGPU_LIT_BATCH && !is_match; ++lit) {
       ps = total & pb_mask;
-      if (rc.bit(T.template at<S_MATCH>((st << pb) + ps))) {
+      rd_topup(rd);  // checkpoint: IsMatch + the literal tree's first half
+      if (rc.bit_u(T.template at<S_MATCH>((st << pb) + ps))) {
         is_match = true;
         break;
       }
@@ -889,6 +1264,14 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
     }
 #endif
     LZ_PROF_MARK(s, 0, t_prof);
+#if LZGPU_PROF && !defined(LZGPU_HOST_EMU)
+    {
+      const uint64_t mm = __builtin_amdgcn_ballot_w64(is_match && !stop);
+      s.prof[9] += mm ? 1 : 0;
+      s.prof[10] += __builtin_popcountll(mm);
+      s.prof[13] += (is_match && !stop) ? 1 : 0;
+    }
+#endif
     if (stop) break;
     if (!is_match) continue;
     if (!rc.bit(T.template at<S_REP>(st))) {
@@ -1046,7 +1429,8 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
     // which would otherwise diverge from the plain literals of the batch.
     if (pos < limit && rd.used() < in_limit) {
       ps = total & pb_mask;
-      if (rc.bit(T.template at<S_MATCH>((st << pb) + ps))) {
+      rd_topup(rd);  // checkpoint: IsMatch + the literal tree's first half
+      if (rc.bit_u(T.template at<S_MATCH>((st << pb) + ps))) {
         pend_match = true;
       } else {
         lz_literal<M>(rc, T, st, prev, total, full, lc, lp_mask, dic, pos, cap, r0
@@ -1335,7 +1719,7 @@ __device__ __forceinline__ int lz_decode_to_dic(LzStateT<Lo>& s, uint64_t dic_li
         uint64_t lim = avail - kLookahead;
         in_limit = lim > 0xFFFFFFF0ull ? 0xFFFFFFF0u : uint32_t(lim);
       }
-      BulkReader rd;
+      typename BulkReaderFor<M>::type rd;
       rd.init(src, avail);
 #if LZGPU_PROF && !defined(LZGPU_HOST_EMU) && LZGPU_READER16
       const int rr = lz_run_split<M>(s, dic_limit, rd, in_limit);

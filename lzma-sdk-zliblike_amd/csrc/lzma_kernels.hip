@@ -149,11 +149,11 @@ extern "C" int lzgpu_launch_session(LzgpuSession* d_sess, uint32_t n, hipStream_
 #if LZGPU_PROF
 // profiling builds: read (and optionally clear) the region cycle sums
 extern "C" int LzmaGpu_ProfileRead(unsigned long long* out, int reset) {
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(lzgpu::g_lz_prof), 8 * sizeof(unsigned long long)) !=
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(lzgpu::g_lz_prof), 24 * sizeof(unsigned long long)) !=
       hipSuccess)
     return -1;
   if (reset) {
-    unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long z[24] = {};
     if (hipMemcpyToSymbol(HIP_SYMBOL(lzgpu::g_lz_prof), z, sizeof z) != hipSuccess) return -1;
   }
   return 0;

@@ -20,7 +20,7 @@ namespace lzgpu {
 
 #if LZGPU_PROF && !defined(LZGPU_HOST_EMU)
 // per-region cycle sums over lanes (profiling builds only)
-__device__ unsigned long long g_lz_prof[8];
+__device__ unsigned long long g_lz_prof[24];
 #endif
 
 // One batch item with the whole probability table in global memory (the
@@ -108,6 +108,10 @@ __device__ __forceinline__ LzmaGpuResult lane_decode_lds(const LzmaGpuStreamDesc
   r.dest_len = 0;
   r.src_len = 0;
   if (d.kind == LZMA_GPU_KIND_LZMA2) {
+#ifdef LZGPU_HACK_NO2
+ r.res=1; return r;
+#endif
+
     // chunks may switch lc/lp/pb (lc + lp <= 4): the slice holds the widest layout
     if (d.probs_off == LZMA_GPU_NO_WORKSPACE || lzma2_lds_cells(M) > lo_cap) {
       r.res = (d.props[0] > 40) ? kErrUnsupported : kErrMem;
@@ -151,15 +155,16 @@ __device__ __forceinline__ LzmaGpuResult lane_decode_lds(const LzmaGpuStreamDesc
   uint64_t sl = d.src_len;
   int status = kStNone;
 #if LZGPU_PROF && !defined(LZGPU_HOST_EMU)
-  for (int k = 0; k < 5; ++k) s.prof[k] = 0;
+  for (int k = 0; k < 18; ++k) s.prof[k] = 0;
   const uint64_t t0 = lz_clock();
 #endif
   int res = lz_decode_to_dic<false, M>(s, d.dst_cap, (const gbyte*)(src + d.src_off), sl,
                                     d.finish_mode, status);
 #if LZGPU_PROF && !defined(LZGPU_HOST_EMU)
   s.prof[3] = lz_clock() - t0;
-  for (int k = 0; k < 5; ++k) atomicAdd(&g_lz_prof[k], (unsigned long long)s.prof[k]);
-  atomicAdd(&g_lz_prof[7], 1ull);
+  s.prof[12] = s.total;  // literals + match bytes: decoded bytes
+  for (int k = 0; k < 17; ++k) atomicAdd(&g_lz_prof[k], (unsigned long long)s.prof[k]);
+  atomicAdd(&g_lz_prof[23], 1ull);
 #endif
   if (res == kOk && status == kStMoreInput) res = kErrInputEof;
   r.res = res;

@@ -144,5 +144,5 @@ def test_plan_batch_workspace_and_order():
     pb_, _ = L.plan_ex(big)
     cb = pb_.classes[0]
     assert (pb_.n_classes, cb.n, cb.lds_cells_per_lane, cb.lds_mask) == (1, 65536, 316, 0x105)
-    assert (cb.lanes_per_group, cb.groups_per_cu, cb.waves_per_simd) == (16, 16, 4)
+    assert (cb.lanes_per_group, cb.groups_per_cu, cb.waves_per_simd) == (32, 8, 2)
     assert plan.queue_offset % 64 == 0 and plan.workspace_bytes >= plan.queue_offset + 256

@@ -33,6 +33,14 @@ EMU_VARIANTS = {
     "bit_branchy": "-DLZGPU_BIT_MASK=0 -DLZGPU_MLIT_PF=0",
     "tail_lit": "-DLZGPU_TAIL_LIT=1",
     "tail_lit_divergent": "-DLZGPU_TAIL_LIT=1 -DLZGPU_UNIFORM_EXIT=0 -DLZGPU_LIT_BATCH=2",
+    "lit_2rt": "-DLZGPU_LIT_2RT=1",
+    "lit_2rt_latency": "-DLZGPU_LIT_2RT=1 -DLZGPU_LDS_MASK=0x1BF",
+    "lit_2rt_all_global": "-DLZGPU_LIT_2RT=1 -DLZGPU_LDS_MASK=0",
+    "lit_unified": "-DLZGPU_LIT_UNIFIED=1",
+    "lit_unified_latency": "-DLZGPU_LIT_UNIFIED=1 -DLZGPU_LDS_MASK=0x1BF",
+    "reader_q": "-DLZGPU_READER_Q=1",
+    "reader_q_latency": "-DLZGPU_READER_Q=1 -DLZGPU_LDS_MASK=0x1BF",
+    "reader_q_no_mlit_pf": "-DLZGPU_READER_Q=1 -DLZGPU_MLIT_PF=0 -DLZGPU_LIT_BATCH=1",
 }
 
 
