@@ -684,9 +684,10 @@ def main():
         L.lib.LzmaGpu_ProfileRead(buf, 0)
         lanes = max(1, buf[23])
         names = ("literal_batches", "match_decode", "copy_tail", "decode_to_dic_total",
-                 "refills", "batch_iters", "lit_lanes", "mlit_lanes", "mixed_iters",
-                 "match_entries", "match_lanes", "live_lanes", "bytes", "matches",
-                 "cyc_ismatch", "cyc_literal", "cyc_lit_tail")
+                 "refills", "batch_iters|slot_sub3_a", "lit_lanes|slot_sub3_b", "mlit_lanes|n_slot",
+                 "mixed_iters|cyc_rep_bits", "match_entries|cyc_len", "match_lanes|cyc_dist",
+                 "live_lanes|n_dist", "bytes", "matches|cyc_drain",
+                 "cyc_ismatch", "cyc_literal", "cyc_lit_tail", "cyc_iterations")
         prof = {k: buf[i] / lanes for i, k in enumerate(names)}
         prof["other_in_decode_to_dic"] = prof["decode_to_dic_total"] - sum(
             prof[k] for k in names[:3])  # refills overlap the first three regions

@@ -214,8 +214,28 @@ typedef __attribute__((address_space(1))) uint32_t gu32;
 #ifndef LZGPU_READER_Q
 #define LZGPU_READER_Q 1
 #endif
+//   LZGPU_LIT_PF       plain literal tree (checkpoint reader) with the next
+//                      level's cell pair read ahead of each decision
+#ifndef LZGPU_LIT_PF
+#define LZGPU_LIT_PF 0
+#endif
+//   LZGPU_MATCH_FAT    match path with fewer dependent global round trips:
+//                      the whole length coder of a posState in one load batch
+//                      (LenHigh in 3), SpecPos in <= 2, Align in 1
+#ifndef LZGPU_MATCH_FAT
+#define LZGPU_MATCH_FAT 1
+#endif
+//   (applied to every placement but the throughput one, LZGPU_LDS_MASK: with
+//   up to 32 lanes per wave its extra load instructions cost more in the
+//   vector-memory pipeline than the round trips they save -- config 3 28.1 vs
+//   27.6 GB/s, config 5 +1.5 %)
 #ifndef LZGPU_COPY_V2
 #define LZGPU_COPY_V2 0
+#endif
+//   LZGPU_COPY_WIDE    match copies with unaligned 8-byte loads/stores (and a
+//                      register-built pattern when rep0 < 8)
+#ifndef LZGPU_COPY_WIDE
+#define LZGPU_COPY_WIDE 1
 #endif
 //   LZGPU_LIT_BATCH    literals decoded per pass of the symbol loop before a
 //                      lane's match path runs (1 = one symbol per pass)
@@ -465,12 +485,20 @@ struct GlobalReader16 {
 // the one after requested.  Same contract as GlobalReader16 otherwise:
 // used() = bytes consumed, never loads a block wholly outside [p, p+avail).
 struct GlobalReaderQ {
+#ifdef LZGPU_HOST_EMU
+  struct u32x4 { uint32_t x, y, z, w; };
+#else
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+#endif
   const gu32* wp;  // next 16-byte block to prefetch (as words)
   uint32_t left;   // blocks with a valid byte still to prefetch
   uint32_t nb;     // valid bytes in win (0..8)
   uint32_t bw;     // words left in blo:bhi (1..4)
   uint64_t win;
-  uint64_t blo, bhi, nlo, nhi;
+  uint64_t blo, bhi;
+  // the prefetched next block, kept in the load's own register tuple: a copy
+  // to other registers would make the compiler wait for the load right away
+  u32x4 nx;
   uint32_t taken;  // bytes moved into win since init (consumed = taken - nb)
 #if LZGPU_PROF && !defined(LZGPU_HOST_EMU)
   uint64_t prof = 0;  // (refills are not timed separately in this reader)
@@ -479,13 +507,9 @@ struct GlobalReaderQ {
   __device__ __forceinline__ void fetch() {
     const gu32* a = left ? wp : (const gu32*)g_lz_zero_word;
 #ifdef LZGPU_HOST_EMU
-    nlo = uint64_t(a[0]) | (uint64_t(a[1]) << 32);
-    nhi = uint64_t(a[2]) | (uint64_t(a[3]) << 32);
+    nx = u32x4{a[0], a[1], a[2], a[3]};
 #else
-    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-    const u32x4 v = *(const __attribute__((address_space(1))) u32x4*)a;
-    nlo = uint64_t(v.x) | (uint64_t(v.y) << 32);
-    nhi = uint64_t(v.z) | (uint64_t(v.w) << 32);
+    nx = *(const __attribute__((address_space(1))) u32x4*)a;
 #endif
     wp += left ? 4 : 0;
     left -= left ? 1u : 0u;
@@ -495,8 +519,8 @@ struct GlobalReaderQ {
     blo = (blo >> 32) | (bhi << 32);
     bhi >>= 32;
     if (--bw == 0) {
-      blo = nlo;
-      bhi = nhi;
+      blo = uint64_t(nx.x) | (uint64_t(nx.y) << 32);
+      bhi = uint64_t(nx.z) | (uint64_t(nx.w) << 32);
       bw = 4;
       fetch();
     }
@@ -508,8 +532,8 @@ struct GlobalReaderQ {
     wp = (const gu32*)a0;
     left = blocks > 0xFFFFFFF0ull ? 0xFFFFFFF0u : uint32_t(blocks);
     fetch();
-    blo = nlo;
-    bhi = nhi;
+    blo = uint64_t(nx.x) | (uint64_t(nx.y) << 32);
+    bhi = uint64_t(nx.z) | (uint64_t(nx.w) << 32);
     bw = 4;
     fetch();
     // skip the words of the first block before p, then the bytes of p's word
@@ -674,6 +698,25 @@ struct Rc {
     return bit_v(p, prob);
 #endif
   }
+  // The plain literal tree (8 levels from node 1) after an IsMatch
+  // checkpoint, with a second checkpoint before level 4; the next level's
+  // two cells are read (one 32-bit read) while the current decision resolves,
+  // so the tree's chain has no load latency in it.  probs 4-byte aligned.
+  template <class P>
+  __device__ __forceinline__ uint32_t lit8_pf(P probs) {
+    uint32_t m = 1;
+    uint32_t p = probs[1];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      uint32_t pair = 0;
+      if (k < 7) pair = *wide(probs + 2 * m);
+      if (k == 4) rd_topup(*rd);
+      const uint32_t b = bit_vu(p, probs + m);
+      m = (m << 1) | b;
+      if (k < 7) p = b ? (pair >> 16) : (pair & 0xFFFFu);
+    }
+    return m;
+  }
   // BITS levels of an MSB-first tree from node m (no refill checks: at most
   // 5 levels after a checkpoint); returns the node reached
   template <int BITS, class P>
@@ -792,6 +835,63 @@ struct Rc {
     const uint32_t b2 = bit_v(p2, probs + m);
     return 2 * m + b2;
   }
+  // Two levels below `root` (cells root, 2root + {0,1}) from one load batch;
+  // returns 4 * root + (the two bits, MSB first).
+  template <class P>
+  __device__ __forceinline__ uint32_t sub2(P probs, uint32_t root) {
+    const uint32_t c0 = probs[root], c10 = probs[2 * root], c11 = probs[2 * root + 1];
+    const uint32_t b0 = bit_v(c0, probs + root);
+    const uint32_t m = 2 * root + b0;
+    const uint32_t b1 = bit_v(b0 ? c11 : c10, probs + m);
+    return 2 * m + b1;
+  }
+  // Four levels below `root` (15 cells) from one load batch; returns
+  // 16 * root + (the four bits, MSB first).
+  template <class P>
+  __device__ __forceinline__ uint32_t sub4(P probs, uint32_t root) {
+    uint32_t c[15];
+#pragma unroll
+    for (int l = 0, o = 0; l < 4; o += (1 << l), ++l)
+#pragma unroll
+      for (int j = 0; j < (1 << l); ++j) c[o + j] = probs[(root << l) + j];
+    uint32_t m = root, j = 0;  // j = bits decoded so far (the node below root)
+#pragma unroll
+    for (int l = 0, o = 0; l < 4; o += (1 << l), ++l) {
+      uint32_t p = c[o];
+#pragma unroll
+      for (int k = 1; k < (1 << l); ++k) p = (j == uint32_t(k)) ? c[o + k] : p;
+      const uint32_t b = bit_v(p, probs + m);
+      m = 2 * m + b;
+      j = 2 * j + b;
+    }
+    return m;
+  }
+  // Seven cells of a 3-level subtree under `root`, loaded as one batch ahead of
+  // the decisions that need them (dec3).
+  template <class P>
+  __device__ __forceinline__ void load7(P probs, uint32_t root, uint32_t* c) {
+    c[0] = probs[root];
+    c[1] = probs[2 * root];
+    c[2] = probs[2 * root + 1];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) c[3 + k] = probs[4 * root + k];
+  }
+  template <class P>
+  __device__ __forceinline__ uint32_t dec3(P probs, uint32_t root, const uint32_t* c) {
+    const uint32_t b0 = bit_v(c[0], probs + root);
+    uint32_t m = 2 * root + b0;
+    const uint32_t b1 = bit_v(b0 ? c[2] : c[1], probs + m);
+    m = 2 * m + b1;
+    const uint32_t p2 = b0 ? (b1 ? c[6] : c[5]) : (b1 ? c[4] : c[3]);
+    const uint32_t b2 = bit_v(p2, probs + m);
+    return 2 * m + b2;
+  }
+  // 8-level tree in global memory in three load batches (3 + 3 + 2 levels)
+  // instead of eight dependent round trips; returns the node (256..511).
+  template <class P>
+  __device__ __forceinline__ uint32_t tree8_g(P probs) {
+    return sub2(probs, sub3(probs, sub3(probs, 1)));
+  }
   // 8-level MSB-first tree (a literal, TREE_DECODE of LzmaDec.c:174) in two
   // memory round trips instead of eight: cells 0..15 (levels 0-3) in four
   // 8-byte reads, then the 15 cells of the 4-level subtree under the node
@@ -854,9 +954,106 @@ __device__ __forceinline__ void lz_store_upto8(gbyte* d, uint64_t v, uint32_t re
 }
 #endif
 
+#if LZGPU_COPY_WIDE
+// Unaligned 8-byte global access (gfx950 runs global memory in unaligned
+// mode: one dwordx2 per 8 bytes instead of eight byte instructions -- the
+// vector-memory pipeline, not bandwidth, is what a lane's byte traffic costs).
+#ifdef LZGPU_HOST_EMU
+__device__ __forceinline__ uint64_t ldu64(const gbyte* p) {
+  uint64_t v;
+  __builtin_memcpy(&v, p, 8);
+  return v;
+}
+__device__ __forceinline__ void stu64(gbyte* p, uint64_t v) { __builtin_memcpy(p, &v, 8); }
+__device__ __forceinline__ void stu32(gbyte* p, uint32_t v) { __builtin_memcpy(p, &v, 4); }
+__device__ __forceinline__ void stu16(gbyte* p, uint32_t v) {
+  const uint16_t h = uint16_t(v);
+  __builtin_memcpy(p, &h, 2);
+}
+#else
+typedef uint64_t lz_u64a1 __attribute__((aligned(1)));
+typedef uint32_t lz_u32a1 __attribute__((aligned(1)));
+typedef uint16_t lz_u16a1 __attribute__((aligned(1)));
+__device__ __forceinline__ uint64_t ldu64(const gbyte* p) {
+  return *(const __attribute__((address_space(1))) lz_u64a1*)p;
+}
+__device__ __forceinline__ void stu64(gbyte* p, uint64_t v) {
+  *(__attribute__((address_space(1))) lz_u64a1*)p = v;
+}
+__device__ __forceinline__ void stu32(gbyte* p, uint32_t v) {
+  *(__attribute__((address_space(1))) lz_u32a1*)p = v;
+}
+__device__ __forceinline__ void stu16(gbyte* p, uint32_t v) {
+  *(__attribute__((address_space(1))) lz_u16a1*)p = uint16_t(v);
+}
+#endif
+// the low rem (1..7) bytes of v to d: at most three stores
+__device__ __forceinline__ void stu_tail(gbyte* d, uint64_t v, uint32_t rem) {
+  if (rem & 4) {
+    stu32(d, uint32_t(v));
+    v >>= 32;
+    d += 4;
+  }
+  if (rem & 2) {
+    stu16(d, uint32_t(v));
+    v >>= 16;
+    d += 2;
+  }
+  if (rem & 1) *d = uint8_t(v);
+}
+#endif
+
 __device__ __forceinline__ uint32_t lz_copy(gbyte* dic, uint64_t pos, uint64_t from, uint32_t n,
                                             uint32_t dist, uint64_t cap) {
   uint32_t last = 0;
+#if LZGPU_COPY_WIDE
+  if (from + n <= cap && from < pos) {
+    // source span does not wrap (always so for a flat LzmaDecode window)
+    gbyte* d = dic + pos;
+    const gbyte* src = dic + from;
+    uint64_t v;
+    uint32_t i = 0;
+    if (dist >= 8) {
+      // src[i..i+8) lies below d + i: written before this step reads it
+      for (; i + 8 <= n; i += 8) {
+        v = ldu64(src + i);
+        stu64(d + i, v);
+      }
+      if (i < n) {
+        v = ldu64(src + i);
+        stu_tail(d + i, v, n - i);
+        return uint32_t(v >> (8 * (n - i - 1))) & 0xFFu;
+      }
+      return uint32_t(v >> 56);
+    }
+    // dist < 8: the output is src[0..dist) repeated; 8 bytes of it in v
+    // (the 8-byte read stays inside the window: src + 8 <= d + 7 < cap
+    // unless the match ends within 7 bytes of it)
+    if (from + 8 <= cap) {
+      v = ldu64(src);
+      v &= ~0ull >> (64 - 8 * dist);
+    } else {
+      v = 0;
+      for (uint32_t k = 0; k < dist; ++k) v |= uint64_t(src[k]) << (8 * k);
+    }
+    v |= v << (8 * dist);
+    if (dist < 4) v |= v << (16 * dist);
+    if (dist < 2) v |= v << 32;
+    const uint32_t t = 8u % dist;  // phase advance per 8 bytes
+    for (;; i += 8) {
+      const uint32_t rem = n - i;
+      if (rem <= 8) {
+        if (rem == 8)
+          stu64(d + i, v);
+        else
+          stu_tail(d + i, v, rem);
+        return uint32_t(v >> (8 * (rem - 1))) & 0xFFu;
+      }
+      stu64(d + i, v);
+      v = (v >> (8 * t)) | (v << (8 * (dist - t)));
+    }
+  }
+#endif
 #if LZGPU_COPY_V2
   if (from + n <= cap && from < pos) {
     // source span [from, from+n) does not wrap; from < pos always holds here
@@ -992,9 +1189,13 @@ __device__ __forceinline__ void lz_literal(Rc<Rd>& rc, const Tab<M, Lo>& T, uint
 #elif LZGPU_READER_Q
     {
       auto lp = T.template at<S_LITP>(ctx << 8);
+#if LZGPU_LIT_PF
+      sym = rc.lit8_pf(lp);
+#else
       const uint32_t m = rc.template tree_u<4>(lp, 1);
       rd_topup(*rc.rd);
       sym = rc.template tree_u<4>(lp, m);
+#endif
     }
 #else
     sym = 0x100u | rc.template tree<8>(T.template at<S_LITP>(ctx << 8));
@@ -1181,6 +1382,9 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
 #pragma unroll 1
     for (int lit = 0; lit < LZGPU_LIT_BATCH; ++lit) {
 #if LZGPU_PROF && !defined(LZGPU_HOST_EMU)
+      const uint64_t t_it = lz_clock();
+#endif
+#if LZGPU_PROF >= 2 && !defined(LZGPU_HOST_EMU)
       {
         const uint64_t on = __builtin_amdgcn_ballot_w64(lit_on);
         const uint64_t ml = __builtin_amdgcn_ballot_w64(lit_on && st >= 7);
@@ -1240,8 +1444,14 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
           s.prof[16] += tD - tC;
         }
       }
-#endif
+      {
+        const bool more = lz_any(lit_on);
+        s.prof[17] += lz_clock() - t_it;  // the whole iteration, every live lane
+        if (!more) break;
+      }
+#else
       if (!lz_any(lit_on)) break;
+#endif
     }
 #else
 #pragma unroll 1
@@ -1264,7 +1474,7 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
     }
 #endif
     LZ_PROF_MARK(s, 0, t_prof);
-#if LZGPU_PROF && !defined(LZGPU_HOST_EMU)
+#if LZGPU_PROF >= 2 && !defined(LZGPU_HOST_EMU)
     {
       const uint64_t mm = __builtin_amdgcn_ballot_w64(is_match && !stop);
       s.prof[9] += mm ? 1 : 0;
@@ -1274,6 +1484,17 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
 #endif
     if (stop) break;
     if (!is_match) continue;
+#if LZGPU_PROF == 1 && !defined(LZGPU_HOST_EMU)
+#if LZGPU_PROF_DRAIN
+    {
+      // how long the outstanding vector-memory operations take to drain here
+      const uint64_t td = lz_clock();
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+      s.prof[13] += lz_clock() - td;
+    }
+#endif
+    const uint64_t tm0 = lz_clock();
+#endif
     if (!rc.bit(T.template at<S_REP>(st))) {
       st += 12;
       lcoder_is_rep = 0;
@@ -1309,6 +1530,10 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
       st = (st < 7) ? 8 : 11;
       lcoder_is_rep = 1;
     }
+#if LZGPU_PROF == 1 && !defined(LZGPU_HOST_EMU)
+    const uint64_t tm1 = lz_clock();
+    s.prof[8] += tm1 - tm0;
+#endif
     {
       // length coder of this match kind (LzmaDec.c:261-292)
       const uint32_t lsec_o = lcoder_is_rep ? T.L.o[S_REPLEN] : T.L.o[S_LEN];
@@ -1320,6 +1545,22 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
       if constexpr (!len_lds && LZGPU_TREE_GPF) {
         // global length coder: the choice bits and the low tree load together,
         // the mid tree only behind choice = 1
+        if constexpr (LZGPU_MATCH_FAT && M != LZGPU_LDS_MASK) {
+        // choice, choice2 and both 3-level trees of this posState in ONE load
+        // batch; only lengths >= 18 go back to memory (LenHigh, 3 batches)
+        auto lo_t = lbase + 2 + (ps << 3);
+        auto mid_t = lbase + 2 + (8u << pb) + (ps << 3);
+        const uint32_t ch = lbase[0], ch2 = lbase[1];
+        uint32_t clo[7], cmid[7];
+        rc.load7(lo_t, 1, clo);
+        rc.load7(mid_t, 1, cmid);
+        if (!rc.bit_v(ch, lbase))
+          len = rc.dec3(lo_t, 1, clo) - 8;
+        else if (!rc.bit_v(ch2, lbase + 1))
+          len = rc.dec3(mid_t, 1, cmid);
+        else
+          len = 16 + rc.tree8_g(T.template at<S_LENHI>(lcoder_is_rep << 8)) - 256;
+        } else {
         const uint32_t ch = lbase[0];
         auto lo_t = lbase + 2 + (ps << 3);
         if (!rc.bit_v(ch, lbase))
@@ -1328,6 +1569,7 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
           len = 8 + rc.sub3(lbase + 2 + (8u << pb) + (ps << 3), 1) - 8;
         else
           len = 16 + rc.template tree<8>(T.template at<S_LENHI>(lcoder_is_rep << 8));
+        }
       } else {
         if (!rc.bit(lbase))
           len = rc.template tree<3>(lbase + 2 + (ps << 3));
@@ -1338,12 +1580,27 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
       }
     }
 
+#if LZGPU_PROF == 1 && !defined(LZGPU_HOST_EMU)
+    const uint64_t tm2 = lz_clock();
+    s.prof[9] += tm2 - tm1;
+#endif
     if (st >= 12) {
       const uint32_t lstate = len < 4 ? len : 3;
       uint32_t dist;
       if constexpr (((M >> S_SLOT) & 1u) == 0u && LZGPU_TREE_GPF) {
         auto sl_t = T.template at<S_SLOT>(lstate << 6);
+#if LZGPU_PROF == 1 && !defined(LZGPU_HOST_EMU)
+        // one global round trip + 3 decisions, timed (profiling builds)
+        const uint64_t t0 = lz_clock();
+        const uint32_t n1 = rc.sub3(sl_t, 1);
+        const uint64_t t1 = lz_clock();
+        dist = rc.sub3(sl_t, n1) - 64;
+        s.prof[5] += t1 - t0;
+        s.prof[6] += lz_clock() - t1;
+        s.prof[7] += 1;
+#else
         dist = rc.sub3(sl_t, rc.sub3(sl_t, 1)) - 64;
+#endif
       } else {
         dist = rc.template tree<6>(T.template at<S_SLOT>(lstate << 6));
       }
@@ -1363,6 +1620,12 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
               mask = 8;
               nbits -= 3;
             }
+            if constexpr (LZGPU_MATCH_FAT && M != LZGPU_LDS_MASK) if (nbits == 2) {
+              // the last two bits in one batch as well
+              const uint32_t n2 = rc.sub2(T.template at<S_SPEC>(sp), node);
+              dist |= (((n2 >> 1) & 1u) ? mask : 0u) | ((n2 & 1u) ? (mask << 1) : 0u);
+              nbits = 0;
+            }
           }
           while (nbits != 0) {
             uint32_t b = rc.bit(T.template at<S_SPEC>(sp + node));
@@ -1377,10 +1640,17 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
           dist <<= 4;
           uint32_t node = 1;
           if constexpr (((M >> S_ALIGN) & 1u) == 0u && LZGPU_TREE_GPF) {
-            node = rc.sub3(T.template at<S_ALIGN>(0), 1);
-            dist |= ((node >> 2) & 1u) | (((node >> 1) & 1u) << 1) | ((node & 1u) << 2);
-            const uint32_t b = rc.bit(T.template at<S_ALIGN>(node));
-            dist |= b << 3;
+            if constexpr (LZGPU_MATCH_FAT && M != LZGPU_LDS_MASK) {
+              // all four reverse bits from one batch of the 15 cells
+              node = rc.sub4(T.template at<S_ALIGN>(0), 1);
+              dist |= ((node >> 3) & 1u) | (((node >> 2) & 1u) << 1) |
+                      (((node >> 1) & 1u) << 2) | ((node & 1u) << 3);
+            } else {
+              node = rc.sub3(T.template at<S_ALIGN>(0), 1);
+              dist |= ((node >> 2) & 1u) | (((node >> 1) & 1u) << 1) | ((node & 1u) << 2);
+              const uint32_t b = rc.bit(T.template at<S_ALIGN>(node));
+              dist |= b << 3;
+            }
           } else {
 #pragma unroll
             for (uint32_t k = 0; k < 4; ++k) {
@@ -1406,6 +1676,10 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
         return kErrData;
       }
       st = (st < 19) ? 7 : 10;
+#if LZGPU_PROF == 1 && !defined(LZGPU_HOST_EMU)
+      s.prof[10] += lz_clock() - tm2;
+      s.prof[11] += 1;
+#endif
     }
     len += 2;
     LZ_PROF_MARK(s, 1, t_prof);

@@ -163,7 +163,7 @@ __device__ __forceinline__ LzmaGpuResult lane_decode_lds(const LzmaGpuStreamDesc
 #if LZGPU_PROF && !defined(LZGPU_HOST_EMU)
   s.prof[3] = lz_clock() - t0;
   s.prof[12] = s.total;  // literals + match bytes: decoded bytes
-  for (int k = 0; k < 17; ++k) atomicAdd(&g_lz_prof[k], (unsigned long long)s.prof[k]);
+  for (int k = 0; k < 18; ++k) atomicAdd(&g_lz_prof[k], (unsigned long long)s.prof[k]);
   atomicAdd(&g_lz_prof[23], 1ull);
 #endif
   if (res == kOk && status == kStMoreInput) res = kErrInputEof;

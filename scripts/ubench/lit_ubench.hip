@@ -31,7 +31,37 @@ __global__ void __launch_bounds__(64, 4) lit_kernel(const uint8_t* src, uint32_t
   for (uint32_t i = 0; i < n_lit; ++i) {
     uint32_t sym;
     if constexpr (V == 0 || V == 1) sym = rc.template tree<8>(lo);
-    if constexpr (V >= 2) {
+    if constexpr (V >= 6) {
+      // children-pair prefetch: the next level's two cells are read while
+      // the current decision resolves (lo must be 4-byte aligned)
+      uint32_t m = 1;
+      uint32_t p = lo[1];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        uint32_t pair = 0;
+        if (k < 7) pair = *wide(lo + 2 * m);
+        if constexpr (V == 6) {
+          const bool n = range < kTop;
+          range = n ? range << 8 : range;
+          code = n ? code << 8 : code;
+        } else {
+          if (range < kTop) {
+            range <<= 8;
+            code = (code << 8) | uint32_t(win & 0xFF);
+            win = (win >> 8) | (win << 56);
+          }
+        }
+        const uint32_t bound = (range >> 11) * p;
+        const bool b = code >= bound;
+        const int32_t mm = b ? 0 : int32_t(kProbOne - 31);
+        lo[m] = uint16_t(int32_t(p) - ((int32_t(p) - mm) >> 5));
+        range = b ? range - bound : bound;
+        code = b ? code - bound : code;
+        m = (m << 1) | (b ? 1u : 0u);
+        if (k < 7) p = b ? (pair >> 16) : (pair & 0xFFFFu);
+      }
+      sym = m;
+    } else if constexpr (V >= 2) {
       uint32_t m = 1;
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
@@ -110,11 +140,14 @@ int main(int argc, char** argv) {
       }
     }
   };
-  const int shapes[][2] = {{16, 16}, {32, 8}, {64, 4}, {16, 4}, {64, 8}, {64, 16}, {32, 16}};
+  const int shapes[][2] = {{32, 8}, {16, 16}, {32, 4}};
   for (auto& sh : shapes) {
     run(lit_kernel<1>, "tree<8> (product code)", sh[0], sh[1]);
     run(lit_kernel<2>, "norm zero-byte branch-free", sh[0], sh[1]);
     run(lit_kernel<4>, "norm win64 branchy", sh[0], sh[1]);
+    run(lit_kernel<5>, "norm win32 branch-free", sh[0], sh[1]);
+    run(lit_kernel<6>, "zero-byte + pair prefetch", sh[0], sh[1]);
+    run(lit_kernel<7>, "win64 branchy + pair prefetch", sh[0], sh[1]);
   }
   return 0;
 }

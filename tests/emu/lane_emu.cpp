@@ -28,7 +28,12 @@ void emu_decode_batch_lds(const LzmaGpuStreamDesc* descs, size_t n, const uint8_
   uint16_t* slab = (uint16_t*)malloc(size_t(stride) * 2 + 16);
   for (size_t i = 0; i < n; ++i) {
     memset(slab, 0xA5, size_t(stride) * 2);  // LDS is not zeroed between workgroups
+#ifdef EMU_LAT_MASK
+    // the latency-placement instantiation (the kernels' second LDS variant)
+    results[i] = lane_decode_lds<LZGPU_LDS_MASK_LAT>(descs[i], src, dst, ws, slab, stride);
+#else
     results[i] = lane_decode_lds(descs[i], src, dst, ws, slab, stride);
+#endif
   }
   free(slab);
 }

@@ -41,6 +41,12 @@ EMU_VARIANTS = {
     "reader_q": "-DLZGPU_READER_Q=1",
     "reader_q_latency": "-DLZGPU_READER_Q=1 -DLZGPU_LDS_MASK=0x1BF",
     "reader_q_no_mlit_pf": "-DLZGPU_READER_Q=1 -DLZGPU_MLIT_PF=0 -DLZGPU_LIT_BATCH=1",
+    "lit_pf": "-DLZGPU_LIT_PF=1",
+    "match_thin": "-DLZGPU_MATCH_FAT=0",
+    "match_fat_global_len": "-DLZGPU_LDS_MASK_LAT=0x105 -DLZGPU_LDS_MASK=0x107 -DEMU_LAT_MASK",
+    "latency_instantiation": "-DEMU_LAT_MASK",
+    "copy_bytes": "-DLZGPU_COPY_WIDE=0",
+    "lit_pf_latency": "-DLZGPU_LIT_PF=1 -DLZGPU_LDS_MASK=0x1BF -DLZGPU_TAIL_LIT=1",
 }
 
 
