@@ -237,6 +237,10 @@ typedef __attribute__((address_space(1))) uint32_t gu32;
 #ifndef LZGPU_COPY_WIDE
 #define LZGPU_COPY_WIDE 1
 #endif
+//   LZGPU_LIT_WC       literal batch output write-combined in a register
+#ifndef LZGPU_LIT_WC
+#define LZGPU_LIT_WC 0
+#endif
 //   LZGPU_LIT_BATCH    literals decoded per pass of the symbol loop before a
 //                      lane's match path runs (1 = one symbol per pass)
 #ifndef LZGPU_LIT_BATCH
@@ -266,6 +270,11 @@ typedef __attribute__((address_space(1))) uint32_t gu32;
 //                      the wave is done (lanes drop out by a flag)
 #ifndef LZGPU_UNIFORM_EXIT
 #define LZGPU_UNIFORM_EXIT 1
+#endif
+// (write-combining needs the batch's wave-uniform exit)
+#if !LZGPU_UNIFORM_EXIT
+#undef LZGPU_LIT_WC
+#define LZGPU_LIT_WC 0
 #endif
 
 // Per-lane decoder state (CLzmaDec fields, LzmaDec.h:50-69).  lo = the LDS
@@ -954,7 +963,6 @@ __device__ __forceinline__ void lz_store_upto8(gbyte* d, uint64_t v, uint32_t re
 }
 #endif
 
-#if LZGPU_COPY_WIDE
 // Unaligned 8-byte global access (gfx950 runs global memory in unaligned
 // mode: one dwordx2 per 8 bytes instead of eight byte instructions -- the
 // vector-memory pipeline, not bandwidth, is what a lane's byte traffic costs).
@@ -1001,7 +1009,6 @@ __device__ __forceinline__ void stu_tail(gbyte* d, uint64_t v, uint32_t rem) {
   }
   if (rem & 1) *d = uint8_t(v);
 }
-#endif
 
 __device__ __forceinline__ uint32_t lz_copy(gbyte* dic, uint64_t pos, uint64_t from, uint32_t n,
                                             uint32_t dist, uint64_t cap) {
@@ -1170,7 +1177,7 @@ __device__ __forceinline__ uint32_t lit_bit(Rc<Rd>& rc, const Tab<M, Lo>& T, uin
 
 // One literal (LzmaDec.c:161-196): plain tree for state < 7, matched tree
 // against the byte at rep0 otherwise; writes the byte, updates state.
-template <uint32_t M, class Lo, class Rd>
+template <uint32_t M, bool St = true, class Lo, class Rd>
 __device__ __forceinline__ void lz_literal(Rc<Rd>& rc, const Tab<M, Lo>& T, uint32_t& st,
                                            uint32_t& prev, uint32_t& total, uint32_t full,
                                            uint32_t lc, uint32_t lp_mask, gbyte* dic,
@@ -1254,7 +1261,8 @@ __device__ __forceinline__ void lz_literal(Rc<Rd>& rc, const Tab<M, Lo>& T, uint
     }
   }
   prev = sym & 0xFFu;
-  dic[pos++] = uint8_t(prev);
+  if constexpr (St) dic[pos] = uint8_t(prev);
+  pos++;
   total++;
 }
 
@@ -1379,6 +1387,13 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
     // when the whole wave is done: no divergent exit, so no per-iteration
     // copies of the lane state into exit registers
     bool lit_on = !is_match;
+#if LZGPU_LIT_WC
+    // the batch's literals are consecutive output bytes: collected in a
+    // register and written with at most three stores after the batch
+    static_assert(LZGPU_LIT_BATCH <= 8, "literal write-combining holds 8 bytes");
+    uint64_t lit_buf = 0;
+    uint32_t lit_n = 0;
+#endif
 #pragma unroll 1
     for (int lit = 0; lit < LZGPU_LIT_BATCH; ++lit) {
 #if LZGPU_PROF && !defined(LZGPU_HOST_EMU)
@@ -1421,11 +1436,16 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
             lz_literal_unified<M>(rc, T, st, prev, total, full, lc, lp_mask, dic, pos, mb_pf);
           else
 #endif
-          lz_literal<M>(rc, T, st, prev, total, full, lc, lp_mask, dic, pos, cap, r0
+          lz_literal<M, !LZGPU_LIT_WC>(rc, T, st, prev, total, full, lc, lp_mask, dic, pos,
+                                         cap, r0
 #if LZGPU_MB_PF
-                        , mb_pf
+                                         , mb_pf
 #endif
           );
+#if LZGPU_LIT_WC
+          lit_buf |= uint64_t(prev) << (8 * lit_n);
+          ++lit_n;
+#endif
 #if LZGPU_PROF && !defined(LZGPU_HOST_EMU)
           tC = lz_clock();
 #endif
@@ -1471,6 +1491,15 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
         stop = true;
         break;
       }
+    }
+#endif
+#if LZGPU_UNIFORM_EXIT && LZGPU_LIT_WC
+    if (lit_n != 0) {
+      gbyte* d = dic + (pos - lit_n);
+      if (lit_n == 8)
+        stu64(d, lit_buf);
+      else
+        stu_tail(d, lit_buf, lit_n);
     }
 #endif
     LZ_PROF_MARK(s, 0, t_prof);
