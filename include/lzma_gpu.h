@@ -74,6 +74,7 @@ typedef int SRes;
 typedef unsigned char Byte;
 typedef unsigned short UInt16;
 typedef unsigned int UInt32;
+typedef unsigned long long UInt64;
 typedef size_t SizeT;
 typedef int Bool;
 typedef struct {
@@ -356,6 +357,79 @@ SRes LzmaGpu_Crc32Batch(const LzmaGpuStreamDesc *d_descs, const LzmaGpuResult *d
                         size_t n, const Byte *d_dst, const uint32_t *d_chunk_base,
                         const uint32_t *d_chunk_range, size_t n_chunks, uint32_t *d_chunk_crc,
                         uint32_t *d_crc, void *stream);
+
+/* ---------------------------------------------------------------- xz, x86 BCJ, CRC-64 */
+
+/* x86 BCJ converter, drop-in for Bra.h:58 / Bra86.c:11-85 (x86_Convert: the
+ * branch-target filter of 7z and xz; encoding 0 = decode).  Runs on the GPU
+ * over the caller's host buffer; returns the bytes processed (the last <= 4
+ * are left for the next call), *state carried like the reference's.  No
+ * error channel: without a device it prints once and returns 0. */
+SizeT x86_Convert(Byte *data, SizeT size, UInt32 ip, UInt32 *state, int encoding);
+
+/* Batch x86 BCJ over device ranges, one lane per range, in place:
+ * d_data[off[i] .. off[i] + len[i]) converted with start ip[i] and state
+ * d_state[i] (in/out); d_done[i] = bytes processed.  Asynchronous on stream. */
+SRes BcjGpu_X86Batch(Byte *d_data, const uint64_t *d_off, const uint64_t *d_len,
+                     const uint32_t *d_ip, uint32_t *d_state, uint64_t *d_done, size_t n,
+                     int encoding, void *stream);
+
+/* CRC-64 (XzCrc64.c, poly 0xC96C5795D7870F42).  Crc64Calc drop-in replaces
+ * XzCrc64.h:20 / XzCrc64.c:30 (host buffer, GPU compute; 0 without a device).
+ * The batch form mirrors CrcGpu_Batch with 2048-byte chunks planned by
+ * CrcGpu_PlanChunks; d_chunk_crc: n_chunks uint64 of scratch. */
+UInt64 Crc64Calc(const void *data, size_t size);
+SRes Crc64Gpu_Batch(const Byte *d_data, const uint64_t *d_off, const uint64_t *d_len, size_t n,
+                    const uint32_t *d_chunk_base, const uint32_t *d_chunk_range, size_t n_chunks,
+                    uint64_t init, uint64_t xorout, uint64_t *d_chunk_crc, uint64_t *d_crc,
+                    void *stream);
+
+/* xz files as block batches.  The reference decodes xz strictly in order
+ * (XzUnpacker_Code, XzDec.c:604-870); the blocks of a multi-block file (and
+ * the streams of a concatenated one) are independent, so here the whole file
+ * is indexed first -- from each stream's footer and index backwards, as
+ * Xzs_ReadBackward does (XzIn.c:150-280) -- and every block decodes as one
+ * lane of an LZMA2 batch, then x86 BCJ, then the block checks on the GPU
+ * (CRC-32, CRC-64; SHA-256 on the host). */
+#define LZMA_GPU_XZ_CHECK_NONE 0
+#define LZMA_GPU_XZ_CHECK_CRC32 1
+#define LZMA_GPU_XZ_CHECK_CRC64 4
+#define LZMA_GPU_XZ_CHECK_SHA256 10
+typedef struct {
+  uint64_t header_off;  /* block header, offset in the file */
+  uint64_t data_off;    /* first byte of the block's LZMA2 data */
+  uint64_t pack_size;   /* LZMA2 data bytes (index unpadded size - header - check) */
+  uint64_t unpack_size; /* uncompressed bytes (index) */
+  uint64_t dst_off;     /* offset of the block's output in the whole file's output */
+  uint64_t check_off;   /* stored check field, offset in the file */
+  uint32_t check_type;  /* LZMA_GPU_XZ_CHECK_* of its stream */
+  uint32_t check_size;  /* 0, 4, 8 or 32 bytes */
+  uint32_t lzma2_prop;  /* dictionary byte of the LZMA2 filter (XZ_ID_LZMA2 0x21) */
+  uint32_t x86;         /* 1: an x86 BCJ filter (XZ_ID_X86 4) precedes LZMA2 */
+  uint32_t x86_ip;      /* its start offset (4-byte filter props, else 0) */
+  uint32_t stream;      /* index of its xz stream in the file */
+} LzmaGpuXzBlock;
+
+/* Index an xz file (one or more concatenated streams with stream padding).
+ * Fills up to `cap` blocks in file order, *n_blocks = the file's block count,
+ * *unpack_total = the sum of their sizes.  Header, block-header, index and
+ * footer validation follows XzDec.c / XzIn.c: SZ_ERROR_NO_ARCHIVE (magic or
+ * stream-header CRC), SZ_ERROR_ARCHIVE (block header or index malformed),
+ * SZ_ERROR_CRC (index CRC, index vs footer), SZ_ERROR_UNSUPPORTED (a filter
+ * chain other than [x86 BCJ] + LZMA2, or stream flags beyond the check
+ * field).  Host only: works without a device. */
+SRes LzmaGpu_XzIndex(const Byte *file, size_t size, LzmaGpuXzBlock *blocks, size_t cap,
+                     size_t *n_blocks, uint64_t *unpack_total);
+
+/* Decode a whole xz file held in host memory: index, upload, one batch launch
+ * over all blocks, BCJ, checks, download.  *destLen in: capacity, out: bytes
+ * written (the whole output, or 0 on error).  Returns SZ_OK, an index error
+ * above, SZ_ERROR_OUTPUT_EOF (capacity short), SZ_ERROR_DATA (a block's LZMA2
+ * data does not decode to exactly its indexed size, ending with the end mark
+ * in exactly its indexed bytes) or SZ_ERROR_CRC (a block check or non-zero
+ * block padding).  *bad_block = the first failing block, or -1. */
+SRes LzmaGpu_XzDecode(Byte *dest, SizeT *destLen, const Byte *file, size_t size,
+                      int64_t *bad_block);
 
 /* Device / diagnostics. */
 int LzmaGpu_DeviceCount(void);

@@ -1127,3 +1127,9 @@ const char* LzmaGpu_LastError(void) { return g_last_error.c_str(); }
 const char* LzmaGpu_Version(void) { return "liblzmagpu 0.1 (gfx950, LZMA SDK 9.20 decoder contract)"; }
 
 }  // extern "C"
+
+namespace lzgpu_host {
+bool ensure_device() { return ::ensure_device(); }
+void set_error(const char* what) { ::set_error(what); }
+bool hip_ok(hipError_t e, const char* what) { return ::hip_ok(e, what); }
+}  // namespace lzgpu_host

@@ -1018,7 +1018,7 @@ __device__ __forceinline__ uint32_t lz_copy(gbyte* dic, uint64_t pos, uint64_t f
     // source span does not wrap (always so for a flat LzmaDecode window)
     gbyte* d = dic + pos;
     const gbyte* src = dic + from;
-    uint64_t v;
+    uint64_t v = 0;
     uint32_t i = 0;
     if (dist >= 8) {
       // src[i..i+8) lies below d + i: written before this step reads it

@@ -1,0 +1,88 @@
+// xz_kernels.hip -- the xz block-batch kernels for gfx950.
+//
+//   lzgpu_crc64_chunk_kernel / lzgpu_crc64_fold_kernel: CRC-64 (XzCrc64.c) of
+//     byte ranges, the crc32_kernels.hip formulation with a 64-bit register
+//     (crc64_device.h): one lane per 2 KiB chunk (slice-by-8 tables in LDS,
+//     aligned 16-byte loads), then one lane per range folds the chunk
+//     registers.
+//   lzgpu_bcj_x86_kernel: x86 BCJ (Bra86.c) in place, one lane per range
+//     (bcj_device.h); an xz block's filter state starts at 0 and runs over the
+//     block's whole output.
+#include <hip/hip_runtime.h>
+
+#include "bcj_device.h"
+#include "crc64_device.h"
+
+using namespace lzgpu;
+
+__constant__ Crc64Tables kCrc64Tables = crc64_make_tables();
+
+__global__ void __launch_bounds__(256) lzgpu_crc64_chunk_kernel(
+    const uint8_t* __restrict__ data, const uint64_t* __restrict__ off,
+    const uint64_t* __restrict__ len, const uint32_t* __restrict__ chunk_base,
+    const uint32_t* __restrict__ chunk_range, uint32_t n_chunks, uint64_t init,
+    uint64_t* __restrict__ chunk_crc) {
+  __shared__ uint64_t tab[8 * 256];
+  const uint64_t* src = &kCrc64Tables.slice[0][0];
+  for (uint32_t i = threadIdx.x; i < 8 * 256; i += blockDim.x) tab[i] = src[i];
+  __syncthreads();
+  const lds_u64t* t = (const lds_u64t*)tab;
+  for (uint32_t slot = blockIdx.x * blockDim.x + threadIdx.x; slot < n_chunks;
+       slot += gridDim.x * blockDim.x) {
+    const uint32_t r = chunk_range[slot];
+    uint64_t c;
+    if (crc64_chunk(t, data + off[r], len[r], slot - chunk_base[r], init, &c)) chunk_crc[slot] = c;
+  }
+}
+
+__global__ void __launch_bounds__(256) lzgpu_crc64_fold_kernel(
+    const uint64_t* __restrict__ len, const uint32_t* __restrict__ chunk_base,
+    const uint64_t* __restrict__ chunk_crc, uint32_t n, uint64_t init, uint64_t xorout,
+    uint64_t* __restrict__ crc_out) {
+  __shared__ uint64_t sh[8 * 256];
+  const uint64_t* src = &kCrc64Tables.shift[0][0];
+  for (uint32_t i = threadIdx.x; i < 8 * 256; i += blockDim.x) sh[i] = src[i];
+  __syncthreads();
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  crc_out[i] = crc64_fold((const lds_u64t*)sh, chunk_crc + chunk_base[i], len[i], init) ^ xorout;
+}
+
+__global__ void __launch_bounds__(64) lzgpu_bcj_x86_kernel(
+    uint8_t* __restrict__ data, const uint64_t* __restrict__ off, const uint64_t* __restrict__ len,
+    const uint32_t* __restrict__ ip, uint32_t* __restrict__ state, uint64_t* __restrict__ done,
+    uint32_t n, int encoding) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t s = state[i];
+  done[i] = bcj_x86((bcj_byte*)(data + off[i]), len[i], ip[i], &s, encoding);
+  state[i] = s;
+}
+
+extern "C" int lzgpu_launch_crc64_arrays(const uint8_t* d_data, const uint64_t* d_off,
+                                         const uint64_t* d_len, uint32_t n,
+                                         const uint32_t* d_chunk_base,
+                                         const uint32_t* d_chunk_range, uint32_t n_chunks,
+                                         uint64_t init, uint64_t xorout, uint64_t* d_chunk_crc,
+                                         uint64_t* d_crc, hipStream_t stream) {
+  if (n == 0) return 0;
+  if (n_chunks) {
+    const uint32_t want = (n_chunks + 255) / 256;
+    const uint32_t grid = want < 2048 ? want : 2048;
+    hipLaunchKernelGGL(lzgpu_crc64_chunk_kernel, dim3(grid), dim3(256), 0, stream, d_data, d_off,
+                       d_len, d_chunk_base, d_chunk_range, n_chunks, init, d_chunk_crc);
+    if (hipGetLastError() != hipSuccess) return -1;
+  }
+  hipLaunchKernelGGL(lzgpu_crc64_fold_kernel, dim3((n + 255) / 256), dim3(256), 0, stream, d_len,
+                     d_chunk_base, d_chunk_crc, n, init, xorout, d_crc);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+extern "C" int lzgpu_launch_bcj_x86(uint8_t* d_data, const uint64_t* d_off, const uint64_t* d_len,
+                                    const uint32_t* d_ip, uint32_t* d_state, uint64_t* d_done,
+                                    uint32_t n, int encoding, hipStream_t stream) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(lzgpu_bcj_x86_kernel, dim3((n + 63) / 64), dim3(64), 0, stream, d_data, d_off,
+                     d_len, d_ip, d_state, d_done, n, encoding);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}

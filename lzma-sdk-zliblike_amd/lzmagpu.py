@@ -106,6 +106,17 @@ class Session(ctypes.Structure):
                 ("out", ctypes.c_void_p), ("out_len", ctypes.c_uint64)]
 
 
+class XzBlock(ctypes.Structure):
+    """LzmaGpuXzBlock (include/lzma_gpu.h): one block of an indexed xz file."""
+    _fields_ = [("header_off", ctypes.c_uint64), ("data_off", ctypes.c_uint64),
+                ("pack_size", ctypes.c_uint64), ("unpack_size", ctypes.c_uint64),
+                ("dst_off", ctypes.c_uint64), ("check_off", ctypes.c_uint64),
+                ("check_type", ctypes.c_uint32), ("check_size", ctypes.c_uint32),
+                ("lzma2_prop", ctypes.c_uint32), ("x86", ctypes.c_uint32),
+                ("x86_ip", ctypes.c_uint32), ("stream", ctypes.c_uint32)]
+
+
+assert ctypes.sizeof(XzBlock) == 72
 assert ctypes.sizeof(StreamDesc) == 48 and ctypes.sizeof(Result) == 24
 assert ctypes.sizeof(Session) == 192 and ctypes.sizeof(Plan) == 184
 assert ctypes.sizeof(CLzmaDec) == 136
@@ -145,6 +156,12 @@ _sig = {
     "CrcGpu_Batch": (ctypes.c_int, [_P, _P, _P, ctypes.c_size_t, _P, _P, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_uint32, _P, _P, _P]),
     "LzmaGpu_Crc32Plan": (ctypes.c_size_t, [ctypes.POINTER(StreamDesc), ctypes.c_size_t, _P, _P]),
     "LzmaGpu_Crc32Batch": (ctypes.c_int, [_P, _P, ctypes.c_size_t, _P, _P, _P, ctypes.c_size_t, _P, _P, _P]),
+    "x86_Convert": (ctypes.c_size_t, [_P, ctypes.c_size_t, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32), ctypes.c_int]),
+    "BcjGpu_X86Batch": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, ctypes.c_size_t, ctypes.c_int, _P]),
+    "Crc64Calc": (ctypes.c_uint64, [_P, ctypes.c_size_t]),
+    "Crc64Gpu_Batch": (ctypes.c_int, [_P, _P, _P, ctypes.c_size_t, _P, _P, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_uint64, _P, _P, _P]),
+    "LzmaGpu_XzIndex": (ctypes.c_int, [_P, ctypes.c_size_t, ctypes.POINTER(XzBlock), ctypes.c_size_t, _sp, ctypes.POINTER(ctypes.c_uint64)]),
+    "LzmaGpu_XzDecode": (ctypes.c_int, [_P, _sp, _P, ctypes.c_size_t, ctypes.POINTER(ctypes.c_int64)]),
     "LzmaGpu_DeviceCount": (ctypes.c_int, []),
     "LzmaGpu_LastError": (ctypes.c_char_p, []),
     "LzmaGpu_Version": (ctypes.c_char_p, []),
@@ -386,6 +403,43 @@ def crc32_batch_decoded(d_descs, d_results, n, d_dst, d_base, d_range, n_chunks,
     """LzmaGpu_Crc32Batch over raw device pointers (ints)."""
     return _lib.LzmaGpu_Crc32Batch(d_descs, d_results, n, d_dst, d_base, d_range, n_chunks,
                                    d_chunk_crc, d_crc, stream or None)
+
+
+# ---------------------------------------------------------------- xz, x86 BCJ, CRC-64
+
+def x86_Convert(data, ip=0, state=0, encoding=0):
+    """Bra86.c x86_Convert on the GPU: (processed, state, converted bytes)."""
+    b = ctypes.create_string_buffer(bytes(data), max(len(data), 1))
+    st = ctypes.c_uint32(state)
+    n = _lib.x86_Convert(b, len(data), ip, ctypes.byref(st), encoding)
+    return n, st.value, b.raw[:len(data)]
+
+
+def Crc64Calc(data):
+    """XzCrc64.c Crc64Calc on the GPU."""
+    return _lib.Crc64Calc(_buf(data), len(data))
+
+
+def xz_index(data):
+    """LzmaGpu_XzIndex: (res, [XzBlock...], unpack_total).  Host only."""
+    n = ctypes.c_size_t(0)
+    tot = ctypes.c_uint64(0)
+    src = _buf(data)
+    r = _lib.LzmaGpu_XzIndex(src, len(data), None, 0, ctypes.byref(n), ctypes.byref(tot))
+    if r != SZ_OK:
+        return r, [], 0
+    arr = (XzBlock * max(n.value, 1))()
+    r = _lib.LzmaGpu_XzIndex(src, len(data), arr, n.value, ctypes.byref(n), ctypes.byref(tot))
+    return r, list(arr)[:n.value], tot.value
+
+
+def XzDecode(data, dest_cap):
+    """LzmaGpu_XzDecode: (res, output bytes, bad_block)."""
+    out = ctypes.create_string_buffer(max(dest_cap, 1))
+    dl = ctypes.c_size_t(dest_cap)
+    bad = ctypes.c_int64(-1)
+    r = _lib.LzmaGpu_XzDecode(out, ctypes.byref(dl), _buf(data), len(data), ctypes.byref(bad))
+    return r, out.raw[:dl.value], bad.value
 
 
 # ---------------------------------------------------------------- streaming sessions

@@ -230,3 +230,54 @@ int ref_lzma2_decode(unsigned char *dst, size_t *dst_len, const unsigned char *s
   Lzma2Dec_FreeProbs(&dec, &g_shim_alloc);
   return res;
 }
+
+/*
+ * xz: XzUnpacker_Code (XzDec.c:604-870) over a whole
+ * in-memory file, FINISH_END, in one call with an output buffer of *dst_len
+ * bytes.  *done = XzUnpacker_IsStreamWasFinished (XzDec.c:872).  The CRC
+ * tables (CrcGenerateTable, Crc64GenerateTable) are built on first use.
+ */
+#include "7zCrc.h"
+#include "Bra.h"
+#include "Xz.h"
+#include "XzCrc64.h"
+
+static void xz_tables(void) {
+  static int done = 0;
+  if (!done) { CrcGenerateTable(); Crc64GenerateTable(); done = 1; }
+}
+
+int ref_xz_decode(unsigned char *dst, size_t *dst_len, const unsigned char *src,
+                  size_t *src_len, int *status, int *done) {
+  CXzUnpacker u;
+  SizeT dl = *dst_len, sl = *src_len;
+  ECoderStatus st = CODER_STATUS_NOT_SPECIFIED;
+  SRes res;
+  int saved;
+  xz_tables();
+  saved = quiet_begin();
+  XzUnpacker_Create(&u, &g_shim_alloc);
+  res = XzUnpacker_Code(&u, dst, &dl, src, &sl, LZMA_FINISH_END, &st);
+  *done = XzUnpacker_IsStreamWasFinished(&u) ? 1 : 0;
+  XzUnpacker_Free(&u);
+  quiet_end(saved);
+  *dst_len = dl;
+  *src_len = sl;
+  *status = (int)st;
+  return res;
+}
+
+/* x86 BCJ (Bra86.c:11) over a buffer: returns the bytes processed, state in/out. */
+size_t ref_x86_convert(unsigned char *data, size_t size, unsigned ip, unsigned *state,
+                       int encoding) {
+  UInt32 s = *state;
+  SizeT r = x86_Convert(data, size, ip, &s, encoding);
+  *state = s;
+  return r;
+}
+
+/* Crc64Calc (XzCrc64.c:30) */
+unsigned long long ref_crc64(const unsigned char *data, size_t size) {
+  xz_tables();
+  return Crc64Calc(data, size);
+}

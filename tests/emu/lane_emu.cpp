@@ -11,6 +11,8 @@
 
 #include "../../lzma-sdk-zliblike_amd/csrc/lzma_lane.h"
 #include "../../lzma-sdk-zliblike_amd/csrc/crc32_device.h"
+#include "../../lzma-sdk-zliblike_amd/csrc/crc64_device.h"
+#include "../../lzma-sdk-zliblike_amd/csrc/bcj_device.h"
 
 using namespace lzgpu;
 
@@ -138,6 +140,25 @@ void emu_crc_ranges(const uint8_t* data, const uint64_t* off, const uint64_t* le
       crc_chunk(&T.slice[0][0], data + off[i], len[i], uint32_t(j), init, &c[j]);
     out[i] = crc_fold(&T.shift[0][0], c.data(), len[i], init) ^ xorout;
   }
+}
+
+// CRC-64 kernels' per-lane code (crc64_chunk per chunk slot, then crc64_fold).
+void emu_crc64_ranges(const uint8_t* data, const uint64_t* off, const uint64_t* len, size_t n,
+                      uint64_t init, uint64_t xorout, uint64_t* out) {
+  static const Crc64Tables T = crc64_make_tables();
+  for (size_t i = 0; i < n; ++i) {
+    const uint64_t nch = (len[i] + kCrc64Chunk - 1) / kCrc64Chunk;
+    std::vector<uint64_t> c(nch + 1);
+    for (uint64_t j = 0; j < nch; ++j)
+      crc64_chunk(&T.slice[0][0], data + off[i], len[i], uint32_t(j), init, &c[j]);
+    out[i] = crc64_fold(&T.shift[0][0], c.data(), len[i], init) ^ xorout;
+  }
+}
+
+// The x86 BCJ kernel's per-lane code (bcj_x86) on one buffer.  The window
+// loads aligned 16-byte blocks holding a valid byte: callers pad buffers.
+uint64_t emu_bcj_x86(uint8_t* data, uint64_t size, uint32_t ip, uint32_t* state, int encoding) {
+  return bcj_x86(data, size, ip, state, encoding);
 }
 
 }  // extern "C"

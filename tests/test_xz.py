@@ -1,0 +1,196 @@
+"""xz files as GPU block batches, x86 BCJ and CRC-64.
+
+Reference: XzUnpacker_Code (XzDec.c:604-870), x86_Convert (Bra86.c:11-85),
+Crc64Calc (XzCrc64.c:30), compiled in place and recorded in
+tests/golden/xz_cases.json + xz_blob.bin (tests/golden/make_golden_xz.py;
+every valid file there also decodes identically through liblzma).
+
+CPU (no GPU): the index (LzmaGpu_XzIndex is host code) against the
+reference's decoded sizes and error codes; the BCJ and CRC-64 kernels'
+per-lane code (host build, tests/emu) against the reference's outputs.
+GPU (-m gpu): LzmaGpu_XzDecode on every fixture file, the x86_Convert and
+Crc64Calc drop-ins, and a many-block file decoded as one batch.
+"""
+import ctypes
+import hashlib
+import json
+import os
+import struct
+import subprocess
+import sys
+
+import pytest
+
+import native
+
+GOLDEN = os.path.join(native.ROOT, "tests", "golden")
+EMU_SO = os.path.join(native.ROOT, "tests", "emu", "liblane_emu.so")
+sys.path.insert(0, GOLDEN)
+sys.path.insert(0, os.path.join(native.ROOT, "lzma-sdk-zliblike_amd"))
+
+
+def fixtures():
+    with open(os.path.join(GOLDEN, "xz_cases.json")) as f:
+        d = json.load(f)
+    with open(os.path.join(GOLDEN, "xz_blob.bin"), "rb") as f:
+        blob = f.read()
+    assert hashlib.sha256(blob).hexdigest() == d["blob_sha256"]
+    d["blob"] = blob
+    return d
+
+
+def data_of(d, c):
+    return d["blob"][c["off"]:c["off"] + c["len"]]
+
+
+@pytest.fixture(scope="module")
+def L():
+    import lzmagpu
+    return lzmagpu
+
+
+@pytest.fixture(scope="module")
+def emu():
+    subprocess.run(["make", "-s", "-f", "tests/emu/Makefile"], cwd=native.ROOT, check=True)
+    lib = ctypes.CDLL(EMU_SO)
+    lib.emu_bcj_x86.restype = ctypes.c_uint64
+    lib.emu_bcj_x86.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_uint32,
+                                ctypes.POINTER(ctypes.c_uint32), ctypes.c_int]
+    lib.emu_crc64_ranges.restype = None
+    lib.emu_crc64_ranges.argtypes = [ctypes.c_char_p, ctypes.c_void_p, ctypes.c_void_p,
+                                     ctypes.c_size_t, ctypes.c_uint64, ctypes.c_uint64,
+                                     ctypes.c_void_p]
+    return lib
+
+
+def test_index_matches_reference(L):
+    d = fixtures()
+    for c in d["xz"]:
+        r, blocks, total = L.xz_index(data_of(d, c))
+        if c["valid"]:
+            assert r == 0, c["note"]
+            assert total == c["dest_len"], c["note"]
+            assert sum(b.unpack_size for b in blocks) == total
+            # blocks tile the output in file order
+            off = 0
+            for b in blocks:
+                assert b.dst_off == off and b.check_size in (0, 4, 8, 32)
+                assert b.data_off > b.header_off and b.check_off >= b.data_off + b.pack_size
+                off += b.unpack_size
+        elif c["res"] == 17:  # bad stream magic: the same class of error
+            assert r == 17, c["note"]
+    notes = {c["note"]: c for c in d["xz"]}
+    r, blocks, _ = L.xz_index(data_of(d, notes["24 small blocks, check 4"]))
+    assert len(blocks) == 24 and all(b.check_type == 4 for b in blocks)
+    r, blocks, _ = L.xz_index(data_of(d, notes["3 concatenated streams + stream padding"]))
+    assert [b.stream for b in blocks] == [0, 1, 2]
+    assert [b.check_type for b in blocks] == [1, 4, 10]
+    x = [c for c in d["xz"] if c["note"].startswith("multi-block, x86")][0]
+    r, blocks, _ = L.xz_index(data_of(d, x))
+    assert [b.x86 for b in blocks] == [1, 1, 1, 1]
+    assert [b.x86_ip for b in blocks] == [0, 0, 0x2000, 0]
+
+
+def test_index_rejects_malformed(L):
+    d = fixtures()
+    good = data_of(d, [c for c in d["xz"] if c["note"].startswith("multi-block stream")][0])
+    assert L.xz_index(b"")[0] == 17
+    assert L.xz_index(good[:-1])[0] == 17                # not a multiple of 4
+    bad = bytearray(good)
+    bad[-1] ^= 1                                         # footer magic
+    assert L.xz_index(bytes(bad))[0] == 17
+    bad = bytearray(good)
+    bad[-4] ^= 1                                         # footer flags: unsupported
+    assert L.xz_index(bytes(bad))[0] in (4, 16)
+    bad = bytearray(good)
+    bad[-12] ^= 1                                        # footer CRC
+    assert L.xz_index(bytes(bad))[0] == 16
+    bad = bytearray(good)
+    bad[13] ^= 0x10                                      # first block header (CRC)
+    assert L.xz_index(bytes(bad))[0] == 16
+
+
+def test_bcj_emu_matches_reference(emu):
+    d = fixtures()
+    for c in d["bcj"]:
+        n = c["len"]
+        buf = ctypes.create_string_buffer(d["blob"][c["off"]:c["off"] + n] + b"\0" * 32, n + 32)
+        st = ctypes.c_uint32(c["state_in"])
+        done = emu.emu_bcj_x86(buf, n, c["ip"], ctypes.byref(st), c["encoding"])
+        assert (done, st.value) == (c["done"], c["state_out"]), c
+        assert hashlib.sha256(buf.raw[:n]).hexdigest() == c["sha256"], c
+
+
+def test_crc64_emu_matches_reference(emu):
+    d = fixtures()
+    for c in d["crc64"]:
+        n = c["len"]
+        pad = 16
+        buf = b"\0" * pad + d["blob"][c["off"]:c["off"] + n] + b"\0" * 32
+        off = (ctypes.c_uint64 * 1)(pad)
+        ln = (ctypes.c_uint64 * 1)(n)
+        out = (ctypes.c_uint64 * 1)()
+        emu.emu_crc64_ranges(buf, off, ln, 1, 2**64 - 1, 2**64 - 1, out)
+        assert out[0] == c["crc64"], c
+
+
+@pytest.mark.gpu
+def test_gpu_xz_decode_fixtures(L):
+    d = fixtures()
+    for c in d["xz"]:
+        data = data_of(d, c)
+        cap = (c["dest_len"] if c["valid"] else 400000) + 64
+        r, out, bad = L.XzDecode(data, cap)
+        if c["valid"]:
+            assert r == 0, (c["note"], r, bad, L.last_error())
+            assert hashlib.sha256(out).hexdigest() == c["sha256"], c["note"]
+        elif c["res"] in (3, 17):  # check mismatch, bad magic: same code
+            assert r == c["res"], (c["note"], r)
+        else:                      # corrupt LZMA2 data: DATA or CRC, as the reference
+            assert r in (1, 3), (c["note"], r)
+    # capacity short
+    v = [c for c in d["xz"] if c["valid"] and c["dest_len"] > 0][0]
+    r, out, _ = L.XzDecode(data_of(d, v), v["dest_len"] - 1)
+    assert r == 7 and out == b""
+
+
+@pytest.mark.gpu
+def test_gpu_x86_convert_matches_reference(L):
+    d = fixtures()
+    for c in d["bcj"]:
+        data = d["blob"][c["off"]:c["off"] + c["len"]]
+        done, st, out = L.x86_Convert(data, c["ip"], c["state_in"], c["encoding"])
+        assert (done, st) == (c["done"], c["state_out"]), c
+        assert hashlib.sha256(out).hexdigest() == c["sha256"], c
+
+
+@pytest.mark.gpu
+def test_gpu_crc64_matches_reference(L):
+    d = fixtures()
+    for c in d["crc64"]:
+        assert L.Crc64Calc(d["blob"][c["off"]:c["off"] + c["len"]]) == c["crc64"], c
+
+
+@pytest.mark.gpu
+def test_gpu_xz_many_blocks_round_trip(L):
+    """A 512-block file (every check type across 4 concatenated streams, x86
+    BCJ on one of them) decodes as one batch; output compared to the input."""
+    import lzma
+    import make_golden_xz as M
+    parts, files = [], b""
+    for s, chk in enumerate((1, 4, 10, 0)):
+        blocks = [(native.gen("text", 7000 + 200 * s + i, 3000 + 131 * i),
+                   {"x86": 0} if s == 1 else {}) for i in range(128)]
+        files += M.make_stream(blocks, chk) + b"\0" * 4
+        parts += [b for b, _ in blocks]
+    plain = b"".join(parts)
+    r, blocks, total = L.xz_index(files)
+    assert r == 0 and len(blocks) == 512 and total == len(plain)
+    r, out, bad = L.XzDecode(files, total)
+    assert r == 0 and out == plain, (r, bad)
+    # one flipped check byte in block 300 is reported there
+    b = blocks[300]
+    bad_file = bytearray(files)
+    bad_file[b.check_off] ^= 1
+    r, out, badb = L.XzDecode(bytes(bad_file), total)
+    assert (r, badb) == (3, 300)
