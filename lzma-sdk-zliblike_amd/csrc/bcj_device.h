@@ -9,10 +9,11 @@
 // kMaskToBitNumber are the reference's tables (Bra86.c:8-9).
 //
 // Memory access: the scan reads a 32-byte register window refilled from
-// aligned 16-byte loads (the operand bytes it looks ahead at, <= 4, are always
-// inside it); a conversion rewrites four bytes with one unaligned 32-bit
-// store.  Bytes a conversion rewrites are behind the scan afterwards, so the
-// stale window copies are never read again.
+// aligned 16-byte loads and tests eight bytes per step for E8/E9 (SWAR); the
+// operand bytes it looks ahead at (<= 4) are always inside the window; a
+// conversion rewrites four bytes with one unaligned 32-bit store.  Bytes a
+// conversion rewrites are behind the scan afterwards, so the stale window
+// copies are never read again.
 #pragma once
 
 #include <stdint.h>
@@ -54,9 +55,16 @@ struct BcjWindow {
     const uint64_t q = (o & 16) ? ((o & 8) ? w[3] : w[2]) : ((o & 8) ? w[1] : w[0]);
     return uint32_t(q >> (8 * (o & 7))) & 0xFFu;
   }
-  // make [a, a + 5) readable
+  // bytes [a, a + 8) as a little-endian word (after slide(a))
+  __device__ __forceinline__ uint64_t word(uintptr_t a) const {
+    const uint32_t o = uint32_t(a - base), i = o >> 3, sh = 8 * (o & 7);
+    const uint64_t lo = (i & 2) ? ((i & 1) ? w[3] : w[2]) : ((i & 1) ? w[1] : w[0]);
+    const uint64_t hi = (i & 2) ? w[3] : ((i & 1) ? w[2] : w[1]);
+    return sh ? ((lo >> sh) | (hi << (64 - sh))) : lo;
+  }
+  // make [a, a + 8) readable
   __device__ __forceinline__ void slide(uintptr_t a) {
-    while (a + 5 > base + 32) {
+    while (a + 8 > base + 32) {
       w[0] = w[2];
       w[1] = w[3];
       base += 16;
@@ -84,13 +92,26 @@ __device__ inline uint64_t bcj_x86(bcj_byte* data, uint64_t size, uint32_t ip, u
   uint64_t pos = 0, prev_pos = ~uint64_t(0);
   const uint64_t limit = size - 4;
   for (;;) {
-    // scan for E8 / E9
+    // scan for E8 / E9 eight bytes at a time: x has a zero byte exactly where
+    // the byte is E8 or E9, and the lowest set bit of the has-zero mask marks
+    // the first of them (higher bits may be borrow artefacts, never lower)
+    const uint64_t scan0 = pos;
     while (pos < limit) {
       win.slide(d0 + pos);
-      if ((win.at(d0 + pos) & 0xFEu) == 0xE8u) break;
-      ++pos;
+      const uint64_t x = (win.word(d0 + pos) & 0xFEFEFEFEFEFEFEFEull) ^ 0xE8E8E8E8E8E8E8E8ull;
+      const uint64_t z = (x - 0x0101010101010101ull) & ~x & 0x8080808080808080ull;
+      if (z != 0) {
+        pos += uint64_t(__builtin_ctzll(z) >> 3);
+        break;
+      }
+      pos += 8;
     }
-    if (pos >= limit) break;
+    if (pos >= limit) {
+      // the byte-wise scan stops at limit; a conversion may have left pos beyond it
+      pos = scan0 < limit ? limit : scan0;
+      break;
+    }
+    win.slide(d0 + pos);  // the operand bytes pos + 1 .. pos + 4
     uint64_t gap = pos - prev_pos;
     if (gap > 3) {
       prev_mask = 0;

@@ -420,6 +420,19 @@ def Crc64Calc(data):
     return _lib.Crc64Calc(_buf(data), len(data))
 
 
+def bcj_x86_batch_device(d_data, d_off, d_len, d_ip, d_state, d_done, n, encoding=0, stream=0):
+    """BcjGpu_X86Batch over raw device pointers (ints)."""
+    return _lib.BcjGpu_X86Batch(d_data, d_off, d_len, d_ip, d_state, d_done, n, encoding,
+                                stream or None)
+
+
+def crc64_batch_device(d_data, d_off, d_len, n, d_base, d_range, n_chunks, init, xorout,
+                       d_chunk_crc, d_crc, stream=0):
+    """Crc64Gpu_Batch over raw device pointers (ints)."""
+    return _lib.Crc64Gpu_Batch(d_data, d_off, d_len, n, d_base, d_range, n_chunks, init, xorout,
+                               d_chunk_crc, d_crc, stream or None)
+
+
 def xz_index(data):
     """LzmaGpu_XzIndex: (res, [XzBlock...], unpack_total).  Host only."""
     n = ctypes.c_size_t(0)

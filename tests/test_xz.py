@@ -176,7 +176,7 @@ def test_gpu_xz_many_blocks_round_trip(L):
     """A 512-block file (every check type across 4 concatenated streams, x86
     BCJ on one of them) decodes as one batch; output compared to the input."""
     import lzma
-    import make_golden_xz as M
+    import xzwrite as M
     parts, files = [], b""
     for s, chk in enumerate((1, 4, 10, 0)):
         blocks = [(native.gen("text", 7000 + 200 * s + i, 3000 + 131 * i),
