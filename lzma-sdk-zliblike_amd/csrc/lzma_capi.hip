@@ -799,8 +799,17 @@ SRes LzmaGpu_PlanBatchEx(LzmaGpuStreamDesc* descs, size_t n, uint32_t* order,
     if ((lat && mask_over != 1) || mask_over == 2) {
       uint32_t stride_lat = 0;
       for (uint32_t i : bucket_idx[b]) stride_lat = std::max(stride_lat, w_lat[i]);
-      if (stride_lat <= kMaxLdsCells)
+      if (stride_lat <= kMaxLdsCells) {
         c = plan_lds_class(stride_lat, bucket_idx[b].size(), LZGPU_LDS_MASK_LAT);
+        // few streams per CU: the wave-cooperative kernel (all 32 lanes on one
+        // stream, literal trees decided by lane speculation) -- config 4
+        // 1.71 -> 2.85 GB/s and the xz leg 1.45 -> 2.36 at 4 streams per CU;
+        // at 16 per CU (config 2) the single-lane waves are faster (5.9 vs 5.2)
+        const uint64_t per_cu_batch = (bucket_idx[b].size() + kPlanCUs - 1) / kPlanCUs;
+        const int coop = env_int("LZGPU_COOP", -1);
+        if (c.lanes_per_group == 1 && (coop == 1 || (coop < 0 && per_cu_batch <= 8)))
+          c.lds_mask = LZGPU_LDS_MASK_LAT | lzgpu::kCoopBit;
+      }
     }
     plan->classes[plan->n_classes++] = c;
     plan->n_lds += c.n;

@@ -592,6 +592,9 @@ typedef GlobalReader PlainReader;
 // throughput placement (many lanes per wave: a refill check in every
 // NORMALIZE fires in some lane almost every decision), the per-byte-checked
 // one elsewhere (one lane per wave: config 2 5.8 vs 5.2 GB/s).
+// Bit 31 of a placement mask marks the wave-cooperative kernel (kCoopBit: one
+// stream per wave, every lane holding the same state; lit8_coop).
+constexpr uint32_t kCoopBit = 0x80000000u;
 template <uint32_t M>
 struct BulkReaderFor {
   typedef PlainReader type;
@@ -602,6 +605,10 @@ struct BulkReaderFor<LZGPU_LDS_MASK> {
   typedef GlobalReaderQ type;
 };
 #endif
+template <>
+struct BulkReaderFor<LZGPU_LDS_MASK_LAT | kCoopBit> {
+  typedef GlobalReaderQ type;
+};
 
 // checkpoint hooks for readers without them: every NORMALIZE checks
 template <class Rd>
@@ -948,6 +955,107 @@ struct Rc {
   }
 };
 
+// ------------------------------------------------------------------ wave-cooperative tree stage
+//
+// Latency placement, cooperative kernel (one stream per wave, all lanes hold the
+// same decoder state): L levels of an MSB-first bit tree below node m0 decoded at
+// once.  Lane j assumes the path bits j (MSB first) and runs the L decisions of
+// that path on its own copy of (range, code, input window): with the bits assumed,
+// each level's new range/code follow from the assumption without waiting for the
+// comparison, and the L cells were read in one batch -- the comparisons only
+// verify the assumption.  Exactly one path is consistent with all L comparisons
+// (the one the serial decoder takes); its lane's state is broadcast and it alone
+// stores its L probability updates.  The reader must hold >= L bytes (a
+// checkpoint precedes the stage).  Returns the node reached (m0 << L | bits).
+#ifdef LZGPU_HOST_EMU
+__device__ __forceinline__ uint32_t lz_lane_id() { return 0; }
+#else
+__device__ __forceinline__ uint32_t lz_lane_id() { return __lane_id(); }
+#endif
+
+template <int L>
+struct SpecPath {
+  uint32_t range, code, nb;
+  uint64_t win;
+  uint32_t np[L];
+  bool ok;
+};
+
+template <int L, class P>
+__device__ __forceinline__ void spec_path(uint32_t j, uint32_t m0, P probs, uint32_t range,
+                                          uint32_t code, uint64_t win, uint32_t nb,
+                                          SpecPath<L>& o) {
+  uint32_t pv[L];
+#pragma unroll
+  for (int k = 0; k < L; ++k) pv[k] = probs[(m0 << k) | (j >> (L - k))];
+  bool ok = true;
+#pragma unroll
+  for (int k = 0; k < L; ++k) {
+    const bool n = range < kTop;  // NORMALIZE (LzmaDec.c:17), branch-free per lane
+    code = n ? ((code << 8) | uint32_t(win & 0xFFu)) : code;
+    range = n ? (range << 8) : range;
+    win = n ? (win >> 8) : win;
+    nb -= n ? 1u : 0u;
+    const uint32_t bound = (range >> 11) * pv[k];
+    const bool bk = ((j >> (L - 1 - k)) & 1u) != 0u;
+    ok = ok && ((code >= bound) == bk);
+    o.np[k] = uint32_t(int32_t(pv[k]) - ((int32_t(pv[k]) - (bk ? 0 : int32_t(kProbOne - 31))) >> 5));
+    range = bk ? range - bound : bound;
+    code = bk ? code - bound : code;
+  }
+  o.range = range;
+  o.code = code;
+  o.win = win;
+  o.nb = nb;
+  o.ok = ok;
+}
+
+template <int L, class P>
+__device__ __forceinline__ uint32_t spec_stage(Rc<GlobalReaderQ>& rc, P probs, uint32_t m0) {
+  constexpr uint32_t kPaths = 1u << L;
+  SpecPath<L> o;
+  uint32_t w;
+#ifdef LZGPU_HOST_EMU
+  for (w = 0; w < kPaths; ++w) {
+    spec_path<L>(w, m0, probs, rc.range, rc.code, rc.rd->win, rc.rd->nb, o);
+    if (o.ok) break;
+  }
+#else
+  const uint32_t j = lz_lane_id() & (kPaths - 1u);
+  spec_path<L>(j, m0, probs, rc.range, rc.code, rc.rd->win, rc.rd->nb, o);
+  const uint64_t hits = __builtin_amdgcn_ballot_w64(o.ok);
+  const uint32_t wl = uint32_t(__builtin_ctzll(hits));  // wave-uniform winner lane
+  w = wl & (kPaths - 1u);
+  const bool mine = lz_lane_id() == wl;
+  o.range = uint32_t(__builtin_amdgcn_readlane(int(o.range), int(wl)));
+  o.code = uint32_t(__builtin_amdgcn_readlane(int(o.code), int(wl)));
+  o.nb = uint32_t(__builtin_amdgcn_readlane(int(o.nb), int(wl)));
+  const uint32_t wlo = uint32_t(__builtin_amdgcn_readlane(int(uint32_t(o.win)), int(wl)));
+  const uint32_t whi = uint32_t(__builtin_amdgcn_readlane(int(uint32_t(o.win >> 32)), int(wl)));
+  o.win = uint64_t(wlo) | (uint64_t(whi) << 32);
+  if (mine)
+#endif
+  {
+#pragma unroll
+    for (int k = 0; k < L; ++k) probs[(m0 << k) | (w >> (L - k))] = uint16_t(o.np[k]);
+  }
+  rc.range = o.range;
+  rc.code = o.code;
+  rc.rd->win = o.win;
+  rc.rd->nb = o.nb;
+  return (m0 << L) | w;
+}
+
+// the plain literal tree in two cooperative stages (5 + 3 levels); the caller's
+// IsMatch checkpoint is followed by one here, and one between the stages
+template <class P>
+__device__ __forceinline__ uint32_t lit8_coop(Rc<GlobalReaderQ>& rc, P probs) {
+  rc.rd->topup();
+  const uint32_t m = spec_stage<5>(rc, probs, 1u);
+  rc.rd->topup();
+  return spec_stage<3>(rc, probs, m);
+}
+
 // Copy n bytes of an LZ match: dic[pos..pos+n) = dic[from..], byte-serial
 // overlap semantics (rep0 < n replicates the period), ring wrap at cap.
 // Non-overlapping, non-wrapping spans go 8 bytes per round trip.
@@ -1194,7 +1302,9 @@ __device__ __forceinline__ void lz_literal(Rc<Rd>& rc, const Tab<M, Lo>& T, uint
 #if LZGPU_LIT_2RT
     sym = rc.tree8_2rt(T.template at<S_LITP>(ctx << 8));
 #elif LZGPU_READER_Q
-    {
+    if constexpr (((M & kCoopBit) != 0u) && __is_same(Rd, GlobalReaderQ)) {
+      sym = lit8_coop(rc, T.template at<S_LITP>(ctx << 8));
+    } else {
       auto lp = T.template at<S_LITP>(ctx << 8);
 #if LZGPU_LIT_PF
       sym = rc.lit8_pf(lp);
@@ -1948,8 +2058,18 @@ __device__ __forceinline__ void fill_prob_init(P p, uint32_t n) {
 template <uint32_t M, class Lo>
 __device__ __forceinline__ void lz_init_state_real(LzStateT<Lo>& s) {
   const Layout L = make_layout(s.lc, s.lp, s.pb, M);
-  if constexpr (M != 0u) fill_prob_init(s.lo, L.lds_cells);
-  fill_prob_init(s.gl, L.glb_cells);
+#ifndef LZGPU_HOST_EMU
+  if constexpr ((M & kCoopBit) != 0u) {
+    // cooperative kernel: the lanes share the stream's tables, each fills a
+    // stride (a wave's own LDS and global stores are seen by its later loads)
+    for (uint32_t i = threadIdx.x; i < L.lds_cells; i += blockDim.x) s.lo[i] = uint16_t(kProbInit);
+    for (uint32_t i = threadIdx.x; i < L.glb_cells; i += blockDim.x) s.gl[i] = uint16_t(kProbInit);
+  } else
+#endif
+  {
+    if constexpr ((M & ~kCoopBit) != 0u) fill_prob_init(s.lo, L.lds_cells);
+    fill_prob_init(s.gl, L.glb_cells);
+  }
   s.rep0 = s.rep1 = s.rep2 = s.rep3 = 1;
   s.st = 0;
   s.need_state_init = 0;

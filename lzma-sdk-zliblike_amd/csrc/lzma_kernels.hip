@@ -56,6 +56,32 @@ __global__ void __launch_bounds__(64, W) lzgpu_decode_lds_kernel(
   }
 }
 
+// Wave-cooperative decode (latency regime): one stream per workgroup of one
+// 32-lane wave.  Every lane runs the same decoder on the same state, so control
+// flow and memory traffic are those of one lane -- except the literal tree,
+// whose levels are decided several at a time by speculating over the lanes
+// (spec_stage in lzma_device.h).  Lane 0 takes the next stream from the queue.
+template <int W, uint32_t M>
+__global__ void __launch_bounds__(32, W) lzgpu_decode_coop_kernel(
+    const LzmaGpuStreamDesc* __restrict__ descs, const uint32_t* __restrict__ order, uint32_t n,
+    const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, uint16_t* __restrict__ ws,
+    LzmaGpuResult* __restrict__ results, uint32_t stride, uint32_t* __restrict__ queue) {
+  extern __shared__ uint32_t lz_smem[];
+  lds_u16* lo = (lds_u16*)((uint16_t*)lz_smem);
+  uint32_t idx = blockIdx.x;
+  while (idx < n) {
+    const uint32_t id = order ? order[idx] : idx;
+    const LzmaGpuStreamDesc d = descs[id];
+    const LzmaGpuResult r = lane_decode_lds<M>(d, src, dst, ws, lo, stride);
+    uint32_t next = 0;
+    if (threadIdx.x == 0) {
+      results[id] = r;
+      next = gridDim.x + atomicAdd(queue, 1u);
+    }
+    idx = uint32_t(__builtin_amdgcn_readfirstlane(int(next)));
+  }
+}
+
 // One DecodeToDic call per lane on a device-resident decoder state.
 __global__ void __launch_bounds__(64) lzgpu_session_kernel(LzgpuSession* __restrict__ sess,
                                                            uint32_t n) {
@@ -104,6 +130,31 @@ static int launch_lds(const LzmaGpuStreamDesc* d_descs, const uint32_t* d_order,
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+template <int W, uint32_t M>
+static int launch_coop(const LzmaGpuStreamDesc* d_descs, const uint32_t* d_order, uint32_t n,
+                       const uint8_t* d_src, uint8_t* d_dst, uint16_t* d_ws,
+                       LzmaGpuResult* d_results, uint32_t stride, uint32_t groups_per_cu,
+                       uint32_t max_groups, uint32_t* d_queue, hipStream_t stream) {
+  static bool attr_set = false;
+  if (!attr_set) {
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(lzgpu_decode_coop_kernel<W, M>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr_set = true;
+  }
+  if (hipMemsetAsync(d_queue, 0, sizeof(uint32_t), stream) != hipSuccess) return -1;
+  size_t lds = size_t(stride) * 2;
+  if (groups_per_cu) {
+    const size_t share = (size_t(160 * 1024) / groups_per_cu) & ~size_t(511);
+    if (share > lds) lds = share;
+  }
+  uint32_t grid = n;
+  if (max_groups && grid > max_groups) grid = max_groups;
+  auto kfn = lzgpu_decode_coop_kernel<W, M>;
+  hipLaunchKernelGGL(kfn, dim3(grid), dim3(32), lds, stream, d_descs, d_order, n, d_src, d_dst,
+                     d_ws, d_results, stride, d_queue);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 template <uint32_t M>
 static int launch_lds_w(const LzmaGpuStreamDesc* d_descs, const uint32_t* d_order, uint32_t n,
                         const uint8_t* d_src, uint8_t* d_dst, uint16_t* d_ws,
@@ -131,6 +182,17 @@ extern "C" int lzgpu_launch_decode_lds(const LzmaGpuStreamDesc* d_descs, const u
     return launch_lds_w<LZGPU_LDS_MASK>(d_descs, d_order, n, d_src, d_dst, d_ws, d_results, lanes,
                                         stride, waves_per_simd, groups_per_cu, max_groups,
                                         d_queue, stream);
+  if (lds_mask == (LZGPU_LDS_MASK_LAT | kCoopBit)) {
+    // one wave per workgroup: register budget by workgroups per SIMD
+    const uint32_t w = (groups_per_cu + 3) / 4;
+    if (w <= 2)
+      return launch_coop<2, LZGPU_LDS_MASK_LAT | kCoopBit>(d_descs, d_order, n, d_src, d_dst,
+                                                            d_ws, d_results, stride, groups_per_cu,
+                                                            max_groups, d_queue, stream);
+    return launch_coop<4, LZGPU_LDS_MASK_LAT | kCoopBit>(d_descs, d_order, n, d_src, d_dst, d_ws,
+                                                          d_results, stride, groups_per_cu,
+                                                          max_groups, d_queue, stream);
+  }
   if (lds_mask == LZGPU_LDS_MASK_LAT)
     return launch_lds_w<LZGPU_LDS_MASK_LAT>(d_descs, d_order, n, d_src, d_dst, d_ws, d_results,
                                             lanes, stride, waves_per_simd, groups_per_cu,

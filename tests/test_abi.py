@@ -134,8 +134,9 @@ def test_plan_batch_workspace_and_order():
     # and LenHigh trees in LDS) = 56 * 2^pb + 324 + 0x100 << (lc+lp) cells
     assert plan.n_classes == 2
     c0, c1 = plan.classes[0], plan.classes[1]
-    assert (c0.n, c0.lds_cells_per_lane, c0.lds_mask) == (1, 56 + 324 + 256, 0x1BF)
-    assert (c1.n, c1.lds_cells_per_lane, c1.lds_mask) == (1, 56 * 4 + 324 + (256 << 3), 0x1BF)
+    COOP = 0x80000000  # one stream per workgroup: the wave-cooperative kernel
+    assert (c0.n, c0.lds_cells_per_lane, c0.lds_mask) == (1, 56 + 324 + 256, 0x1BF | COOP)
+    assert (c1.n, c1.lds_cells_per_lane, c1.lds_mask) == (1, 56 * 4 + 324 + (256 << 3), 0x1BF | COOP)
     assert (c0.lanes_per_group, c0.groups_per_cu) == (1, 16)
     # a full-size batch is in the throughput regime: placement 0x105 (IsMatch,
     # IsRep/G0/G1/G2, plain literal tree) = 12 * 2^pb + 48 + 0x100 << (lc+lp) cells

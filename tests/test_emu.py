@@ -45,6 +45,7 @@ EMU_VARIANTS = {
     "match_thin": "-DLZGPU_MATCH_FAT=0",
     "match_fat_global_len": "-DLZGPU_LDS_MASK_LAT=0x105 -DLZGPU_LDS_MASK=0x107 -DEMU_LAT_MASK",
     "latency_instantiation": "-DEMU_LAT_MASK",
+    "coop_instantiation": "-DEMU_COOP",
     "copy_bytes": "-DLZGPU_COPY_WIDE=0",
     "lit_store_each": "-DLZGPU_LIT_WC=0",
     "lit_pf_latency": "-DLZGPU_LIT_PF=1 -DLZGPU_LDS_MASK=0x1BF -DLZGPU_TAIL_LIT=1",
