@@ -215,6 +215,25 @@ def build_cfg4_unique(workers):
     return parts, crcs
 
 
+def print_prof(L):
+    """Region cycles and counters of a profiling build (LZGPU_PROF), else nothing."""
+    if hasattr(L.lib, "LzmaGpu_ProfileRead"):  # profiling variant builds only
+        buf = (ctypes.c_ulonglong * 24)()
+        L.lib.LzmaGpu_ProfileRead(buf, 0)
+        lanes = max(1, buf[23])
+        names = ("literal_batches", "match_decode", "copy_tail", "decode_to_dic_total",
+                 "refills", "batch_iters|slot_sub3_a", "lit_lanes|slot_sub3_b", "mlit_lanes|n_slot",
+                 "mixed_iters|cyc_rep_bits", "match_entries|cyc_len", "match_lanes|cyc_dist",
+                 "live_lanes|n_dist", "bytes", "matches|cyc_drain",
+                 "cyc_ismatch", "cyc_literal", "cyc_lit_tail", "cyc_iterations")
+        prof = {k: buf[i] / lanes for i, k in enumerate(names)}
+        prof["other_in_decode_to_dic"] = prof["decode_to_dic_total"] - sum(
+            prof[k] for k in names[:3])  # refills overlap the first three regions
+        log("PROF per stream (cycles: lane-summed wave time; counts: wave-level "
+            "seen by each lane): " + json.dumps(
+            {k: round(v) for k, v in prof.items()}))
+
+
 def run_cfg4(args):
     import dist_bench as D
     world, rank, local_rank = D.world_info()
@@ -296,6 +315,7 @@ def run_cfg4(args):
     D.barrier()
     torch.cuda.synchronize()
     elapsed = D.reduce_max(time.perf_counter() - t0, dev)
+    print_prof(L)
     scat_ms = float(np.mean([a.elapsed_time(b) for a, b, _ in ev]))
     dec_ms = float(np.mean([b.elapsed_time(c) for _, b, c in ev]))
     scat_ms = D.reduce_max(scat_ms, dev)
@@ -855,21 +875,7 @@ def main():
         log(f"[rank {rank}] VERIFY FAILED: res={np.unique(res['res'])} "
             f"status={np.unique(res['status'])}")
 
-    if hasattr(L.lib, "LzmaGpu_ProfileRead"):  # profiling variant builds only
-        buf = (ctypes.c_ulonglong * 24)()
-        L.lib.LzmaGpu_ProfileRead(buf, 0)
-        lanes = max(1, buf[23])
-        names = ("literal_batches", "match_decode", "copy_tail", "decode_to_dic_total",
-                 "refills", "batch_iters|slot_sub3_a", "lit_lanes|slot_sub3_b", "mlit_lanes|n_slot",
-                 "mixed_iters|cyc_rep_bits", "match_entries|cyc_len", "match_lanes|cyc_dist",
-                 "live_lanes|n_dist", "bytes", "matches|cyc_drain",
-                 "cyc_ismatch", "cyc_literal", "cyc_lit_tail", "cyc_iterations")
-        prof = {k: buf[i] / lanes for i, k in enumerate(names)}
-        prof["other_in_decode_to_dic"] = prof["decode_to_dic_total"] - sum(
-            prof[k] for k in names[:3])  # refills overlap the first three regions
-        log("PROF per stream (cycles: lane-summed wave time; counts: wave-level "
-            "seen by each lane): " + json.dumps(
-            {k: round(v) for k, v in prof.items()}))
+    print_prof(L)
     crc = measure_crc(L, torch, descs, d_desc, d_res, d_dst, plain, count, n, stream, dev,
                       args.steps) if not args.no_crc else None
     if crc is not None:

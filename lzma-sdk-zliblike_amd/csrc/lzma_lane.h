@@ -123,8 +123,18 @@ __device__ __forceinline__ LzmaGpuResult lane_decode_lds(const LzmaGpuStreamDesc
     if (r.res != kOk) return r;
     uint64_t sl = d.src_len;
     int status = kStNone;
+#if LZGPU_PROF && !defined(LZGPU_HOST_EMU)
+    for (int k = 0; k < 18; ++k) p.dec.prof[k] = 0;
+    const uint64_t t0 = lz_clock();
+#endif
     r.res = lz2_decode_to_dic<M>(p, d.dst_cap, (const gbyte*)(src + d.src_off), sl,
                                               d.finish_mode, status);
+#if LZGPU_PROF && !defined(LZGPU_HOST_EMU)
+    p.dec.prof[3] = lz_clock() - t0;
+    p.dec.prof[12] = p.dec.total;
+    for (int k = 0; k < 18; ++k) atomicAdd(&g_lz_prof[k], (unsigned long long)p.dec.prof[k]);
+    atomicAdd(&g_lz_prof[23], 1ull);
+#endif
     r.status = status;
     r.dest_len = p.dec.pos;
     r.src_len = sl;
