@@ -246,6 +246,12 @@ typedef __attribute__((address_space(1))) uint32_t gu32;
 #ifndef LZGPU_LIT_BATCH
 #define LZGPU_LIT_BATCH 8
 #endif
+//   LZGPU_LIT_THR      with the uniform exit: leave the literal batch when fewer
+//                      than this % of the live lanes still decode literals
+//                      (0 = only when none does); LZGPU_LIT_BATCH is the cap
+#ifndef LZGPU_LIT_THR
+#define LZGPU_LIT_THR 0
+#endif
 //   LZGPU_MLIT_PF      matched literal with the matched-tree cells in global
 //                      memory: load the eight cells of the all-match path at
 //                      once (one round trip instead of up to eight)
@@ -1578,6 +1584,18 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
         const bool more = lz_any(lit_on);
         s.prof[17] += lz_clock() - t_it;  // the whole iteration, every live lane
         if (!more) break;
+      }
+#elif LZGPU_LIT_THR
+      {
+        // leave the batch once fewer than LZGPU_LIT_THR % of the wave's live
+        // lanes are still on literals (the others wait for the match path)
+#ifdef LZGPU_HOST_EMU
+        if (!lit_on) break;
+#else
+        const uint32_t on = uint32_t(__builtin_popcountll(__builtin_amdgcn_ballot_w64(lit_on)));
+        const uint32_t live = uint32_t(__builtin_popcountll(__builtin_amdgcn_ballot_w64(true)));
+        if (on == 0 || on * 100u < live * uint32_t(LZGPU_LIT_THR)) break;
+#endif
       }
 #else
       if (!lz_any(lit_on)) break;

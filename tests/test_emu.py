@@ -48,6 +48,7 @@ EMU_VARIANTS = {
     "coop_instantiation": "-DEMU_COOP",
     "copy_bytes": "-DLZGPU_COPY_WIDE=0",
     "lit_store_each": "-DLZGPU_LIT_WC=0",
+    "lit_threshold": "-DLZGPU_LIT_THR=60 -DLZGPU_LIT_BATCH=32",
     "lit_pf_latency": "-DLZGPU_LIT_PF=1 -DLZGPU_LDS_MASK=0x1BF -DLZGPU_TAIL_LIT=1",
 }
 
