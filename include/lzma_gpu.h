@@ -431,6 +431,59 @@ SRes LzmaGpu_XzIndex(const Byte *file, size_t size, LzmaGpuXzBlock *blocks, size
 SRes LzmaGpu_XzDecode(Byte *dest, SizeT *destLen, const Byte *file, size_t size,
                       int64_t *bad_block);
 
+/* ---- 7z archives as folder batches ----------------
+ * Replaces SzArEx_Open (7zIn.c:1314) + a SzArEx_Extract loop over every file
+ * (7zIn.c:1322; ExtractAllFiles 7zIn.c:1405 in the fork): the header walk
+ * runs on the host (an LZMA / LZMA2-packed header is decoded on the GPU),
+ * every folder of the archive is one item of a single GPU batch, BCJ x86
+ * folders go through the BCJ kernel and every folder / file CRC through one
+ * CRC-32 batch.  Folder shapes: Copy / LZMA / LZMA2, optionally followed by
+ * BCJ x86 (CheckSupportedFolder, 7zDec.c:269); ARM and BCJ2 folders, which
+ * the reference also decodes, return SZ_ERROR_UNSUPPORTED here. */
+typedef struct LzmaGpu7zFolder {   /* 80 bytes */
+  uint64_t pack_off;     /* archive offset of the main coder's pack stream */
+  uint64_t pack_size;
+  uint64_t unpack_size;  /* SzFolder_GetUnpackSize */
+  uint64_t dst_off;      /* offset of the folder's output in the extraction buffer */
+  uint64_t method;       /* coder 0 method id (0 Copy, 0x030101 LZMA, 0x21 LZMA2) */
+  uint32_t x86;          /* 1: a BCJ x86 coder follows */
+  uint32_t supported;    /* SZ_OK, or the SRes the folder fails with before decoding */
+  uint32_t crc_defined, crc;
+  uint32_t first_file;   /* FolderStartFileIndex */
+  uint32_t num_files;    /* NumUnpackStreams */
+  uint32_t num_coders;
+  uint32_t props_size;
+  Byte props[8];
+} LzmaGpu7zFolder;
+
+typedef struct LzmaGpu7zFile {     /* 48 bytes */
+  uint64_t size;
+  uint64_t dst_off;      /* offset of the file's bytes in the extraction buffer */
+  uint32_t folder;       /* FileIndexToFolderIndexMap: 0xFFFFFFFF = no data */
+  uint32_t crc, crc_defined;
+  uint32_t has_stream, is_dir;
+  uint32_t name_off, name_len;  /* UTF-16 units into the names buffer (name_len counts the NUL) */
+  uint32_t reserved;
+} LzmaGpu7zFile;
+
+/* SzArEx_Open: SZ_OK or its error (SZ_ERROR_NO_ARCHIVE, _UNSUPPORTED, _CRC,
+ * _ARCHIVE, _INPUT_EOF, a packed header's decode error).  Fills up to
+ * folder_cap / file_cap / names_cap entries (any pointer may be NULL); the
+ * counts and *unpack_total (the extraction buffer size) are always set. */
+SRes LzmaGpu_7zOpen(const Byte *archive, size_t size, LzmaGpu7zFolder *folders,
+                    size_t folder_cap, size_t *n_folders, LzmaGpu7zFile *files, size_t file_cap,
+                    size_t *n_files, UInt16 *names, size_t names_cap, size_t *names_len,
+                    UInt64 *unpack_total);
+
+/* Every folder decoded into dest (folders back to back, files at their
+ * LzmaGpu7zFile.dst_off); *destLen in: capacity (SZ_ERROR_OUTPUT_EOF if
+ * below unpack_total), out: unpack_total.  file_res[i] = what SzArEx_Extract
+ * returns for file i with a fresh folder cache (SZ_OK, the folder's decode
+ * error, SZ_ERROR_CRC, SZ_ERROR_FAIL).  Returns SzArEx_Open's error, else the
+ * first file's non-OK result, else SZ_OK. */
+SRes LzmaGpu_7zExtract(Byte *dest, SizeT *destLen, const Byte *archive, size_t size,
+                       SRes *file_res, size_t file_cap);
+
 /* Device / diagnostics. */
 int LzmaGpu_DeviceCount(void);
 const char *LzmaGpu_LastError(void);

@@ -39,6 +39,37 @@ namespace lzgpu_host {
 bool ensure_device();
 void set_error(const char* what);
 bool hip_ok(hipError_t e, const char* what);
+
+// host CRC-32 for container metadata (7zCrc.c semantics; headers, a few
+// bytes per block -- decoded data is checked on the GPU)
+inline uint32_t crc32_host(const uint8_t* p, size_t n) {
+  static uint32_t t[256];
+  static bool init = false;
+  if (!init) {
+    for (uint32_t v = 0; v < 256; ++v) {
+      uint32_t r = v;
+      for (int j = 0; j < 8; ++j) r = (r >> 1) ^ ((r & 1u) ? 0xEDB88320u : 0u);
+      t[v] = r;
+    }
+    init = true;
+  }
+  uint32_t c = 0xFFFFFFFFu;
+  for (size_t i = 0; i < n; ++i) c = t[(c ^ p[i]) & 0xFFu] ^ (c >> 8);
+  return c ^ 0xFFFFFFFFu;
+}
+
+// owning device array for the container drivers' per-call buffers
+template <class T>
+struct DevArr {
+  T* p = nullptr;
+  DevArr() = default;
+  DevArr(const DevArr&) = delete;
+  DevArr& operator=(const DevArr&) = delete;
+  ~DevArr() {
+    if (p) (void)hipFree(p);
+  }
+  bool alloc(size_t n) { return hipMalloc(&p, (n ? n : 1) * sizeof(T)) == hipSuccess; }
+};
 }  // namespace lzgpu_host
 
 extern "C" int lzgpu_launch_crc_decoded(const LzmaGpuStreamDesc* d_descs,

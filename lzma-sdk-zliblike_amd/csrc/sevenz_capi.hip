@@ -1,0 +1,984 @@
+// sevenz_capi.hip -- 7z archives as GPU folder batches (include/lzma_gpu.h,
+// SURVEY.md 8(f) row 3).
+//
+// The reference opens an archive with SzArEx_Open (7zIn.c:1214-1320: start
+// header, next header, an optional packed header decoded through a folder)
+// and extracts file by file with SzArEx_Extract (7zIn.c:1322-1402), which
+// decodes the file's whole folder (SzFolder_Decode, 7zDec.c:335-471) into a
+// cached buffer and checks the folder and file CRCs.  Here the header walk
+// is restated on the host (it is a few hundred bytes of metadata), and every
+// folder of the archive becomes one item of a single GPU batch: LZMA / LZMA2
+// main coders through LzmaGpu_PlanBatchEx / LzmaGpu_DecodeBatchEx, Copy
+// folders as device copies, then the x86 BCJ kernel over BCJ folders and one
+// CRC-32 batch over every folder and file range.  Per-file results are what
+// SzArEx_Extract returns for that file with a fresh folder cache.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <vector>
+
+#include "lzma_gpu_internal.h"
+
+using lzgpu_host::crc32_host;
+using lzgpu_host::DevArr;
+using lzgpu_host::ensure_device;
+using lzgpu_host::hip_ok;
+using lzgpu_host::set_error;
+
+namespace {
+
+// property ids (7z.h:17-45)
+enum : uint64_t {
+  kEnd = 0, kHeader, kArchiveProperties, kAdditionalStreamsInfo, kMainStreamsInfo, kFilesInfo,
+  kPackInfo, kUnpackInfo, kSubStreamsInfo, kSize, kCRC, kFolder, kCodersUnpackSize,
+  kNumUnpackStream, kEmptyStream, kEmptyFile, kAnti, kName, kCTime, kATime, kMTime,
+  kWinAttributes, kComment, kEncodedHeader
+};
+// coder ids (7zDec.c:19-31)
+constexpr uint64_t kCopy = 0, kLzma = 0x30101, kLzma2 = 0x21, kBcj = 0x03030103,
+                   kArm = 0x03030501, kBcj2 = 0x0303011B;
+constexpr size_t kStartHeader = 32;
+constexpr uint32_t kNoFolder = 0xFFFFFFFFu;
+
+#define RINOK7(x)                  \
+  do {                             \
+    const SRes r_ = (x);           \
+    if (r_ != SZ_OK) return r_;    \
+  } while (0)
+
+struct Coder {
+  uint64_t method = 0;
+  uint32_t nin = 1, nout = 1;
+  std::vector<Byte> props;
+};
+struct BindPair {
+  uint32_t in = 0, out = 0;
+};
+struct Folder {
+  std::vector<Coder> coders;
+  std::vector<BindPair> bind;
+  std::vector<uint32_t> pack_streams;
+  std::vector<uint64_t> unpack_sizes;
+  bool crc_defined = false;
+  uint32_t crc = 0;
+  uint32_t num_unpack_streams = 1;
+  uint32_t num_out() const {
+    uint32_t n = 0;
+    for (const Coder& c : coders) n += c.nout;
+    return n;
+  }
+  bool bound_in(uint32_t i) const {
+    for (const BindPair& b : bind)
+      if (b.in == i) return true;
+    return false;
+  }
+  bool bound_out(uint32_t i) const {
+    for (const BindPair& b : bind)
+      if (b.out == i) return true;
+    return false;
+  }
+  // SzFolder_GetUnpackSize (7zIn.c:83-93): the one out stream nothing binds
+  uint64_t unpack_size() const {
+    for (int i = int(num_out()) - 1; i >= 0; --i)
+      if (!bound_out(uint32_t(i))) return i < int(unpack_sizes.size()) ? unpack_sizes[i] : 0;
+    return 0;
+  }
+};
+struct Ar {
+  std::vector<uint64_t> pack_sizes;
+  std::vector<Folder> folders;
+  uint64_t data_pos = 0;
+};
+struct SubStreams {
+  uint32_t n = 0;
+  std::vector<uint64_t> sizes;
+  std::vector<Byte> defined;
+  std::vector<uint32_t> digests;
+};
+struct FileItem {
+  bool has_stream = true, is_dir = false;
+  uint64_t size = 0;
+  uint32_t crc = 0;
+  bool crc_defined = false;
+};
+struct Archive {
+  Ar db;
+  std::vector<FileItem> files;
+  std::vector<Byte> names;           // FileNames: UTF-16LE
+  std::vector<size_t> name_offsets;  // FileNameOffsets (UTF-16 units), numFiles + 1
+  std::vector<uint32_t> folder_start_pack, folder_start_file, file_folder;
+  std::vector<uint64_t> pack_start;
+};
+
+// CSzData readers (7zIn.c:310-400)
+struct Sd {
+  const Byte* p;
+  size_t n;
+};
+SRes rd_byte(Sd& s, Byte* b) {
+  if (s.n == 0) return SZ_ERROR_ARCHIVE;
+  --s.n;
+  *b = *s.p++;
+  return SZ_OK;
+}
+SRes rd_bytes(Sd& s, Byte* d, size_t k) {
+  for (size_t i = 0; i < k; ++i) RINOK7(rd_byte(s, d + i));
+  return SZ_OK;
+}
+SRes rd_u32(Sd& s, uint32_t* v) {
+  *v = 0;
+  for (int i = 0; i < 4; ++i) {
+    Byte b;
+    RINOK7(rd_byte(s, &b));
+    *v |= uint32_t(b) << (8 * i);
+  }
+  return SZ_OK;
+}
+// SzReadNumber: leading one bits of the first byte = extra bytes
+SRes rd_num(Sd& s, uint64_t* v) {
+  Byte first, mask = 0x80;
+  RINOK7(rd_byte(s, &first));
+  *v = 0;
+  for (int i = 0; i < 8; ++i) {
+    if ((first & mask) == 0) {
+      *v += uint64_t(first & (mask - 1)) << (8 * i);
+      return SZ_OK;
+    }
+    Byte b;
+    RINOK7(rd_byte(s, &b));
+    *v |= uint64_t(b) << (8 * i);
+    mask >>= 1;
+  }
+  return SZ_OK;
+}
+SRes rd_num32(Sd& s, uint32_t* v) {
+  uint64_t x;
+  RINOK7(rd_num(s, &x));
+  if (x >= 0x80000000ull) return SZ_ERROR_UNSUPPORTED;
+  *v = uint32_t(x);
+  return SZ_OK;
+}
+SRes skip_size(Sd& s, uint64_t size) {
+  if (size > s.n) return SZ_ERROR_ARCHIVE;
+  s.n -= size_t(size);
+  s.p += size_t(size);
+  return SZ_OK;
+}
+SRes skip_data(Sd& s) {
+  uint64_t size;
+  RINOK7(rd_num(s, &size));
+  return skip_size(s, size);
+}
+SRes wait_attr(Sd& s, uint64_t attr) {
+  for (;;) {
+    uint64_t t;
+    RINOK7(rd_num(s, &t));
+    if (t == attr) return SZ_OK;
+    if (t == kEnd) return SZ_ERROR_ARCHIVE;
+    RINOK7(skip_data(s));
+  }
+}
+SRes bool_vec(Sd& s, size_t n, std::vector<Byte>* v) {
+  v->assign(n, 0);
+  Byte b = 0, mask = 0;
+  for (size_t i = 0; i < n; ++i) {
+    if (mask == 0) {
+      RINOK7(rd_byte(s, &b));
+      mask = 0x80;
+    }
+    (*v)[i] = (b & mask) ? 1 : 0;
+    mask >>= 1;
+  }
+  return SZ_OK;
+}
+SRes bool_vec2(Sd& s, size_t n, std::vector<Byte>* v) {
+  Byte all;
+  RINOK7(rd_byte(s, &all));
+  if (all == 0) return bool_vec(s, n, v);
+  v->assign(n, 1);
+  return SZ_OK;
+}
+SRes hash_digests(Sd& s, size_t n, std::vector<Byte>* defined, std::vector<uint32_t>* digests) {
+  RINOK7(bool_vec2(s, n, defined));
+  digests->assign(n, 0);
+  for (size_t i = 0; i < n; ++i)
+    if ((*defined)[i]) RINOK7(rd_u32(s, &(*digests)[i]));
+  return SZ_OK;
+}
+SRes rd_switch(Sd& s) {
+  Byte external;
+  RINOK7(rd_byte(s, &external));
+  return external == 0 ? SZ_OK : SZ_ERROR_UNSUPPORTED;
+}
+
+// SzReadPackInfo (7zIn.c:481-527)
+SRes read_pack_info(Sd& s, uint64_t* data_offset, Ar& a) {
+  uint32_t n;
+  RINOK7(rd_num(s, data_offset));
+  RINOK7(rd_num32(s, &n));
+  RINOK7(wait_attr(s, kSize));
+  a.pack_sizes.assign(n, 0);
+  for (uint32_t i = 0; i < n; ++i) RINOK7(rd_num(s, &a.pack_sizes[i]));
+  for (;;) {
+    uint64_t t;
+    RINOK7(rd_num(s, &t));
+    if (t == kEnd) break;
+    if (t == kCRC) {
+      std::vector<Byte> d;
+      std::vector<uint32_t> c;
+      RINOK7(hash_digests(s, n, &d, &c));  // pack CRCs: read, never checked by the reader
+      continue;
+    }
+    RINOK7(skip_data(s));
+  }
+  return SZ_OK;
+}
+
+// SzGetNextFolderItem (7zIn.c:536-644)
+SRes next_folder(Sd& s, Folder& f) {
+  uint32_t nc, n_in = 0, n_out = 0;
+  RINOK7(rd_num32(s, &nc));
+  if (nc > 32) return SZ_ERROR_UNSUPPORTED;
+  f.coders.assign(nc, Coder());
+  for (uint32_t i = 0; i < nc; ++i) {
+    Coder& c = f.coders[i];
+    Byte main;
+    RINOK7(rd_byte(s, &main));
+    const unsigned id_size = main & 0xF;
+    Byte id[15];
+    RINOK7(rd_bytes(s, id, id_size));
+    if (id_size > 8) return SZ_ERROR_UNSUPPORTED;
+    c.method = 0;
+    for (unsigned j = 0; j < id_size; ++j) c.method |= uint64_t(id[id_size - 1 - j]) << (8 * j);
+    if (main & 0x10) {
+      RINOK7(rd_num32(s, &c.nin));
+      RINOK7(rd_num32(s, &c.nout));
+      if (c.nin > 32 || c.nout > 32) return SZ_ERROR_UNSUPPORTED;
+    }
+    if (main & 0x20) {
+      uint64_t ps;
+      RINOK7(rd_num(s, &ps));
+      if (ps > s.n) return SZ_ERROR_ARCHIVE;
+      c.props.resize(size_t(ps));
+      RINOK7(rd_bytes(s, c.props.data(), size_t(ps)));
+    }
+    while (main & 0x80) {  // alternative methods: skipped
+      RINOK7(rd_byte(s, &main));
+      RINOK7(skip_size(s, main & 0xF));
+      if (main & 0x10) {
+        uint32_t x;
+        RINOK7(rd_num32(s, &x));
+        RINOK7(rd_num32(s, &x));
+      }
+      if (main & 0x20) {
+        uint64_t ps;
+        RINOK7(rd_num(s, &ps));
+        RINOK7(skip_size(s, ps));
+      }
+    }
+    n_in += c.nin;
+    n_out += c.nout;
+  }
+  if (n_out == 0) return SZ_ERROR_UNSUPPORTED;
+  f.bind.assign(n_out - 1, BindPair());
+  for (BindPair& b : f.bind) {
+    RINOK7(rd_num32(s, &b.in));
+    RINOK7(rd_num32(s, &b.out));
+  }
+  if (n_in < f.bind.size()) return SZ_ERROR_UNSUPPORTED;
+  const uint32_t np = n_in - uint32_t(f.bind.size());
+  f.pack_streams.assign(np, 0);
+  if (np == 1) {
+    uint32_t i = 0;
+    while (i < n_in && f.bound_in(i)) ++i;
+    if (i == n_in) return SZ_ERROR_UNSUPPORTED;
+    f.pack_streams[0] = i;
+  } else {
+    for (uint32_t i = 0; i < np; ++i) RINOK7(rd_num32(s, &f.pack_streams[i]));
+  }
+  return SZ_OK;
+}
+
+// SzReadUnpackInfo (7zIn.c:646-714)
+SRes read_unpack_info(Sd& s, Ar& a) {
+  uint32_t nf;
+  RINOK7(wait_attr(s, kFolder));
+  RINOK7(rd_num32(s, &nf));
+  RINOK7(rd_switch(s));
+  a.folders.assign(nf, Folder());
+  for (uint32_t i = 0; i < nf; ++i) RINOK7(next_folder(s, a.folders[i]));
+  RINOK7(wait_attr(s, kCodersUnpackSize));
+  for (Folder& f : a.folders) {
+    f.unpack_sizes.assign(f.num_out(), 0);
+    for (uint64_t& u : f.unpack_sizes) RINOK7(rd_num(s, &u));
+  }
+  for (;;) {
+    uint64_t t;
+    RINOK7(rd_num(s, &t));
+    if (t == kEnd) return SZ_OK;
+    if (t == kCRC) {
+      std::vector<Byte> d;
+      std::vector<uint32_t> c;
+      RINOK7(hash_digests(s, nf, &d, &c));
+      for (uint32_t i = 0; i < nf; ++i) {
+        a.folders[i].crc_defined = d[i] != 0;
+        a.folders[i].crc = c[i];
+      }
+      continue;
+    }
+    RINOK7(skip_data(s));
+  }
+}
+
+// SzReadSubStreamsInfo (7zIn.c:716-860)
+SRes read_substreams(Sd& s, Ar& a, SubStreams& ss) {
+  uint64_t t = 0;
+  for (Folder& f : a.folders) f.num_unpack_streams = 1;
+  ss.n = uint32_t(a.folders.size());
+  for (;;) {
+    RINOK7(rd_num(s, &t));
+    if (t == kNumUnpackStream) {
+      ss.n = 0;
+      for (Folder& f : a.folders) {
+        RINOK7(rd_num32(s, &f.num_unpack_streams));
+        ss.n += f.num_unpack_streams;
+      }
+      continue;
+    }
+    if (t == kCRC || t == kSize || t == kEnd) break;
+    RINOK7(skip_data(s));
+  }
+  ss.sizes.assign(ss.n, 0);
+  ss.defined.assign(ss.n, 0);
+  ss.digests.assign(ss.n, 0);
+  uint32_t si = 0;
+  for (Folder& f : a.folders) {
+    const uint32_t k = f.num_unpack_streams;
+    if (k == 0) continue;
+    uint64_t sum = 0;
+    if (t == kSize)
+      for (uint32_t j = 1; j < k; ++j) {
+        uint64_t size;
+        RINOK7(rd_num(s, &size));
+        if (si < ss.n) ss.sizes[si] = size;
+        ++si;
+        sum += size;
+      }
+    if (si < ss.n) ss.sizes[si] = f.unpack_size() - sum;
+    ++si;
+  }
+  if (t == kSize) RINOK7(rd_num(s, &t));
+  uint32_t n_digests = 0;
+  for (const Folder& f : a.folders)
+    if (f.num_unpack_streams != 1 || !f.crc_defined) n_digests += f.num_unpack_streams;
+  si = 0;
+  for (;;) {
+    if (t == kCRC) {
+      std::vector<Byte> d2;
+      std::vector<uint32_t> c2;
+      RINOK7(hash_digests(s, n_digests, &d2, &c2));
+      size_t di = 0;
+      for (const Folder& f : a.folders) {
+        if (f.num_unpack_streams == 1 && f.crc_defined) {
+          if (si < ss.n) {
+            ss.defined[si] = 1;
+            ss.digests[si] = f.crc;
+          }
+          ++si;
+        } else {
+          for (uint32_t j = 0; j < f.num_unpack_streams; ++j, ++di, ++si)
+            if (si < ss.n && di < d2.size()) {
+              ss.defined[si] = d2[di];
+              ss.digests[si] = c2[di];
+            }
+        }
+      }
+    } else if (t == kEnd) {
+      return SZ_OK;
+    } else {
+      RINOK7(skip_data(s));
+    }
+    RINOK7(rd_num(s, &t));
+  }
+}
+
+// SzReadStreamsInfo (7zIn.c:862-917)
+SRes read_streams_info(Sd& s, uint64_t* data_offset, Ar& a, SubStreams& ss, bool* have_ss) {
+  for (;;) {
+    uint64_t t;
+    RINOK7(rd_num(s, &t));
+    if (t > 0x7FFFFFFFull) return SZ_ERROR_UNSUPPORTED;
+    switch (t) {
+      case kEnd:
+        return SZ_OK;
+      case kPackInfo:
+        RINOK7(read_pack_info(s, data_offset, a));
+        break;
+      case kUnpackInfo:
+        RINOK7(read_unpack_info(s, a));
+        break;
+      case kSubStreamsInfo:
+        RINOK7(read_substreams(s, a, ss));
+        *have_ss = true;
+        break;
+      default:
+        return SZ_ERROR_UNSUPPORTED;
+    }
+  }
+}
+
+// SzReadFileNames (7zIn.c:919-938); size in UTF-16 units
+SRes read_file_names(const Byte* p, size_t size, uint32_t n, std::vector<size_t>* off) {
+  off->assign(size_t(n) + 1, 0);
+  size_t pos = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    (*off)[i] = pos;
+    for (;;) {
+      if (pos >= size) return SZ_ERROR_ARCHIVE;
+      if (p[pos * 2] == 0 && p[pos * 2 + 1] == 0) break;
+      ++pos;
+    }
+    ++pos;
+  }
+  (*off)[n] = pos;
+  return pos == size ? SZ_OK : SZ_ERROR_ARCHIVE;
+}
+
+// SzArEx_Fill (7zIn.c:179-247)
+SRes fill(Archive& x) {
+  const Ar& a = x.db;
+  x.folder_start_pack.assign(a.folders.size(), 0);
+  uint32_t sp = 0;
+  for (size_t i = 0; i < a.folders.size(); ++i) {
+    x.folder_start_pack[i] = sp;
+    sp += uint32_t(a.folders[i].pack_streams.size());
+  }
+  x.pack_start.assign(a.pack_sizes.size(), 0);
+  uint64_t pos = 0;
+  for (size_t i = 0; i < a.pack_sizes.size(); ++i) {
+    x.pack_start[i] = pos;
+    pos += a.pack_sizes[i];
+  }
+  x.folder_start_file.assign(a.folders.size(), 0);
+  x.file_folder.assign(x.files.size(), kNoFolder);
+  uint32_t fi = 0, in_folder = 0;
+  for (size_t i = 0; i < x.files.size(); ++i) {
+    const bool empty = !x.files[i].has_stream;
+    if (empty && in_folder == 0) continue;
+    if (in_folder == 0) {
+      for (;;) {
+        if (fi >= a.folders.size()) return SZ_ERROR_ARCHIVE;
+        x.folder_start_file[fi] = uint32_t(i);
+        if (a.folders[fi].num_unpack_streams != 0) break;
+        ++fi;
+      }
+    }
+    x.file_folder[i] = fi;
+    if (empty) continue;
+    if (++in_folder >= a.folders[fi].num_unpack_streams) {
+      ++fi;
+      in_folder = 0;
+    }
+  }
+  return SZ_OK;
+}
+
+// SzReadHeader2 (7zIn.c:940-1120)
+SRes read_header(Archive& x, Sd& s) {
+  uint64_t t;
+  SubStreams ss;
+  bool have_ss = false;
+  RINOK7(rd_num(s, &t));
+  if (t == kArchiveProperties) {
+    for (;;) {  // SzReadArchiveProperties: the skip result is not checked there
+      uint64_t u;
+      RINOK7(rd_num(s, &u));
+      if (u == kEnd) break;
+      (void)skip_data(s);
+    }
+    RINOK7(rd_num(s, &t));
+  }
+  if (t == kMainStreamsInfo) {
+    RINOK7(read_streams_info(s, &x.db.data_pos, x.db, ss, &have_ss));
+    x.db.data_pos += kStartHeader;
+    RINOK7(rd_num(s, &t));
+  }
+  if (t == kEnd) return SZ_OK;
+  if (t != kFilesInfo) return SZ_ERROR_ARCHIVE;
+  uint32_t nf;
+  RINOK7(rd_num32(s, &nf));
+  x.files.assign(nf, FileItem());
+  std::vector<Byte> empty_stream, empty_file, defined;
+  uint32_t n_empty = 0;
+  for (;;) {
+    uint64_t type, size;
+    RINOK7(rd_num(s, &type));
+    if (type == kEnd) break;
+    RINOK7(rd_num(s, &size));
+    if (size > s.n) return SZ_ERROR_ARCHIVE;
+    if (type > 0x7FFFFFFFull) {
+      RINOK7(skip_size(s, size));
+      continue;
+    }
+    switch (type) {
+      case kName: {
+        RINOK7(rd_switch(s));
+        const size_t ns = size_t(size) - 1;
+        if (ns & 1) return SZ_ERROR_ARCHIVE;
+        if (ns > s.n) return SZ_ERROR_ARCHIVE;
+        x.names.assign(s.p, s.p + ns);
+        RINOK7(read_file_names(s.p, ns >> 1, nf, &x.name_offsets));
+        RINOK7(skip_size(s, ns));
+        break;
+      }
+      case kEmptyStream:
+        RINOK7(bool_vec(s, nf, &empty_stream));
+        n_empty = 0;
+        for (Byte b : empty_stream) n_empty += b;
+        break;
+      case kEmptyFile:
+        RINOK7(bool_vec(s, n_empty, &empty_file));
+        break;
+      case kWinAttributes:
+      case kMTime: {
+        RINOK7(bool_vec2(s, nf, &defined));
+        RINOK7(rd_switch(s));
+        for (uint32_t i = 0; i < nf; ++i)
+          if (defined[i]) {
+            uint32_t v;
+            RINOK7(rd_u32(s, &v));
+            if (type == kMTime) RINOK7(rd_u32(s, &v));
+          }
+        break;
+      }
+      default:
+        RINOK7(skip_size(s, size));
+    }
+  }
+  uint32_t ei = 0, si = 0;
+  for (uint32_t i = 0; i < nf; ++i) {
+    FileItem& f = x.files[i];
+    f.has_stream = empty_stream.empty() ? true : empty_stream[i] == 0;
+    if (f.has_stream) {
+      // the reference indexes its substream arrays here unchecked
+      if (!have_ss || si >= ss.n) return SZ_ERROR_ARCHIVE;
+      f.is_dir = false;
+      f.size = ss.sizes[si];
+      f.crc = ss.digests[si];
+      f.crc_defined = ss.defined[si] != 0;
+      ++si;
+    } else {
+      f.is_dir = empty_file.empty() ? true : (ei < empty_file.size() ? empty_file[ei] == 0 : true);
+      ++ei;
+      f.size = 0;
+      f.crc = 0;
+      f.crc_defined = false;
+    }
+  }
+  return fill(x);
+}
+
+// One folder's decode job (SzFolder_Decode2's 1- and 2-coder shapes)
+struct Job {
+  uint64_t pack_off = 0, pack_size = 0, avail = 0, unpack = 0, dst_off = 0;
+  uint64_t method = 0;
+  std::vector<Byte> props;
+  bool x86 = false;
+  SRes res = SZ_OK;
+};
+
+// CheckSupportedFolder (7zDec.c:269-322) + the coder checks SzDecodeLzma /
+// SzDecodeLzma2 make before decoding.  ARM and BCJ2 folders pass the
+// reference's check but are not built here: SZ_ERROR_UNSUPPORTED.
+Job make_job(const Archive& x, const Ar& a, uint32_t fi, uint64_t start, const Byte*, size_t size) {
+  Job j;
+  const Folder& f = a.folders[fi];
+  j.unpack = f.unpack_size();
+  auto main_ok = [](const Coder& c) {
+    return c.nin == 1 && c.nout == 1 && c.method <= 0xFFFFFFFFull &&
+           (c.method == kCopy || c.method == kLzma || c.method == kLzma2);
+  };
+  const size_t nc = f.coders.size();
+  j.res = SZ_ERROR_UNSUPPORTED;
+  if (nc < 1 || nc > 4 || !main_ok(f.coders[0])) return j;
+  if (nc == 1) {
+    if (f.pack_streams.size() != 1 || f.pack_streams[0] != 0 || !f.bind.empty()) return j;
+  } else if (nc == 2) {
+    const Coder& c = f.coders[1];
+    if (c.method > 0xFFFFFFFFull || c.nin != 1 || c.nout != 1 || f.pack_streams.size() != 1 ||
+        f.pack_streams[0] != 0 || f.bind.size() != 1 || f.bind[0].in != 1 || f.bind[0].out != 0)
+      return j;
+    if (c.method != kBcj) return j;  // k_ARM: passes the reference's check, not built here
+    j.x86 = true;
+  } else {
+    return j;  // the BCJ2 layout (4 coders): not built here
+  }
+  (void)kArm;
+  (void)kBcj2;
+  const Coder& c = f.coders[0];
+  j.method = c.method;
+  j.props = c.props;
+  const uint32_t ps = x.folder_start_pack.empty() ? 0 : x.folder_start_pack[fi];
+  j.pack_size = ps < a.pack_sizes.size() ? a.pack_sizes[ps] : 0;
+  j.pack_off = start;
+  j.avail = start >= size ? 0 : std::min<uint64_t>(j.pack_size, size - start);
+  j.res = SZ_OK;
+  if (c.method == kCopy) {
+    if (j.pack_size != j.unpack) j.res = SZ_ERROR_DATA;
+    else if (j.avail < j.pack_size) j.res = SZ_ERROR_INPUT_EOF;
+  } else if (c.method == kLzma) {
+    // LzmaProps_Decode (LzmaDec.c:898-922)
+    if (c.props.size() < 5 || c.props[0] >= 9 * 5 * 5) j.res = SZ_ERROR_UNSUPPORTED;
+  } else {
+    // SzDecodeLzma2 (7zDec.c:181-183) + Lzma2Dec_GetOldProps (Lzma2Dec.c:69)
+    if (c.props.size() != 1) j.res = SZ_ERROR_DATA;
+    else if (c.props[0] > 40) j.res = SZ_ERROR_UNSUPPORTED;
+  }
+  return j;
+}
+
+// Runs the folder jobs on the GPU from the archive already in d_arc, output
+// at each job's dst_off in d_dst; sets each job's res to SzFolder_Decode's.
+SRes run_jobs(std::vector<Job>& jobs, const Byte* d_arc, Byte* d_dst) {
+  std::vector<LzmaGpuStreamDesc> descs;
+  std::vector<size_t> which;
+  std::vector<uint64_t> bcj_off, bcj_len;
+  for (size_t i = 0; i < jobs.size(); ++i) {
+    Job& j = jobs[i];
+    if (j.res != SZ_OK) continue;
+    if (j.method == kCopy) {
+      if (j.unpack && !hip_ok(hipMemcpyAsync(d_dst + j.dst_off, d_arc + j.pack_off, j.unpack,
+                                             hipMemcpyDeviceToDevice, nullptr),
+                              "7z copy folder"))
+        return SZ_ERROR_FAIL;
+    } else {
+      LzmaGpuStreamDesc d;
+      memset(&d, 0, sizeof d);
+      d.src_off = j.pack_off;
+      d.src_len = j.avail;
+      d.dst_off = j.dst_off;
+      d.dst_cap = j.unpack;
+      d.finish_mode = LZMA_FINISH_END;
+      if (j.method == kLzma) {
+        memcpy(d.props, j.props.data(), 5);
+        d.props_size = 5;
+        d.kind = LZMA_GPU_KIND_LZMA;
+      } else {
+        d.props[0] = j.props[0];
+        d.props_size = 1;
+        d.kind = LZMA_GPU_KIND_LZMA2;
+      }
+      descs.push_back(d);
+      which.push_back(i);
+    }
+    if (j.x86 && j.unpack) {
+      bcj_off.push_back(j.dst_off);
+      bcj_len.push_back(j.unpack);
+    }
+  }
+  const size_t n = descs.size(), nb = bcj_off.size();
+  std::vector<LzmaGpuResult> res(n);
+  if (n) {
+    std::vector<uint32_t> order(n);
+    LzmaGpuPlan plan;
+    SRes r = LzmaGpu_PlanBatchEx(descs.data(), n, order.data(), &plan);
+    if (r != SZ_OK) return r;
+    DevArr<Byte> d_ws;
+    DevArr<LzmaGpuStreamDesc> d_desc;
+    DevArr<uint32_t> d_order;
+    DevArr<LzmaGpuResult> d_res;
+    if (!d_ws.alloc(plan.workspace_bytes) || !d_desc.alloc(n) || !d_order.alloc(n) ||
+        !d_res.alloc(n)) {
+      set_error("7z: device allocation failed");
+      return SZ_ERROR_MEM;
+    }
+    if (!hip_ok(hipMemcpy(d_desc.p, descs.data(), n * sizeof(LzmaGpuStreamDesc),
+                          hipMemcpyHostToDevice), "7z H2D") ||
+        !hip_ok(hipMemcpy(d_order.p, order.data(), n * 4, hipMemcpyHostToDevice), "7z H2D"))
+      return SZ_ERROR_FAIL;
+    if ((r = LzmaGpu_DecodeBatchEx(&plan, d_desc.p, d_order.p, d_arc, d_dst, d_ws.p, d_res.p,
+                                   nullptr)) != SZ_OK)
+      return r;
+    if (!hip_ok(hipDeviceSynchronize(), "7z decode") ||
+        !hip_ok(hipMemcpy(res.data(), d_res.p, n * sizeof(LzmaGpuResult), hipMemcpyDeviceToHost),
+                "7z D2H"))
+      return SZ_ERROR_FAIL;
+  }
+  if (nb) {  // x86_Convert(outBuffer, outSize, 0, &state0, 0) per BCJ folder
+    DevArr<uint64_t> d64;
+    DevArr<uint32_t> d32;
+    std::vector<uint64_t> h64(bcj_off);
+    h64.insert(h64.end(), bcj_len.begin(), bcj_len.end());
+    h64.resize(3 * nb, 0);
+    std::vector<uint32_t> h32(2 * nb, 0);
+    if (!d64.alloc(3 * nb) || !d32.alloc(2 * nb)) return SZ_ERROR_MEM;
+    if (!hip_ok(hipMemcpy(d64.p, h64.data(), h64.size() * 8, hipMemcpyHostToDevice), "7z H2D") ||
+        !hip_ok(hipMemcpy(d32.p, h32.data(), h32.size() * 4, hipMemcpyHostToDevice), "7z H2D"))
+      return SZ_ERROR_FAIL;
+    SRes r = BcjGpu_X86Batch(d_dst, d64.p, d64.p + nb, d32.p, d32.p + nb, d64.p + 2 * nb, nb, 0,
+                             nullptr);
+    if (r != SZ_OK) return r;
+    if (!hip_ok(hipDeviceSynchronize(), "7z BCJ")) return SZ_ERROR_FAIL;
+  } else if (!hip_ok(hipDeviceSynchronize(), "7z copy")) {
+    return SZ_ERROR_FAIL;
+  }
+  // SzDecodeLzma / SzDecodeLzma2 acceptance (7zDec.c:161-168, 209-216): the
+  // whole output, the whole pack stream, a finished status
+  for (size_t k = 0; k < n; ++k) {
+    Job& j = jobs[which[k]];
+    const LzmaGpuResult& q = res[k];
+    if (q.res != SZ_OK) {
+      j.res = q.res;
+      continue;
+    }
+    const bool status_ok = j.method == kLzma
+                               ? (q.status == LZMA_STATUS_FINISHED_WITH_MARK ||
+                                  q.status == LZMA_STATUS_MAYBE_FINISHED_WITHOUT_MARK)
+                               : q.status == LZMA_STATUS_FINISHED_WITH_MARK;
+    if (q.dest_len != j.unpack || q.src_len != j.avail || j.avail != j.pack_size || !status_ok)
+      j.res = SZ_ERROR_DATA;
+  }
+  return SZ_OK;
+}
+
+// SzArEx_Open2 (7zIn.c:1214-1312)
+SRes open_archive(const Byte* arc, size_t size, Archive& x) {
+  if (size < kStartHeader) return SZ_ERROR_NO_ARCHIVE;
+  static const Byte sig[6] = {'7', 'z', 0xBC, 0xAF, 0x27, 0x1C};
+  if (memcmp(arc, sig, 6) != 0) return SZ_ERROR_NO_ARCHIVE;
+  if (arc[6] != 0) return SZ_ERROR_UNSUPPORTED;
+  uint64_t off = 0, hsize = 0;
+  uint32_t hcrc = 0, scrc = 0;
+  for (int i = 7; i >= 0; --i) off = (off << 8) | arc[12 + i];
+  for (int i = 7; i >= 0; --i) hsize = (hsize << 8) | arc[20 + i];
+  for (int i = 3; i >= 0; --i) hcrc = (hcrc << 8) | arc[28 + i];
+  for (int i = 3; i >= 0; --i) scrc = (scrc << 8) | arc[8 + i];
+  if (crc32_host(arc + 12, 20) != scrc) return SZ_ERROR_CRC;
+  if (hsize == 0) return SZ_OK;
+  if (off > off + hsize || off > off + hsize + kStartHeader) return SZ_ERROR_NO_ARCHIVE;
+  if (uint64_t(size) < off + kStartHeader + hsize || uint64_t(size) < off + kStartHeader)
+    return SZ_ERROR_INPUT_EOF;
+  const Byte* h = arc + kStartHeader + off;
+  if (crc32_host(h, size_t(hsize)) != hcrc) return SZ_ERROR_ARCHIVE;
+  Sd s{h, size_t(hsize)};
+  uint64_t t;
+  RINOK7(rd_num(s, &t));
+  std::vector<Byte> unpacked;
+  if (t == kEncodedHeader) {
+    // SzReadAndDecodePackedStreams2 (7zIn.c:1147-1189): one folder, on the GPU
+    Archive hx;
+    SubStreams ss;
+    bool have_ss = false;
+    uint64_t start = 0;
+    RINOK7(read_streams_info(s, &start, hx.db, ss, &have_ss));
+    start += kStartHeader;
+    if (hx.db.folders.size() != 1) return SZ_ERROR_ARCHIVE;
+    hx.folder_start_pack.assign(1, 0);
+    std::vector<Job> jobs(1, make_job(hx, hx.db, 0, start, arc, size));
+    const Folder& f = hx.db.folders[0];
+    if (jobs[0].res != SZ_OK) return jobs[0].res;
+    unpacked.resize(size_t(f.unpack_size()));
+    if (!ensure_device()) return SZ_ERROR_FAIL;
+    DevArr<Byte> d_arc, d_out;
+    if (!d_arc.alloc(size) || !d_out.alloc(unpacked.size())) return SZ_ERROR_MEM;
+    if (!hip_ok(hipMemcpy(d_arc.p, arc, size, hipMemcpyHostToDevice), "7z H2D"))
+      return SZ_ERROR_FAIL;
+    RINOK7(run_jobs(jobs, d_arc.p, d_out.p));
+    if (jobs[0].res != SZ_OK) return jobs[0].res;
+    if (!unpacked.empty() &&
+        !hip_ok(hipMemcpy(unpacked.data(), d_out.p, unpacked.size(), hipMemcpyDeviceToHost),
+                "7z D2H"))
+      return SZ_ERROR_FAIL;
+    if (f.crc_defined && crc32_host(unpacked.data(), unpacked.size()) != f.crc)
+      return SZ_ERROR_CRC;
+    s = Sd{unpacked.data(), unpacked.size()};
+    RINOK7(rd_num(s, &t));
+  }
+  if (t != kHeader) return SZ_ERROR_UNSUPPORTED;
+  return read_header(x, s);
+}
+
+SRes open_checked(const Byte* arc, size_t size, Archive& x) {
+  const SRes r = open_archive(arc, size, x);
+  if (r != SZ_OK) x = Archive();
+  return r;
+}
+
+}  // namespace
+
+SRes LzmaGpu_7zOpen(const Byte* archive, size_t size, LzmaGpu7zFolder* folders, size_t folder_cap,
+                    size_t* n_folders, LzmaGpu7zFile* files, size_t file_cap, size_t* n_files,
+                    UInt16* names, size_t names_cap, size_t* names_len, UInt64* unpack_total) {
+  Archive x;
+  const SRes r = open_checked(archive, size, x);
+  if (n_folders) *n_folders = x.db.folders.size();
+  if (n_files) *n_files = x.files.size();
+  if (names_len) *names_len = x.names.size() / 2;
+  uint64_t total = 0;
+  std::vector<uint64_t> fdst(x.db.folders.size(), 0);
+  for (size_t i = 0; i < x.db.folders.size(); ++i) {
+    fdst[i] = total;
+    total += x.db.folders[i].unpack_size();
+  }
+  if (unpack_total) *unpack_total = total;
+  if (r != SZ_OK) return r;
+  for (size_t i = 0; i < x.db.folders.size() && folders && i < folder_cap; ++i) {
+    const Folder& f = x.db.folders[i];
+    const Job j = make_job(x, x.db, uint32_t(i),
+                           x.db.data_pos + (x.folder_start_pack[i] < x.pack_start.size()
+                                                ? x.pack_start[x.folder_start_pack[i]]
+                                                : 0),
+                           archive, size);
+    LzmaGpu7zFolder& o = folders[i];
+    memset(&o, 0, sizeof o);
+    o.pack_off = j.pack_off;
+    o.pack_size = j.pack_size;
+    o.unpack_size = f.unpack_size();
+    o.dst_off = fdst[i];
+    o.method = f.coders.empty() ? 0 : f.coders[0].method;
+    o.x86 = j.x86 ? 1 : 0;
+    o.supported = uint32_t(j.res);
+    o.crc_defined = f.crc_defined ? 1 : 0;
+    o.crc = f.crc;
+    o.first_file = x.folder_start_file[i];
+    o.num_files = f.num_unpack_streams;
+    o.num_coders = uint32_t(f.coders.size());
+    const std::vector<Byte>& p = f.coders.empty() ? std::vector<Byte>() : f.coders[0].props;
+    o.props_size = uint32_t(p.size());
+    memcpy(o.props, p.data(), std::min<size_t>(p.size(), sizeof o.props));
+  }
+  for (size_t i = 0; i < x.files.size() && files && i < file_cap; ++i) {
+    const FileItem& f = x.files[i];
+    LzmaGpu7zFile& o = files[i];
+    memset(&o, 0, sizeof o);
+    o.size = f.size;
+    o.folder = x.file_folder[i];
+    if (o.folder != kNoFolder) {
+      uint64_t off = fdst[o.folder];
+      for (uint32_t k = x.folder_start_file[o.folder]; k < i; ++k) off += x.files[k].size;
+      o.dst_off = off;
+    }
+    o.crc = f.crc;
+    o.crc_defined = f.crc_defined ? 1 : 0;
+    o.has_stream = f.has_stream ? 1 : 0;
+    o.is_dir = f.is_dir ? 1 : 0;
+    if (!x.name_offsets.empty()) {
+      o.name_off = uint32_t(x.name_offsets[i]);
+      o.name_len = uint32_t(x.name_offsets[i + 1] - x.name_offsets[i]);
+    }
+  }
+  if (names)
+    for (size_t i = 0; i < x.names.size() / 2 && i < names_cap; ++i)
+      names[i] = UInt16(x.names[2 * i] | (x.names[2 * i + 1] << 8));
+  return SZ_OK;
+}
+
+SRes LzmaGpu_7zExtract(Byte* dest, SizeT* destLen, const Byte* archive, size_t size,
+                       SRes* file_res, size_t file_cap) {
+  const SizeT cap = *destLen;
+  *destLen = 0;
+  Archive x;
+  SRes r = open_checked(archive, size, x);
+  if (r != SZ_OK) return r;
+  const Ar& a = x.db;
+  const size_t nf = a.folders.size(), nfiles = x.files.size();
+  std::vector<Job> jobs(nf);
+  uint64_t total = 0;
+  for (size_t i = 0; i < nf; ++i) {
+    const uint64_t start = a.data_pos + (x.folder_start_pack[i] < x.pack_start.size()
+                                             ? x.pack_start[x.folder_start_pack[i]]
+                                             : 0);
+    jobs[i] = make_job(x, a, uint32_t(i), start, archive, size);
+    jobs[i].dst_off = total;
+    total += jobs[i].unpack;
+  }
+  if (total > cap) return SZ_ERROR_OUTPUT_EOF;
+  // file ranges inside their folder's output (SzArEx_Extract's offset walk)
+  std::vector<uint64_t> foff(nfiles, 0);
+  std::vector<SRes> fres(nfiles, SZ_OK);
+  for (size_t i = 0; i < nfiles; ++i) {
+    const uint32_t fo = x.file_folder[i];
+    if (fo == kNoFolder) continue;
+    uint64_t off = 0;
+    for (uint32_t k = x.folder_start_file[fo]; k < i; ++k) off += uint32_t(x.files[k].size);
+    foff[i] = off;
+  }
+  if (nf) {
+    if (!ensure_device()) return SZ_ERROR_FAIL;
+    DevArr<Byte> d_arc, d_dst;
+    if (!d_arc.alloc(size) || !d_dst.alloc(total)) {
+      set_error("7z: device allocation failed");
+      return SZ_ERROR_MEM;
+    }
+    if (!hip_ok(hipMemcpy(d_arc.p, archive, size, hipMemcpyHostToDevice), "7z H2D"))
+      return SZ_ERROR_FAIL;
+    RINOK7(run_jobs(jobs, d_arc.p, d_dst.p));
+    // CRC-32 of every decoded folder with a CRC and of every file range
+    std::vector<uint64_t> off, len;
+    std::vector<int64_t> tag;  // >= 0: folder, < 0: ~file
+    for (size_t i = 0; i < nf; ++i)
+      if (jobs[i].res == SZ_OK && a.folders[i].crc_defined) {
+        off.push_back(jobs[i].dst_off);
+        len.push_back(jobs[i].unpack);
+        tag.push_back(int64_t(i));
+      }
+    for (size_t i = 0; i < nfiles; ++i) {
+      const uint32_t fo = x.file_folder[i];
+      if (fo == kNoFolder || jobs[fo].res != SZ_OK || !x.files[i].crc_defined) continue;
+      if (foff[i] + x.files[i].size > jobs[fo].unpack) continue;
+      off.push_back(jobs[fo].dst_off + foff[i]);
+      len.push_back(x.files[i].size);
+      tag.push_back(~int64_t(i));
+    }
+    const size_t nc = off.size();
+    std::vector<uint32_t> crc(nc);
+    if (nc) {
+      const size_t nch = CrcGpu_PlanChunks(len.data(), nc, nullptr, nullptr);
+      if (nch == size_t(-1)) return SZ_ERROR_PARAM;
+      std::vector<uint32_t> cb(nc + nch);
+      CrcGpu_PlanChunks(len.data(), nc, cb.data(), cb.data() + nc);
+      std::vector<uint64_t> ol(off);
+      ol.insert(ol.end(), len.begin(), len.end());
+      DevArr<uint64_t> d_ol;
+      DevArr<uint32_t> d_cb, d_chunk, d_crc;
+      if (!d_ol.alloc(2 * nc) || !d_cb.alloc(cb.size()) || !d_chunk.alloc(nch) ||
+          !d_crc.alloc(nc))
+        return SZ_ERROR_MEM;
+      if (!hip_ok(hipMemcpy(d_ol.p, ol.data(), ol.size() * 8, hipMemcpyHostToDevice), "7z H2D") ||
+          !hip_ok(hipMemcpy(d_cb.p, cb.data(), cb.size() * 4, hipMemcpyHostToDevice), "7z H2D"))
+        return SZ_ERROR_FAIL;
+      if ((r = CrcGpu_Batch(d_dst.p, d_ol.p, d_ol.p + nc, nc, d_cb.p, d_cb.p + nc, nch,
+                            0xFFFFFFFFu, 0xFFFFFFFFu, d_chunk.p, d_crc.p, nullptr)) != SZ_OK)
+        return r;
+      if (!hip_ok(hipDeviceSynchronize(), "7z CRC") ||
+          !hip_ok(hipMemcpy(crc.data(), d_crc.p, nc * 4, hipMemcpyDeviceToHost), "7z D2H"))
+        return SZ_ERROR_FAIL;
+    }
+    for (size_t k = 0; k < nc; ++k)
+      if (tag[k] >= 0 && crc[k] != a.folders[size_t(tag[k])].crc) jobs[size_t(tag[k])].res = SZ_ERROR_CRC;
+    for (size_t i = 0; i < nfiles; ++i) {
+      const uint32_t fo = x.file_folder[i];
+      if (fo == kNoFolder) continue;
+      if (jobs[fo].res != SZ_OK) {
+        fres[i] = jobs[fo].res;
+      } else if (foff[i] + x.files[i].size > jobs[fo].unpack) {
+        fres[i] = SZ_ERROR_FAIL;
+      }
+    }
+    for (size_t k = 0; k < nc; ++k)
+      if (tag[k] < 0) {
+        const size_t i = size_t(~tag[k]);
+        if (fres[i] == SZ_OK && crc[k] != x.files[i].crc) fres[i] = SZ_ERROR_CRC;
+      }
+    if (total && !hip_ok(hipMemcpy(dest, d_dst.p, total, hipMemcpyDeviceToHost), "7z D2H"))
+      return SZ_ERROR_FAIL;
+  }
+  SRes first = SZ_OK;
+  for (size_t i = 0; i < nfiles; ++i) {
+    if (file_res && i < file_cap) file_res[i] = fres[i];
+    if (first == SZ_OK) first = fres[i];
+  }
+  *destLen = SizeT(total);
+  return first;
+}

@@ -22,6 +22,8 @@
 using lzgpu_host::ensure_device;
 using lzgpu_host::hip_ok;
 using lzgpu_host::set_error;
+using lzgpu_host::crc32_host;
+using lzgpu_host::DevArr;
 
 namespace {
 
@@ -29,23 +31,6 @@ constexpr size_t kXzHeader = 12, kXzFooter = 12;
 
 uint32_t le32(const Byte* p) {
   return uint32_t(p[0]) | (uint32_t(p[1]) << 8) | (uint32_t(p[2]) << 16) | (uint32_t(p[3]) << 24);
-}
-
-// host CRC-32 for container metadata (7zCrc.c semantics; a few bytes per block)
-uint32_t crc32_host(const Byte* p, size_t n) {
-  static uint32_t t[256];
-  static bool init = false;
-  if (!init) {
-    for (uint32_t v = 0; v < 256; ++v) {
-      uint32_t r = v;
-      for (int j = 0; j < 8; ++j) r = (r >> 1) ^ ((r & 1u) ? 0xEDB88320u : 0u);
-      t[v] = r;
-    }
-    init = true;
-  }
-  uint32_t c = 0xFFFFFFFFu;
-  for (size_t i = 0; i < n; ++i) c = t[(c ^ p[i]) & 0xFFu] ^ (c >> 8);
-  return c ^ 0xFFFFFFFFu;
 }
 
 // Xz_ReadVarInt (XzDec.c:30-44): 0 on failure
@@ -293,15 +278,6 @@ SRes index_file(const Byte* f, size_t size, std::vector<LzmaGpuXzBlock>* blocks,
   *total = dst;
   return SZ_OK;
 }
-
-template <class T>
-struct DevArr {
-  T* p = nullptr;
-  ~DevArr() {
-    if (p) (void)hipFree(p);
-  }
-  bool alloc(size_t n) { return hipMalloc(&p, std::max<size_t>(n, 1) * sizeof(T)) == hipSuccess; }
-};
 
 }  // namespace
 

@@ -116,7 +116,28 @@ class XzBlock(ctypes.Structure):
                 ("x86_ip", ctypes.c_uint32), ("stream", ctypes.c_uint32)]
 
 
+class SzFolder(ctypes.Structure):
+    """LzmaGpu7zFolder (include/lzma_gpu.h): one folder of an opened 7z archive."""
+    _fields_ = [("pack_off", ctypes.c_uint64), ("pack_size", ctypes.c_uint64),
+                ("unpack_size", ctypes.c_uint64), ("dst_off", ctypes.c_uint64),
+                ("method", ctypes.c_uint64), ("x86", ctypes.c_uint32),
+                ("supported", ctypes.c_uint32), ("crc_defined", ctypes.c_uint32),
+                ("crc", ctypes.c_uint32), ("first_file", ctypes.c_uint32),
+                ("num_files", ctypes.c_uint32), ("num_coders", ctypes.c_uint32),
+                ("props_size", ctypes.c_uint32), ("props", ctypes.c_ubyte * 8)]
+
+
+class SzFile(ctypes.Structure):
+    """LzmaGpu7zFile (include/lzma_gpu.h): one file entry of an opened 7z archive."""
+    _fields_ = [("size", ctypes.c_uint64), ("dst_off", ctypes.c_uint64),
+                ("folder", ctypes.c_uint32), ("crc", ctypes.c_uint32),
+                ("crc_defined", ctypes.c_uint32), ("has_stream", ctypes.c_uint32),
+                ("is_dir", ctypes.c_uint32), ("name_off", ctypes.c_uint32),
+                ("name_len", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
+
+
 assert ctypes.sizeof(XzBlock) == 72
+assert ctypes.sizeof(SzFolder) == 80 and ctypes.sizeof(SzFile) == 48
 assert ctypes.sizeof(StreamDesc) == 48 and ctypes.sizeof(Result) == 24
 assert ctypes.sizeof(Session) == 192 and ctypes.sizeof(Plan) == 184
 assert ctypes.sizeof(CLzmaDec) == 136
@@ -162,6 +183,10 @@ _sig = {
     "Crc64Gpu_Batch": (ctypes.c_int, [_P, _P, _P, ctypes.c_size_t, _P, _P, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_uint64, _P, _P, _P]),
     "LzmaGpu_XzIndex": (ctypes.c_int, [_P, ctypes.c_size_t, ctypes.POINTER(XzBlock), ctypes.c_size_t, _sp, ctypes.POINTER(ctypes.c_uint64)]),
     "LzmaGpu_XzDecode": (ctypes.c_int, [_P, _sp, _P, ctypes.c_size_t, ctypes.POINTER(ctypes.c_int64)]),
+    "LzmaGpu_7zOpen": (ctypes.c_int, [_P, ctypes.c_size_t, _P, ctypes.c_size_t, _sp, _P,
+                                      ctypes.c_size_t, _sp, _P, ctypes.c_size_t, _sp,
+                                      ctypes.POINTER(ctypes.c_uint64)]),
+    "LzmaGpu_7zExtract": (ctypes.c_int, [_P, _sp, _P, ctypes.c_size_t, _P, ctypes.c_size_t]),
     "LzmaGpu_DeviceCount": (ctypes.c_int, []),
     "LzmaGpu_LastError": (ctypes.c_char_p, []),
     "LzmaGpu_Version": (ctypes.c_char_p, []),
@@ -453,6 +478,35 @@ def XzDecode(data, dest_cap):
     bad = ctypes.c_int64(-1)
     r = _lib.LzmaGpu_XzDecode(out, ctypes.byref(dl), _buf(data), len(data), ctypes.byref(bad))
     return r, out.raw[:dl.value], bad.value
+
+
+def sz_open(data):
+    """LzmaGpu_7zOpen: (res, [SzFolder...], [SzFile...], names (UTF-16LE bytes),
+    unpack_total).  A packed header is decoded on the GPU."""
+    nfo, nfi, nn = ctypes.c_size_t(0), ctypes.c_size_t(0), ctypes.c_size_t(0)
+    tot = ctypes.c_uint64(0)
+    src = _buf(data)
+    r = _lib.LzmaGpu_7zOpen(src, len(data), None, 0, ctypes.byref(nfo), None, 0,
+                            ctypes.byref(nfi), None, 0, ctypes.byref(nn), ctypes.byref(tot))
+    if r != SZ_OK:
+        return r, [], [], b"", 0
+    fo = (SzFolder * max(nfo.value, 1))()
+    fi = (SzFile * max(nfi.value, 1))()
+    names = (ctypes.c_uint16 * max(nn.value, 1))()
+    r = _lib.LzmaGpu_7zOpen(src, len(data), fo, nfo.value, ctypes.byref(nfo), fi, nfi.value,
+                            ctypes.byref(nfi), names, nn.value, ctypes.byref(nn),
+                            ctypes.byref(tot))
+    raw = bytes(bytearray(ctypes.string_at(names, 2 * nn.value)))
+    return r, list(fo)[:nfo.value], list(fi)[:nfi.value], raw, tot.value
+
+
+def SzExtract(data, dest_cap, max_files=1 << 16):
+    """LzmaGpu_7zExtract: (res, extraction buffer, [per-file SRes])."""
+    out = ctypes.create_string_buffer(max(dest_cap, 1))
+    dl = ctypes.c_size_t(dest_cap)
+    fres = (ctypes.c_int * max_files)()
+    r = _lib.LzmaGpu_7zExtract(out, ctypes.byref(dl), _buf(data), len(data), fres, max_files)
+    return r, out.raw[:dl.value], list(fres)
 
 
 # ---------------------------------------------------------------- streaming sessions

@@ -30,7 +30,7 @@ def case_bytes(c):
 
 
 def main():
-    lib = ctypes.CDLL(native.REF_SO)
+    lib = native._load(native.REF_SO)
     lib.CrcGenerateTable.restype = None
     lib.CrcGenerateTable()
     upd, calc = native.crc_funcs(lib, "CrcUpdate", "CrcCalc")

@@ -57,7 +57,7 @@ def x86_like(seed, n):
 
 
 def main():
-    lib = ctypes.CDLL(native.REF_SO)
+    lib = native._load(native.REF_SO)
     lib.ref_xz_decode.restype = ctypes.c_int
     lib.ref_xz_decode.argtypes = [ctypes.c_char_p, _sp, ctypes.c_char_p, _sp, _ip, _ip]
     lib.ref_x86_convert.restype = ctypes.c_size_t

@@ -23,7 +23,9 @@ int_p = ctypes.POINTER(ctypes.c_int)
 
 def _load(path):
     if path not in _c:
-        _c[path] = ctypes.CDLL(path)
+        # lazy binding: the reference's 7zFile.c calls two Windows-only file
+        # openers (InFile_OpenW / OutFile_OpenW) on a path nothing here runs
+        _c[path] = ctypes.CDLL(path, mode=os.RTLD_LAZY)
     return _c[path]
 
 

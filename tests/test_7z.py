@@ -1,0 +1,166 @@
+"""7z archives as GPU folder batches.
+
+Reference: SzArEx_Open (7zIn.c:1214-1320) and SzArEx_Extract
+(7zIn.c:1322-1402) over SzFolder_Decode (7zDec.c:335-471), compiled in
+place and recorded in tests/golden/sz_cases.json + sz_blob.bin
+(tests/golden/make_golden_7z.py): the open result, every file's extract
+result and size, the bytes of the files that extract OK, the name buffer.
+
+CPU (no GPU): LzmaGpu_7zOpen on every archive whose header is not packed
+(the header walk is host code) against the reference's open result, file
+sizes and names.  GPU (-m gpu): LzmaGpu_7zExtract on every fixture, packed
+headers, and a many-folder archive decoded as one batch.
+"""
+import hashlib
+import json
+import os
+import struct
+import sys
+import zlib
+
+import pytest
+
+import native
+
+GOLDEN = os.path.join(native.ROOT, "tests", "golden")
+sys.path.insert(0, os.path.join(native.ROOT, "lzma-sdk-zliblike_amd"))
+
+
+def fixtures():
+    with open(os.path.join(GOLDEN, "sz_cases.json")) as f:
+        d = json.load(f)
+    with open(os.path.join(GOLDEN, "sz_blob.bin"), "rb") as f:
+        blob = f.read()
+    assert hashlib.sha256(blob).hexdigest() == d["blob_sha256"]
+    d["blob"] = blob
+    return d
+
+
+def arc_of(d, c):
+    return d["blob"][c["off"]:c["off"] + c["len"]]
+
+
+@pytest.fixture(scope="module")
+def L():
+    import lzmagpu
+    return lzmagpu
+
+
+def packed_header(arc):
+    """True when the archive's next header starts with kEncodedHeader (0x17)."""
+    if len(arc) < 32:
+        return False
+    off, size = struct.unpack("<QQ", arc[12:28])
+    return size > 0 and 32 + off < len(arc) and arc[32 + off] == 0x17
+
+
+def test_open_matches_reference(L):
+    d = fixtures()
+    checked = 0
+    for c in d["cases"]:
+        arc = arc_of(d, c)
+        if packed_header(arc):
+            continue  # decoded on the GPU: test_gpu_7z_fixtures
+        r, folders, files, names, total = L.sz_open(arc)
+        assert r == c["open_res"], (c["note"], r)
+        if r == 0:
+            assert [f.size for f in files] == c["file_size"], c["note"]
+            assert hashlib.sha256(names).hexdigest() == c["names_sha256"], c["note"]
+            assert total == sum(f.unpack_size for f in folders)
+            for f in files:
+                if f.folder != 0xFFFFFFFF:
+                    fo = folders[f.folder]
+                    assert fo.dst_off <= f.dst_off and f.dst_off + f.size <= fo.dst_off + fo.unpack_size
+        checked += 1
+    assert checked >= 18
+
+
+def test_open_structure(L):
+    d = fixtures()
+    notes = {c["note"]: c for c in d["cases"]}
+    c = notes["5 folders (LZMA lc0 4 KiB dict, LZMA2, Copy, BCJ, 12 files), empty file + dir"]
+    r, folders, files, names, total = L.sz_open(arc_of(d, c))
+    assert r == 0 and len(folders) == 5 and len(files) == 20
+    assert [f.method for f in folders] == [0x030101, 0x21, 0, 0x030101, 0x030101]
+    assert [f.x86 for f in folders] == [0, 0, 0, 1, 0]
+    assert [f.num_files for f in folders] == [1, 3, 1, 1, 12]
+    assert [f.crc_defined for f in folders] == [0, 1, 1, 0, 0]
+    assert all(f.supported == 0 for f in folders)
+    empty, dirent = files[-2], files[-1]
+    assert (empty.has_stream, empty.is_dir, empty.folder) == (0, 0, 0xFFFFFFFF)
+    assert (dirent.has_stream, dirent.is_dir) == (0, 1)
+    name = names[2 * dirent.name_off:2 * (dirent.name_off + dirent.name_len - 1)]
+    assert name.decode("utf-16-le") == "dir"
+    c = notes["unsupported coder (PPMd id)"]
+    r, folders, files, _, _ = L.sz_open(arc_of(d, c))
+    assert r == 0 and [f.supported for f in folders] == [4, 0]
+
+
+def test_open_rejects_malformed(L):
+    d = fixtures()
+    good = arc_of(d, d["cases"][0])
+    assert L.sz_open(b"")[0] == 17                      # SZ_ERROR_NO_ARCHIVE
+    assert L.sz_open(good[:31])[0] == 17
+    bad = bytearray(good)
+    bad[6] = 1                                          # major version
+    assert L.sz_open(bytes(bad))[0] == 4
+    # an empty archive (next header size 0) opens with nothing in it
+    start = struct.pack("<QQI", 0, 0, 0)
+    empty = b"7z\xbc\xaf\x27\x1c\x00\x04" + struct.pack("<I", zlib.crc32(start)) + start
+    r, folders, files, _, total = L.sz_open(empty)
+    assert (r, folders, files, total) == (0, [], [], 0)
+
+
+@pytest.mark.gpu
+def test_gpu_7z_fixtures(L):
+    d = fixtures()
+    for c in d["cases"]:
+        arc = arc_of(d, c)
+        r, out, fres = L.SzExtract(arc, 64 << 20)
+        if c["open_res"] != 0:
+            assert r == c["open_res"], (c["note"], r)
+            continue
+        n = len(c["file_res"])
+        assert fres[:n] == c["file_res"], (c["note"], fres[:n])
+        want = next((x for x in c["file_res"] if x != 0), 0)
+        assert r == want, (c["note"], r)
+        ro, folders, files, names, total = L.sz_open(arc)
+        assert ro == 0 and len(out) == total
+        assert hashlib.sha256(names).hexdigest() == c["names_sha256"], c["note"]
+        got = b"".join(out[f.dst_off:f.dst_off + f.size] for f, x in zip(files, fres)
+                       if x == 0 and f.folder != 0xFFFFFFFF)
+        assert len(got) == c["out_len"], c["note"]
+        assert hashlib.sha256(got).hexdigest() == c["sha256"], c["note"]
+    # capacity short
+    c = d["cases"][0]
+    r, out, _ = L.SzExtract(arc_of(d, c), c["out_len"] - 1)
+    assert r == 7 and out == b""
+
+
+@pytest.mark.gpu
+def test_gpu_7z_many_folders_round_trip(L):
+    """1024 folders (LZMA / LZMA2 / Copy / BCJ + LZMA, 1-4 files each, packed
+    header) decode as one batch; output compared to the input files."""
+    import sevenzwrite as W
+    folders, plain = [], []
+    kinds = [dict(method=W.M_LZMA), dict(method=W.M_LZMA2), dict(method=W.M_COPY),
+             dict(method=W.M_LZMA, bcj=True), dict(method=W.M_LZMA, lc=0, lp=0, pb=0)]
+    for i in range(1024):
+        nf = 1 + i % 4
+        fs = [(f"d{i}/f{k}", native.gen("text", 9000 + 7 * i + k, 500 + (i * 131 + k * 977) % 6000))
+              for k in range(nf)]
+        folders.append(W.Folder(fs, crc=(i % 3 == 0), **kinds[i % len(kinds)]))
+        plain += [b for _, b in fs]
+    arc = W.archive(folders, encode_header=True)
+    r, fo, files, _, total = L.sz_open(arc)
+    assert r == 0 and len(fo) == 1024 and len(files) == len(plain)
+    r, out, fres = L.SzExtract(arc, total)
+    assert r == 0 and all(x == 0 for x in fres[:len(plain)])
+    assert [out[f.dst_off:f.dst_off + f.size] for f in files] == plain
+    # one corrupt byte in the coder data of folder 700: its files fail, no others
+    bad = bytearray(arc)
+    bad[fo[700].pack_off + fo[700].pack_size // 2] ^= 0x20
+    r, out, fres = L.SzExtract(bytes(bad), total)
+    failed = {i for i, x in enumerate(fres[:len(plain)]) if x != 0}
+    assert failed == {i for i, f in enumerate(files) if f.folder == 700}
+    assert all(fres[i] in (1, 3) for i in failed)
