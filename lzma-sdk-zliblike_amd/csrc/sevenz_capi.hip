@@ -780,9 +780,13 @@ SRes open_archive(const Byte* arc, size_t size, Archive& x) {
     if (jobs[0].res != SZ_OK) return jobs[0].res;
     unpacked.resize(size_t(f.unpack_size()));
     if (!ensure_device()) return SZ_ERROR_FAIL;
+    // only the header's pack stream goes to the device
+    const uint64_t at = jobs[0].pack_off, nbytes = jobs[0].avail;
+    jobs[0].pack_off = 0;
     DevArr<Byte> d_arc, d_out;
-    if (!d_arc.alloc(size) || !d_out.alloc(unpacked.size())) return SZ_ERROR_MEM;
-    if (!hip_ok(hipMemcpy(d_arc.p, arc, size, hipMemcpyHostToDevice), "7z H2D"))
+    if (!d_arc.alloc(size_t(nbytes)) || !d_out.alloc(unpacked.size())) return SZ_ERROR_MEM;
+    if (nbytes && !hip_ok(hipMemcpy(d_arc.p, arc + at, size_t(nbytes), hipMemcpyHostToDevice),
+                          "7z H2D"))
       return SZ_ERROR_FAIL;
     RINOK7(run_jobs(jobs, d_arc.p, d_out.p));
     if (jobs[0].res != SZ_OK) return jobs[0].res;
@@ -856,7 +860,7 @@ SRes LzmaGpu_7zOpen(const Byte* archive, size_t size, LzmaGpu7zFolder* folders, 
     o.folder = x.file_folder[i];
     if (o.folder != kNoFolder) {
       uint64_t off = fdst[o.folder];
-      for (uint32_t k = x.folder_start_file[o.folder]; k < i; ++k) off += x.files[k].size;
+      for (uint32_t k = x.folder_start_file[o.folder]; k < i; ++k) off += uint32_t(x.files[k].size);
       o.dst_off = off;
     }
     o.crc = f.crc;
@@ -901,6 +905,7 @@ SRes LzmaGpu_7zExtract(Byte* dest, SizeT* destLen, const Byte* archive, size_t s
     const uint32_t fo = x.file_folder[i];
     if (fo == kNoFolder) continue;
     uint64_t off = 0;
+    // SzArEx_Extract sums (UInt32)Files[k].Size (7zIn.c:1392)
     for (uint32_t k = x.folder_start_file[fo]; k < i; ++k) off += uint32_t(x.files[k].size);
     foff[i] = off;
   }
