@@ -374,6 +374,37 @@ SRes BcjGpu_X86Batch(Byte *d_data, const uint64_t *d_off, const uint64_t *d_len,
                      const uint32_t *d_ip, uint32_t *d_state, uint64_t *d_done, size_t n,
                      int encoding, void *stream);
 
+/* RISC branch converters, drop-ins for Bra.h:59-63 (Bra.c ARM_Convert :6,
+ * ARMT_Convert :33, PPC_Convert :68, SPARC_Convert :99; BraIA64.c
+ * IA64_Convert :14): the same in-place conversion of the caller's host buffer,
+ * computed on the GPU; returns the bytes processed (0 without a device).
+ * ARM/PPC/SPARC convert one lane per 4-byte word, IA64 one per 16-byte bundle,
+ * ARMT one lane per buffer (its matches chain). */
+SizeT ARM_Convert(Byte *data, SizeT size, UInt32 ip, int encoding);
+SizeT ARMT_Convert(Byte *data, SizeT size, UInt32 ip, int encoding);
+SizeT PPC_Convert(Byte *data, SizeT size, UInt32 ip, int encoding);
+SizeT SPARC_Convert(Byte *data, SizeT size, UInt32 ip, int encoding);
+SizeT IA64_Convert(Byte *data, SizeT size, UInt32 ip, int encoding);
+
+/* Delta filter, drop-ins for Delta.h:13-15 (Delta.c:6 Delta_Init, :20
+ * Delta_Encode, :42 Delta_Decode).  state: DELTA_STATE_SIZE (256) bytes,
+ * delta in 1..256; data converted in place on the GPU, state carried. */
+#define LZMA_GPU_DELTA_STATE_SIZE 256
+void Delta_Init(Byte *state);
+void Delta_Encode(Byte *state, unsigned delta, Byte *data, SizeT size);
+void Delta_Decode(Byte *state, unsigned delta, Byte *data, SizeT size);
+
+/* Batch forms over device ranges, in place, asynchronous on stream.
+ * BraGpu_Batch: kind = the xz filter ID (5 PPC, 6 IA64, 7 ARM, 8 ARMT,
+ * 9 SPARC; else SZ_ERROR_UNSUPPORTED); range i starts at ip[i];
+ * d_done[i] = what the reference's Convert returns for it.
+ * DeltaGpu_Batch: d_delta[i] in 1..256 (unchecked on the device), d_state:
+ * n x 256 bytes, range i's state at d_state + 256 * i (in/out). */
+SRes BraGpu_Batch(unsigned kind, Byte *d_data, const uint64_t *d_off, const uint64_t *d_len,
+                  const uint32_t *d_ip, uint64_t *d_done, size_t n, int encoding, void *stream);
+SRes DeltaGpu_Batch(Byte *d_data, const uint64_t *d_off, const uint64_t *d_len,
+                    const uint32_t *d_delta, Byte *d_state, size_t n, int encoding, void *stream);
+
 /* CRC-64 (XzCrc64.c, poly 0xC96C5795D7870F42).  Crc64Calc drop-in replaces
  * XzCrc64.h:20 / XzCrc64.c:30 (host buffer, GPU compute; 0 without a device).
  * The batch form mirrors CrcGpu_Batch with 2048-byte chunks planned by

@@ -33,6 +33,12 @@ extern "C" int lzgpu_launch_crc64_arrays(const uint8_t* d_data, const uint64_t* 
 extern "C" int lzgpu_launch_bcj_x86(uint8_t* d_data, const uint64_t* d_off, const uint64_t* d_len,
                                     const uint32_t* d_ip, uint32_t* d_state, uint64_t* d_done,
                                     uint32_t n, int encoding, hipStream_t stream);
+extern "C" int lzgpu_launch_bra(uint32_t kind, uint8_t* d_data, const uint64_t* d_off,
+                                const uint64_t* d_len, const uint32_t* d_ip, uint64_t* d_done,
+                                uint32_t n, int encoding, hipStream_t stream);
+extern "C" int lzgpu_launch_delta(uint8_t* d_data, const uint64_t* d_off, const uint64_t* d_len,
+                                  const uint32_t* d_delta, uint8_t* d_state, uint32_t n,
+                                  int encoding, hipStream_t stream);
 
 // host-side helpers shared by the C-ABI translation units (lzma_capi.hip)
 namespace lzgpu_host {

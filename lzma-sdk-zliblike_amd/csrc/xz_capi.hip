@@ -352,6 +352,115 @@ SizeT x86_Convert(Byte* data, SizeT size, UInt32 ip, UInt32* state, int encoding
   return SizeT(done);
 }
 
+namespace {
+
+bool bra_kind_ok(unsigned kind) {
+  return kind == 5 || kind == 6 || kind == 7 || kind == 8 || kind == 9;
+}
+
+// one RISC converter over a host buffer: upload, one range, download
+SizeT bra_convert_host(unsigned kind, const char* name, Byte* data, SizeT size, UInt32 ip,
+                       int encoding) {
+  if (!ensure_device()) return 0;
+  if (size < (kind == 6 ? 16u : 4u)) return 0;
+  DevArr<Byte> d;
+  DevArr<uint64_t> meta;  // off, len, done
+  DevArr<uint32_t> m32;   // ip
+  const uint64_t ol[2] = {0, uint64_t(size)};
+  uint64_t done = 0;
+  if (!d.alloc(size) || !meta.alloc(3) || !m32.alloc(1)) {
+    set_error("Bra converter: device allocation failed");
+    return 0;
+  }
+  if (!hip_ok(hipMemcpy(d.p, data, size, hipMemcpyHostToDevice), name) ||
+      !hip_ok(hipMemcpy(meta.p, ol, 16, hipMemcpyHostToDevice), name) ||
+      !hip_ok(hipMemcpy(m32.p, &ip, 4, hipMemcpyHostToDevice), name))
+    return 0;
+  if (lzgpu_launch_bra(kind, d.p, meta.p, meta.p + 1, m32.p, meta.p + 2, 1, encoding, nullptr) !=
+          0 ||
+      !hip_ok(hipDeviceSynchronize(), name) ||
+      !hip_ok(hipMemcpy(data, d.p, size, hipMemcpyDeviceToHost), name) ||
+      !hip_ok(hipMemcpy(&done, meta.p + 2, 8, hipMemcpyDeviceToHost), name))
+    return 0;
+  return SizeT(done);
+}
+
+void delta_host(Byte* state, unsigned delta, Byte* data, SizeT size, int encoding) {
+  if (!ensure_device()) return;
+  if (delta == 0 || delta > 256) {
+    set_error("Delta: delta outside 1..256");
+    return;
+  }
+  DevArr<Byte> d, st;
+  DevArr<uint64_t> meta;  // off, len
+  DevArr<uint32_t> dl;
+  const uint64_t ol[2] = {0, uint64_t(size)};
+  if (!d.alloc(size ? size : 1) || !st.alloc(256) || !meta.alloc(2) || !dl.alloc(1)) {
+    set_error("Delta: device allocation failed");
+    return;
+  }
+  if ((size && !hip_ok(hipMemcpy(d.p, data, size, hipMemcpyHostToDevice), "Delta H2D")) ||
+      !hip_ok(hipMemcpy(st.p, state, delta, hipMemcpyHostToDevice), "Delta H2D") ||
+      !hip_ok(hipMemcpy(meta.p, ol, 16, hipMemcpyHostToDevice), "Delta H2D") ||
+      !hip_ok(hipMemcpy(dl.p, &delta, 4, hipMemcpyHostToDevice), "Delta H2D"))
+    return;
+  if (lzgpu_launch_delta(d.p, meta.p, meta.p + 1, dl.p, st.p, 1, encoding, nullptr) != 0 ||
+      !hip_ok(hipDeviceSynchronize(), "Delta kernel") ||
+      (size && !hip_ok(hipMemcpy(data, d.p, size, hipMemcpyDeviceToHost), "Delta D2H")) ||
+      !hip_ok(hipMemcpy(state, st.p, delta, hipMemcpyDeviceToHost), "Delta D2H"))
+    return;
+}
+
+}  // namespace
+
+SizeT ARM_Convert(Byte* data, SizeT size, UInt32 ip, int encoding) {
+  return bra_convert_host(7, "ARM_Convert", data, size, ip, encoding);
+}
+SizeT ARMT_Convert(Byte* data, SizeT size, UInt32 ip, int encoding) {
+  return bra_convert_host(8, "ARMT_Convert", data, size, ip, encoding);
+}
+SizeT PPC_Convert(Byte* data, SizeT size, UInt32 ip, int encoding) {
+  return bra_convert_host(5, "PPC_Convert", data, size, ip, encoding);
+}
+SizeT SPARC_Convert(Byte* data, SizeT size, UInt32 ip, int encoding) {
+  return bra_convert_host(9, "SPARC_Convert", data, size, ip, encoding);
+}
+SizeT IA64_Convert(Byte* data, SizeT size, UInt32 ip, int encoding) {
+  return bra_convert_host(6, "IA64_Convert", data, size, ip, encoding);
+}
+void Delta_Init(Byte* state) { memset(state, 0, 256); }
+void Delta_Encode(Byte* state, unsigned delta, Byte* data, SizeT size) {
+  delta_host(state, delta, data, size, 1);
+}
+void Delta_Decode(Byte* state, unsigned delta, Byte* data, SizeT size) {
+  delta_host(state, delta, data, size, 0);
+}
+
+SRes BraGpu_Batch(unsigned kind, Byte* d_data, const uint64_t* d_off, const uint64_t* d_len,
+                  const uint32_t* d_ip, uint64_t* d_done, size_t n, int encoding, void* stream) {
+  if (!bra_kind_ok(kind)) return SZ_ERROR_UNSUPPORTED;
+  if (!ensure_device()) return SZ_ERROR_FAIL;
+  if (n > 0xFFFFFFFFull) return SZ_ERROR_PARAM;
+  if (lzgpu_launch_bra(kind, d_data, d_off, d_len, d_ip, d_done, uint32_t(n), encoding,
+                       static_cast<hipStream_t>(stream)) != 0) {
+    set_error("branch converter kernel launch failed");
+    return SZ_ERROR_FAIL;
+  }
+  return SZ_OK;
+}
+
+SRes DeltaGpu_Batch(Byte* d_data, const uint64_t* d_off, const uint64_t* d_len,
+                    const uint32_t* d_delta, Byte* d_state, size_t n, int encoding, void* stream) {
+  if (!ensure_device()) return SZ_ERROR_FAIL;
+  if (n > 0xFFFFFFFFull) return SZ_ERROR_PARAM;
+  if (lzgpu_launch_delta(d_data, d_off, d_len, d_delta, d_state, uint32_t(n), encoding,
+                         static_cast<hipStream_t>(stream)) != 0) {
+    set_error("delta kernel launch failed");
+    return SZ_ERROR_FAIL;
+  }
+  return SZ_OK;
+}
+
 UInt64 Crc64Calc(const void* data, size_t size) {
   if (!ensure_device()) return 0;
   if (size == 0) return 0;

@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 
 #include "bcj_device.h"
+#include "bra_device.h"
 #include "crc64_device.h"
 
 using namespace lzgpu;
@@ -84,5 +85,79 @@ extern "C" int lzgpu_launch_bcj_x86(uint8_t* d_data, const uint64_t* d_off, cons
   if (n == 0) return 0;
   hipLaunchKernelGGL(lzgpu_bcj_x86_kernel, dim3((n + 63) / 64), dim3(64), 0, stream, d_data, d_off,
                      d_len, d_ip, d_state, d_done, n, encoding);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// ---- RISC branch converters and delta (bra_device.h; Bra.c, BraIA64.c, Delta.c)
+
+// ARM / PPC / SPARC / IA64: one lane per aligned unit, blockIdx.y walks the ranges
+__global__ void __launch_bounds__(256) lzgpu_bra_unit_kernel(
+    uint8_t* __restrict__ data, const uint64_t* __restrict__ off, const uint64_t* __restrict__ len,
+    const uint32_t* __restrict__ ip, uint64_t* __restrict__ done, uint32_t n, uint32_t kind,
+    int encoding) {
+  const uint32_t u = bra_unit(kind);
+  for (uint32_t r = blockIdx.y; r < n; r += gridDim.y) {
+    const uint64_t units = bra_done_units(kind, len[r]);
+    if (blockIdx.x == 0 && threadIdx.x == 0) done[r] = units * u;
+    bra_byte* base = (bra_byte*)(data + off[r]);
+    const uint32_t ip0 = ip[r];
+    for (uint64_t k = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; k < units;
+         k += uint64_t(gridDim.x) * blockDim.x)
+      bra_unit_convert(kind, base + k * u, ip0 + uint32_t(k * u), encoding);
+  }
+}
+
+__global__ void __launch_bounds__(64) lzgpu_bra_armt_kernel(
+    uint8_t* __restrict__ data, const uint64_t* __restrict__ off, const uint64_t* __restrict__ len,
+    const uint32_t* __restrict__ ip, uint64_t* __restrict__ done, uint32_t n, int encoding) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  done[i] = bra_armt((bra_byte*)(data + off[i]), len[i], ip[i], encoding);
+}
+
+// one workgroup per range, lane r < delta runs residue r; state is 256 B per
+// range (DELTA_STATE_SIZE), rewritten as the last `delta` bytes seen
+__global__ void __launch_bounds__(256) lzgpu_delta_kernel(
+    uint8_t* __restrict__ data, const uint64_t* __restrict__ off, const uint64_t* __restrict__ len,
+    const uint32_t* __restrict__ delta, uint8_t* __restrict__ state, uint32_t n, int encoding) {
+  for (uint32_t r = blockIdx.x; r < n; r += gridDim.x) {
+    const uint32_t d = delta[r];
+    const uint64_t size = len[r];
+    const uint32_t t = threadIdx.x;
+    uint8_t prev = 0;
+    if (t < d) prev = state[uint64_t(r) * 256 + t];
+    __syncthreads();  // every lane has read its state byte before any is rewritten
+    if (t < d) {
+      const uint8_t last = delta_residue((bra_byte*)(data + off[r]), size, d, t, prev, encoding);
+      state[uint64_t(r) * 256 + delta_state_slot(size, d, t)] = last;
+    }
+    __syncthreads();
+  }
+}
+
+extern "C" int lzgpu_launch_bra(uint32_t kind, uint8_t* d_data, const uint64_t* d_off,
+                                const uint64_t* d_len, const uint32_t* d_ip, uint64_t* d_done,
+                                uint32_t n, int encoding, hipStream_t stream) {
+  if (n == 0) return 0;
+  if (kind == kBraARMT) {
+    hipLaunchKernelGGL(lzgpu_bra_armt_kernel, dim3((n + 63) / 64), dim3(64), 0, stream, d_data,
+                       d_off, d_len, d_ip, d_done, n, encoding);
+  } else {
+    // a few workgroups per range; enough ranges in y to fill 256 CUs
+    const uint32_t gy = n < 65535 ? n : 65535;
+    const uint32_t gx = n >= 2048 ? 2 : (n >= 256 ? 8 : 64);
+    hipLaunchKernelGGL(lzgpu_bra_unit_kernel, dim3(gx, gy), dim3(256), 0, stream, d_data, d_off,
+                       d_len, d_ip, d_done, n, kind, encoding);
+  }
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+extern "C" int lzgpu_launch_delta(uint8_t* d_data, const uint64_t* d_off, const uint64_t* d_len,
+                                  const uint32_t* d_delta, uint8_t* d_state, uint32_t n,
+                                  int encoding, hipStream_t stream) {
+  if (n == 0) return 0;
+  const uint32_t grid = n < 65536 ? n : 65536;
+  hipLaunchKernelGGL(lzgpu_delta_kernel, dim3(grid), dim3(256), 0, stream, d_data, d_off, d_len,
+                     d_delta, d_state, n, encoding);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }

@@ -179,6 +179,16 @@ _sig = {
     "LzmaGpu_Crc32Batch": (ctypes.c_int, [_P, _P, ctypes.c_size_t, _P, _P, _P, ctypes.c_size_t, _P, _P, _P]),
     "x86_Convert": (ctypes.c_size_t, [_P, ctypes.c_size_t, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint32), ctypes.c_int]),
     "BcjGpu_X86Batch": (ctypes.c_int, [_P, _P, _P, _P, _P, _P, ctypes.c_size_t, ctypes.c_int, _P]),
+    "ARM_Convert": (ctypes.c_size_t, [_P, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_int]),
+    "ARMT_Convert": (ctypes.c_size_t, [_P, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_int]),
+    "PPC_Convert": (ctypes.c_size_t, [_P, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_int]),
+    "SPARC_Convert": (ctypes.c_size_t, [_P, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_int]),
+    "IA64_Convert": (ctypes.c_size_t, [_P, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_int]),
+    "Delta_Init": (None, [_P]),
+    "Delta_Encode": (None, [_P, ctypes.c_uint, _P, ctypes.c_size_t]),
+    "Delta_Decode": (None, [_P, ctypes.c_uint, _P, ctypes.c_size_t]),
+    "BraGpu_Batch": (ctypes.c_int, [ctypes.c_uint, _P, _P, _P, _P, _P, ctypes.c_size_t, ctypes.c_int, _P]),
+    "DeltaGpu_Batch": (ctypes.c_int, [_P, _P, _P, _P, _P, ctypes.c_size_t, ctypes.c_int, _P]),
     "Crc64Calc": (ctypes.c_uint64, [_P, ctypes.c_size_t]),
     "Crc64Gpu_Batch": (ctypes.c_int, [_P, _P, _P, ctypes.c_size_t, _P, _P, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_uint64, _P, _P, _P]),
     "LzmaGpu_XzIndex": (ctypes.c_int, [_P, ctypes.c_size_t, ctypes.POINTER(XzBlock), ctypes.c_size_t, _sp, ctypes.POINTER(ctypes.c_uint64)]),
@@ -438,6 +448,34 @@ def x86_Convert(data, ip=0, state=0, encoding=0):
     st = ctypes.c_uint32(state)
     n = _lib.x86_Convert(b, len(data), ip, ctypes.byref(st), encoding)
     return n, st.value, b.raw[:len(data)]
+
+
+BRA_KINDS = {"PPC": 5, "IA64": 6, "ARM": 7, "ARMT": 8, "SPARC": 9}
+
+
+def bra_convert(kind, data, ip=0, encoding=0):
+    """Bra.c / BraIA64.c <kind>_Convert on the GPU: (processed, converted bytes)."""
+    b = ctypes.create_string_buffer(bytes(data), max(len(data), 1))
+    n = getattr(_lib, kind + "_Convert")(b, len(data), ip, encoding)
+    return n, b.raw[:len(data)]
+
+
+def delta_convert(data, delta, state=b"", encoding=0):
+    """Delta.c Delta_Decode (encoding 0) / Delta_Encode on the GPU: (state, bytes)."""
+    st = ctypes.create_string_buffer(bytes(state).ljust(256, b"\0")[:256], 256)
+    b = ctypes.create_string_buffer(bytes(data), max(len(data), 1))
+    (_lib.Delta_Encode if encoding else _lib.Delta_Decode)(st, delta, b, len(data))
+    return st.raw, b.raw[:len(data)]
+
+
+def bra_batch_device(kind, d_data, d_off, d_len, d_ip, d_done, n, encoding=0, stream=0):
+    """BraGpu_Batch over raw device pointers (ints)."""
+    return _lib.BraGpu_Batch(kind, d_data, d_off, d_len, d_ip, d_done, n, encoding, stream or None)
+
+
+def delta_batch_device(d_data, d_off, d_len, d_delta, d_state, n, encoding=0, stream=0):
+    """DeltaGpu_Batch over raw device pointers (ints)."""
+    return _lib.DeltaGpu_Batch(d_data, d_off, d_len, d_delta, d_state, n, encoding, stream or None)
 
 
 def Crc64Calc(data):

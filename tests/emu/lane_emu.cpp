@@ -13,6 +13,7 @@
 #include "../../lzma-sdk-zliblike_amd/csrc/crc32_device.h"
 #include "../../lzma-sdk-zliblike_amd/csrc/crc64_device.h"
 #include "../../lzma-sdk-zliblike_amd/csrc/bcj_device.h"
+#include "../../lzma-sdk-zliblike_amd/csrc/bra_device.h"
 
 using namespace lzgpu;
 
@@ -164,6 +165,24 @@ void emu_crc64_ranges(const uint8_t* data, const uint64_t* off, const uint64_t* 
 // loads aligned 16-byte blocks holding a valid byte: callers pad buffers.
 uint64_t emu_bcj_x86(uint8_t* data, uint64_t size, uint32_t ip, uint32_t* state, int encoding) {
   return bcj_x86(data, size, ip, state, encoding);
+}
+
+// The branch-converter kernels' code on one buffer, unit by unit in lane
+// order (lzgpu_bra_unit_kernel / lzgpu_bra_armt_kernel).
+uint64_t emu_bra(uint32_t kind, uint8_t* data, uint64_t size, uint32_t ip, int encoding) {
+  if (kind == kBraARMT) return bra_armt(data, size, ip, encoding);
+  const uint32_t u = bra_unit(kind);
+  const uint64_t units = bra_done_units(kind, size);
+  for (uint64_t k = 0; k < units; ++k) bra_unit_convert(kind, data + k * u, ip + uint32_t(k * u), encoding);
+  return units * u;
+}
+
+// lzgpu_delta_kernel's lanes for one range: read all state bytes, run the residues, rewrite state.
+void emu_delta(uint8_t* state, uint32_t delta, uint8_t* data, uint64_t size, int encoding) {
+  uint8_t prev[256], last[256];
+  for (uint32_t t = 0; t < delta; ++t) prev[t] = state[t];
+  for (uint32_t t = 0; t < delta; ++t) last[t] = delta_residue(data, size, delta, t, prev[t], encoding);
+  for (uint32_t t = 0; t < delta; ++t) state[delta_state_slot(size, delta, t)] = last[t];
 }
 
 }  // extern "C"
