@@ -420,8 +420,10 @@ SRes Crc64Gpu_Batch(const Byte *d_data, const uint64_t *d_off, const uint64_t *d
  * the streams of a concatenated one) are independent, so here the whole file
  * is indexed first -- from each stream's footer and index backwards, as
  * Xzs_ReadBackward does (XzIn.c:150-280) -- and every block decodes as one
- * lane of an LZMA2 batch, then x86 BCJ, then the block checks on the GPU
- * (CRC-32, CRC-64; SHA-256 on the host). */
+ * lane of an LZMA2 batch, then its filter chain (x86 / PPC / IA64 / ARM /
+ * ARMT / SPARC branch converters, delta; last filter first, one batch per
+ * kind and depth), then the block checks on the GPU (CRC-32, CRC-64;
+ * SHA-256 on the host). */
 #define LZMA_GPU_XZ_CHECK_NONE 0
 #define LZMA_GPU_XZ_CHECK_CRC32 1
 #define LZMA_GPU_XZ_CHECK_CRC64 4
@@ -439,6 +441,9 @@ typedef struct {
   uint32_t x86;         /* 1: an x86 BCJ filter (XZ_ID_X86 4) precedes LZMA2 */
   uint32_t x86_ip;      /* its start offset (4-byte filter props, else 0) */
   uint32_t stream;      /* index of its xz stream in the file */
+  uint32_t num_filters; /* filters before LZMA2 (0..3), in header order */
+  uint32_t filter_id[3];   /* XZ_ID_Delta 3, X86 4, PPC 5, IA64 6, ARM 7, ARMT 8, SPARC 9 */
+  uint32_t filter_prop[3]; /* start offset (branch converters) or distance 1..256 (delta) */
 } LzmaGpuXzBlock;
 
 /* Index an xz file (one or more concatenated streams with stream padding).

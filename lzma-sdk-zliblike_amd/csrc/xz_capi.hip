@@ -19,6 +19,8 @@
 
 #include "lzma_gpu_internal.h"
 
+static_assert(sizeof(LzmaGpuXzBlock) == 104, "LzmaGpuXzBlock layout (lzmagpu.py XzBlock)");
+
 using lzgpu_host::ensure_device;
 using lzgpu_host::hip_ok;
 using lzgpu_host::set_error;
@@ -218,15 +220,35 @@ SRes index_stream(const Byte* f, size_t end, uint32_t stream, std::vector<LzmaGp
       if (h[p++] != 0) return SZ_ERROR_ARCHIVE;
     LzmaGpuXzBlock blk;
     memset(&blk, 0, sizeof blk);
-    // supported chains: [LZMA2] and [x86 BCJ, LZMA2] (XZ_ID_X86 4, XZ_ID_LZMA2 0x21)
+    // chains: up to three of Delta / x86 / PPC / IA64 / ARM / ARMT / SPARC, then
+    // LZMA2 (XZ_ID_LZMA2 0x21); props validated as BraState_SetProps does
+    // (XzDec.c:71-109)
     const int last = nf - 1;
     if (ids[last] != 0x21 || psz[last] != 1 || props[last][0] > 40) return SZ_ERROR_UNSUPPORTED;
-    if (nf == 2) {
-      if (ids[0] != 4 || (psz[0] != 0 && psz[0] != 4)) return SZ_ERROR_UNSUPPORTED;
-      blk.x86 = 1;
-      blk.x86_ip = psz[0] == 4 ? le32(props[0]) : 0;
-    } else if (nf != 1) {
-      return SZ_ERROR_UNSUPPORTED;
+    blk.num_filters = uint32_t(last);
+    for (int k = 0; k < last; ++k) {
+      const uint64_t id = ids[k];
+      uint32_t prop = 0;
+      if (id == 3) {  // XZ_ID_Delta: one byte, distance = byte + 1
+        if (psz[k] != 1) return SZ_ERROR_UNSUPPORTED;
+        prop = uint32_t(props[k][0]) + 1;
+      } else if (id >= 4 && id <= 9) {
+        if (psz[k] == 4) {
+          prop = le32(props[k]);
+          const uint32_t align = id == 6 ? 0xF : (id == 8 ? 1 : (id == 4 ? 0 : 3));
+          if (prop & align) return SZ_ERROR_UNSUPPORTED;
+        } else if (psz[k] != 0) {
+          return SZ_ERROR_UNSUPPORTED;
+        }
+        if (id == 4) {
+          blk.x86 = 1;
+          blk.x86_ip = prop;
+        }
+      } else {
+        return SZ_ERROR_UNSUPPORTED;
+      }
+      blk.filter_id[k] = uint32_t(id);
+      blk.filter_prop[k] = prop;
     }
     blk.header_off = at;
     blk.data_off = at + hsize;
@@ -545,54 +567,76 @@ SRes LzmaGpu_XzDecode(Byte* dest, SizeT* destLen, const Byte* file, size_t size,
   std::vector<uint32_t> cb32(len32.size() + nch32), cb64(len64.size() + nch64);
   CrcGpu_PlanChunks(len32.data(), len32.size(), cb32.data(), cb32.data() + len32.size());
   CrcGpu_PlanChunks(len64.data(), len64.size(), cb64.data(), cb64.data() + len64.size());
-  std::vector<uint64_t> bcj_off, bcj_len;
-  std::vector<uint32_t> bcj_ip;
-  for (size_t i = 0; i < n; ++i)
-    if (blk[i].x86) {
-      bcj_off.push_back(blk[i].dst_off);
-      bcj_len.push_back(blk[i].unpack_size);
-      bcj_ip.push_back(blk[i].x86_ip);
-    }
-  const size_t nb = bcj_off.size();
 
   DevArr<Byte> d_src, d_dst, d_ws;
   DevArr<LzmaGpuStreamDesc> d_desc;
-  DevArr<uint32_t> d_order, d_cb32, d_cb64, d_crc32, d_chunk32, d_bcj32;
+  DevArr<uint32_t> d_order, d_cb32, d_cb64, d_crc32, d_chunk32;
   DevArr<LzmaGpuResult> d_res;
-  DevArr<uint64_t> d_ol32, d_ol64, d_chunk64, d_crc64, d_bcj64;
+  DevArr<uint64_t> d_ol32, d_ol64, d_chunk64, d_crc64;
   if (!d_src.alloc(size) || !d_dst.alloc(total) || !d_ws.alloc(plan.workspace_bytes) ||
       !d_desc.alloc(n) || !d_order.alloc(n) || !d_res.alloc(n) ||
       !d_ol32.alloc(2 * off32.size()) || !d_cb32.alloc(cb32.size()) ||
       !d_chunk32.alloc(nch32) || !d_crc32.alloc(off32.size()) ||
       !d_ol64.alloc(2 * off64.size()) || !d_cb64.alloc(cb64.size()) ||
-      !d_chunk64.alloc(nch64) || !d_crc64.alloc(off64.size()) || !d_bcj64.alloc(3 * nb) ||
-      !d_bcj32.alloc(2 * nb)) {
+      !d_chunk64.alloc(nch64) || !d_crc64.alloc(off64.size())) {
     set_error("XzDecode: device allocation failed");
     return SZ_ERROR_MEM;
   }
   auto h2d = [](void* d, const void* h, size_t bytes) {
     return bytes == 0 || hip_ok(hipMemcpy(d, h, bytes, hipMemcpyHostToDevice), "XzDecode H2D");
   };
-  std::vector<uint64_t> ol32(off32), ol64(off64), bc64(bcj_off);
+  std::vector<uint64_t> ol32(off32), ol64(off64);
   ol32.insert(ol32.end(), len32.begin(), len32.end());
   ol64.insert(ol64.end(), len64.begin(), len64.end());
-  bc64.insert(bc64.end(), bcj_len.begin(), bcj_len.end());
-  bc64.resize(3 * nb, 0);
-  std::vector<uint32_t> bc32(bcj_ip);
-  bc32.resize(2 * nb, 0);  // states start at 0
   if (!h2d(d_src.p, file, size) || !h2d(d_desc.p, descs.data(), n * sizeof(LzmaGpuStreamDesc)) ||
       !h2d(d_order.p, order.data(), n * 4) || !h2d(d_ol32.p, ol32.data(), ol32.size() * 8) ||
       !h2d(d_cb32.p, cb32.data(), cb32.size() * 4) ||
       !h2d(d_ol64.p, ol64.data(), ol64.size() * 8) ||
-      !h2d(d_cb64.p, cb64.data(), cb64.size() * 4) || !h2d(d_bcj64.p, bc64.data(), bc64.size() * 8) ||
-      !h2d(d_bcj32.p, bc32.data(), bc32.size() * 4))
+      !h2d(d_cb64.p, cb64.data(), cb64.size() * 4))
     return SZ_ERROR_FAIL;
   if ((r = LzmaGpu_DecodeBatchEx(&plan, d_desc.p, d_order.p, d_src.p, d_dst.p, d_ws.p, d_res.p,
                                  nullptr)) != SZ_OK)
     return r;
-  if (nb && (r = BcjGpu_X86Batch(d_dst.p, d_bcj64.p, d_bcj64.p + nb, d_bcj32.p, d_bcj32.p + nb,
-                                 d_bcj64.p + 2 * nb, nb, 0, nullptr)) != SZ_OK)
-    return r;
+  // filter chains, last filter first (MixCoder order, XzDec.c:574-585): at each
+  // depth, one batch per filter kind over the blocks that have that many
+  for (uint32_t depth = 0; depth < 3; ++depth) {
+    for (uint32_t kind = 3; kind <= 9; ++kind) {
+      std::vector<uint64_t> fo, fl;
+      std::vector<uint32_t> fp;
+      for (size_t i = 0; i < n; ++i) {
+        const uint32_t nf = blk[i].num_filters;
+        if (nf > depth && blk[i].filter_id[nf - 1 - depth] == kind) {
+          fo.push_back(blk[i].dst_off);
+          fl.push_back(blk[i].unpack_size);
+          fp.push_back(blk[i].filter_prop[nf - 1 - depth]);
+        }
+      }
+      const size_t nb = fo.size();
+      if (nb == 0) continue;
+      DevArr<uint64_t> d64;  // off, len, done
+      DevArr<uint32_t> d32;  // ip / distance, x86 state
+      DevArr<Byte> dstate;   // delta states
+      fo.insert(fo.end(), fl.begin(), fl.end());
+      fo.resize(3 * nb, 0);
+      fp.resize(2 * nb, 0);  // states start at 0 (x86_Convert_Init, Delta_Init)
+      if (!d64.alloc(3 * nb) || !d32.alloc(2 * nb) || !dstate.alloc(kind == 3 ? 256 * nb : 1)) {
+        set_error("XzDecode: device allocation failed");
+        return SZ_ERROR_MEM;
+      }
+      if (!h2d(d64.p, fo.data(), fo.size() * 8) || !h2d(d32.p, fp.data(), fp.size() * 4) ||
+          (kind == 3 && !hip_ok(hipMemset(dstate.p, 0, 256 * nb), "XzDecode memset")))
+        return SZ_ERROR_FAIL;
+      if (kind == 3)
+        r = DeltaGpu_Batch(d_dst.p, d64.p, d64.p + nb, d32.p, dstate.p, nb, 0, nullptr);
+      else if (kind == 4)
+        r = BcjGpu_X86Batch(d_dst.p, d64.p, d64.p + nb, d32.p, d32.p + nb, d64.p + 2 * nb, nb, 0,
+                            nullptr);
+      else
+        r = BraGpu_Batch(kind, d_dst.p, d64.p, d64.p + nb, d32.p, d64.p + 2 * nb, nb, 0, nullptr);
+      if (r != SZ_OK) return r;
+      if (!hip_ok(hipDeviceSynchronize(), "XzDecode filters")) return SZ_ERROR_FAIL;
+    }
+  }
   const size_t n32 = off32.size(), n64 = off64.size();
   if (n32 && (r = CrcGpu_Batch(d_dst.p, d_ol32.p, d_ol32.p + n32, n32, d_cb32.p, d_cb32.p + n32,
                                nch32, 0xFFFFFFFFu, 0xFFFFFFFFu, d_chunk32.p, d_crc32.p,

@@ -113,7 +113,9 @@ class XzBlock(ctypes.Structure):
                 ("dst_off", ctypes.c_uint64), ("check_off", ctypes.c_uint64),
                 ("check_type", ctypes.c_uint32), ("check_size", ctypes.c_uint32),
                 ("lzma2_prop", ctypes.c_uint32), ("x86", ctypes.c_uint32),
-                ("x86_ip", ctypes.c_uint32), ("stream", ctypes.c_uint32)]
+                ("x86_ip", ctypes.c_uint32), ("stream", ctypes.c_uint32),
+                ("num_filters", ctypes.c_uint32), ("filter_id", ctypes.c_uint32 * 3),
+                ("filter_prop", ctypes.c_uint32 * 3)]
 
 
 class SzFolder(ctypes.Structure):
@@ -136,7 +138,7 @@ class SzFile(ctypes.Structure):
                 ("name_len", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
 
 
-assert ctypes.sizeof(XzBlock) == 72
+assert ctypes.sizeof(XzBlock) == 104
 assert ctypes.sizeof(SzFolder) == 80 and ctypes.sizeof(SzFile) == 48
 assert ctypes.sizeof(StreamDesc) == 48 and ctypes.sizeof(Result) == 24
 assert ctypes.sizeof(Session) == 192 and ctypes.sizeof(Plan) == 184
