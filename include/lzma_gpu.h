@@ -472,10 +472,11 @@ SRes LzmaGpu_XzDecode(Byte *dest, SizeT *destLen, const Byte *file, size_t size,
  * (7zIn.c:1322; ExtractAllFiles 7zIn.c:1405 in the fork): the header walk
  * runs on the host (an LZMA / LZMA2-packed header is decoded on the GPU),
  * every folder of the archive is one item of a single GPU batch, BCJ x86
- * folders go through the BCJ kernel and every folder / file CRC through one
- * CRC-32 batch.  Folder shapes: Copy / LZMA / LZMA2, optionally followed by
- * BCJ x86 (CheckSupportedFolder, 7zDec.c:269); ARM and BCJ2 folders, which
- * the reference also decodes, return SZ_ERROR_UNSUPPORTED here. */
+ * and ARM folders go through the branch-converter kernels and every folder /
+ * file CRC through one CRC-32 batch.  Folder shapes: Copy / LZMA / LZMA2,
+ * optionally followed by BCJ x86 or ARM (CheckSupportedFolder, 7zDec.c:269;
+ * ARM_Convert at ip 0, :449); BCJ2 folders, which the reference also
+ * decodes, return SZ_ERROR_UNSUPPORTED here. */
 typedef struct LzmaGpu7zFolder {   /* 80 bytes */
   uint64_t pack_off;     /* archive offset of the main coder's pack stream */
   uint64_t pack_size;

@@ -585,12 +585,13 @@ struct Job {
   uint64_t method = 0;
   std::vector<Byte> props;
   bool x86 = false;
+  bool arm = false;
   SRes res = SZ_OK;
 };
 
 // CheckSupportedFolder (7zDec.c:269-322) + the coder checks SzDecodeLzma /
-// SzDecodeLzma2 make before decoding.  ARM and BCJ2 folders pass the
-// reference's check but are not built here: SZ_ERROR_UNSUPPORTED.
+// SzDecodeLzma2 make before decoding.  BCJ2 folders pass the reference's
+// check but are not built here: SZ_ERROR_UNSUPPORTED.
 Job make_job(const Archive& x, const Ar& a, uint32_t fi, uint64_t start, const Byte*, size_t size) {
   Job j;
   const Folder& f = a.folders[fi];
@@ -609,12 +610,15 @@ Job make_job(const Archive& x, const Ar& a, uint32_t fi, uint64_t start, const B
     if (c.method > 0xFFFFFFFFull || c.nin != 1 || c.nout != 1 || f.pack_streams.size() != 1 ||
         f.pack_streams[0] != 0 || f.bind.size() != 1 || f.bind[0].in != 1 || f.bind[0].out != 0)
       return j;
-    if (c.method != kBcj) return j;  // k_ARM: passes the reference's check, not built here
-    j.x86 = true;
+    if (c.method == kBcj)
+      j.x86 = true;
+    else if (c.method == kArm)
+      j.arm = true;  // CASE_BRA_CONV(ARM), 7zDec.c:449
+    else
+      return j;
   } else {
     return j;  // the BCJ2 layout (4 coders): not built here
   }
-  (void)kArm;
   (void)kBcj2;
   const Coder& c = f.coders[0];
   j.method = c.method;
@@ -643,7 +647,7 @@ Job make_job(const Archive& x, const Ar& a, uint32_t fi, uint64_t start, const B
 SRes run_jobs(std::vector<Job>& jobs, const Byte* d_arc, Byte* d_dst) {
   std::vector<LzmaGpuStreamDesc> descs;
   std::vector<size_t> which;
-  std::vector<uint64_t> bcj_off, bcj_len;
+  std::vector<uint64_t> bcj_off, bcj_len, arm_off, arm_len;
   for (size_t i = 0; i < jobs.size(); ++i) {
     Job& j = jobs[i];
     if (j.res != SZ_OK) continue;
@@ -675,6 +679,10 @@ SRes run_jobs(std::vector<Job>& jobs, const Byte* d_arc, Byte* d_dst) {
     if (j.x86 && j.unpack) {
       bcj_off.push_back(j.dst_off);
       bcj_len.push_back(j.unpack);
+    }
+    if (j.arm && j.unpack) {
+      arm_off.push_back(j.dst_off);
+      arm_len.push_back(j.unpack);
     }
   }
   const size_t n = descs.size(), nb = bcj_off.size();
@@ -722,6 +730,20 @@ SRes run_jobs(std::vector<Job>& jobs, const Byte* d_arc, Byte* d_dst) {
     if (!hip_ok(hipDeviceSynchronize(), "7z BCJ")) return SZ_ERROR_FAIL;
   } else if (!hip_ok(hipDeviceSynchronize(), "7z copy")) {
     return SZ_ERROR_FAIL;
+  }
+  if (const size_t na = arm_off.size()) {  // ARM_Convert(outBuffer, outSize, 0, 0) per ARM folder
+    DevArr<uint64_t> d64;  // off, len, done
+    DevArr<uint32_t> d32;  // ip = 0
+    std::vector<uint64_t> h64(arm_off);
+    h64.insert(h64.end(), arm_len.begin(), arm_len.end());
+    h64.resize(3 * na, 0);
+    if (!d64.alloc(3 * na) || !d32.alloc(na)) return SZ_ERROR_MEM;
+    if (!hip_ok(hipMemcpy(d64.p, h64.data(), h64.size() * 8, hipMemcpyHostToDevice), "7z H2D") ||
+        !hip_ok(hipMemset(d32.p, 0, na * 4), "7z memset"))
+      return SZ_ERROR_FAIL;
+    SRes r = BraGpu_Batch(7, d_dst, d64.p, d64.p + na, d32.p, d64.p + 2 * na, na, 0, nullptr);
+    if (r != SZ_OK) return r;
+    if (!hip_ok(hipDeviceSynchronize(), "7z ARM")) return SZ_ERROR_FAIL;
   }
   // SzDecodeLzma / SzDecodeLzma2 acceptance (7zDec.c:161-168, 209-216): the
   // whole output, the whole pack stream, a finished status

@@ -19,7 +19,7 @@ END, HEADER, MAIN_STREAMS, FILES, PACK_INFO, UNPACK_INFO, SUBSTREAMS = 0, 1, 4, 
 SIZE, CRC, FOLDER, CODERS_UNPACK_SIZE, NUM_UNPACK_STREAM = 9, 10, 11, 12, 13
 EMPTY_STREAM, EMPTY_FILE, NAME, ENCODED_HEADER = 14, 15, 17, 23
 
-M_COPY, M_LZMA, M_LZMA2, M_BCJ = 0, 0x030101, 0x21, 0x03030103
+M_COPY, M_LZMA, M_LZMA2, M_BCJ, M_ARM = 0, 0x030101, 0x21, 0x03030103, 0x03030501
 
 
 def number(v):
@@ -73,8 +73,8 @@ def encode(method, data, dict_size=1 << 16, lc=3, lp=0, pb=2):
     raise ValueError(method)
 
 
-def x86_encode(data):
-    f = [{"id": lzma.FILTER_X86}, {"id": lzma.FILTER_LZMA2, "dict_size": 1 << 16}]
+def x86_encode(data, fid=lzma.FILTER_X86):
+    f = [{"id": fid}, {"id": lzma.FILTER_LZMA2, "dict_size": 1 << 16}]
     raw = lzma.compress(data, format=lzma.FORMAT_RAW, filters=f)
     # liblzma cannot emit the filter alone: decode LZMA2 only to get x86(data)
     return lzma.decompress(raw, format=lzma.FORMAT_RAW,
@@ -91,15 +91,17 @@ def coder(m, props):
 
 class Folder:
     """One folder: `files` (list of (name, bytes)), packed with `packed`
-    (bytes) by `method` with `props`; `bcj` adds the x86 coder;
-    `crc` writes the folder CRC (unpack CRC) too."""
+    (bytes) by `method` with `props`; `bcj` adds the x86 coder, `arm` the
+    ARM one; `crc` writes the folder CRC (unpack CRC) too."""
 
     def __init__(self, files, method=M_LZMA, packed=None, props=None, bcj=False, crc=False,
-                 **enc):
-        self.files, self.method, self.bcj, self.crc = files, method, bcj, crc
+                 arm=False, **enc):
+        self.files, self.method, self.bcj, self.crc = files, method, bcj or arm, crc
+        self.filter = M_ARM if arm else M_BCJ
         self.data = b"".join(d for _, d in files)
         if packed is None:
-            src = x86_encode(self.data) if bcj else self.data
+            src = (x86_encode(self.data, lzma.FILTER_ARM if arm else lzma.FILTER_X86)
+                   if self.bcj else self.data)
             packed, props = encode(method, src, **enc)
         self.packed, self.props = packed, props
 
@@ -107,7 +109,7 @@ class Folder:
         if not self.bcj:
             return number(1) + coder(self.method, self.props)
         # coder 0 = main, coder 1 = BCJ; bind pair: in 1 <- out 0
-        return number(2) + coder(self.method, self.props) + coder(M_BCJ, b"") + number(1) + number(0)
+        return number(2) + coder(self.method, self.props) + coder(self.filter, b"") + number(1) + number(0)
 
     def unpack_sizes(self):
         n = len(self.data)

@@ -92,6 +92,14 @@ def archives():
     A.append(("256 small files in one LZMA folder", W.archive(
         [W.Folder([(f"s/{i}", native.gen("text", 720 + i, 50 + 37 * i)) for i in range(256)])])))
 
+    from make_golden_bra import branchy
+    ad = branchy("ARM", 730, 70001)
+    A.append(("ARM + LZMA, folder CRC", W.archive(
+        [W.Folder(files("arm", ad[:30000], ad[30000:]), arm=True, crc=True)])))
+    A.append(("ARM + LZMA2 and BCJ x86 + LZMA folders", W.archive(
+        [W.Folder(files("a2", ad[:50000]), method=W.M_LZMA2, arm=True),
+         W.Folder(files("b2", xd[:30000]), bcj=True)])))
+
     base = A[6][1]  # 5 folders
 
     def flip(b, at, mask=1):

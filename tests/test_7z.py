@@ -144,7 +144,8 @@ def test_gpu_7z_many_folders_round_trip(L):
     import sevenzwrite as W
     folders, plain = [], []
     kinds = [dict(method=W.M_LZMA), dict(method=W.M_LZMA2), dict(method=W.M_COPY),
-             dict(method=W.M_LZMA, bcj=True), dict(method=W.M_LZMA, lc=0, lp=0, pb=0)]
+             dict(method=W.M_LZMA, bcj=True), dict(method=W.M_LZMA, lc=0, lp=0, pb=0),
+             dict(method=W.M_LZMA2, arm=True)]
     for i in range(1024):
         nf = 1 + i % 4
         fs = [(f"d{i}/f{k}", native.gen("text", 9000 + 7 * i + k, 500 + (i * 131 + k * 977) % 6000))
