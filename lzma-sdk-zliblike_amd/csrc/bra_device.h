@@ -9,9 +9,15 @@
 // ARM, PPC, SPARC (one 32-bit word) and IA64 (one 16-byte bundle) convert
 // every aligned unit on its own: the unit at offset i depends only on its own
 // bytes and ip + i, so the batch kernel gives each unit its own lane.  ARMT
-// skips the next halfword pair after a conversion, which chains the units, so
-// it runs one lane per range like x86.  Delta is a running sum per residue
-// class modulo `delta`: one lane per (range, residue).
+// looks serial (a converted pair skips the next halfword, Bra.c:63) but is not:
+// a candidate at even i needs byte i+1 = 11110xxx and byte i+3 = 11111xxx, so
+// the candidates at i-2 and i+2 are impossible next to one at i (they need the
+// other pattern in the same byte), the skip never skips a candidate, and a
+// conversion rewrites only the even bytes and the low 3 bits of the odd ones,
+// which no other candidate reads or tests.  So every even position is its own
+// lane too (bra_armt_at), and the serial bra_armt below is kept as its
+// statement.  Delta is a running sum per residue class modulo `delta`: one lane
+// per (range, residue).
 #pragma once
 
 #include <stdint.h>
@@ -30,14 +36,18 @@ typedef __attribute__((address_space(1))) uint8_t bra_byte;
 
 // unit size and the bytes Convert returns for a buffer of `size` bytes
 // (the last unit that fits entirely; nothing when size < one unit)
-__host__ __device__ inline uint32_t bra_unit(uint32_t kind) { return kind == kBraIA64 ? 16u : 4u; }
+// (ARMT: `units` candidate positions 2 bytes apart, each reading 4 bytes)
+__host__ __device__ inline uint32_t bra_unit(uint32_t kind) {
+  return kind == kBraIA64 ? 16u : (kind == kBraARMT ? 2u : 4u);
+}
 __host__ __device__ inline uint64_t bra_done_units(uint32_t kind, uint64_t size) {
-  const uint64_t u = bra_unit(kind);
-  return size < u ? 0 : (size - u) / u + 1;
+  const uint64_t u = bra_unit(kind), need = kind == kBraARMT ? 4 : u;
+  return size < need ? 0 : (size - need) / u + 1;
 }
 
 // ARM BL (Bra.c:15-29): byte 3 == 0xEB, 24-bit word offset, ip + 8
-__device__ __forceinline__ void bra_arm_word(bra_byte* p, uint32_t pos, int encoding) {
+template <typename B>
+__device__ __forceinline__ void bra_arm_word(B* p, uint32_t pos, int encoding) {
   if (p[3] != 0xEB) return;
   const uint32_t src = ((uint32_t(p[2]) << 16) | (uint32_t(p[1]) << 8) | p[0]) << 2;
   uint32_t dest = encoding ? pos + 8 + src : src - (pos + 8);
@@ -48,7 +58,8 @@ __device__ __forceinline__ void bra_arm_word(bra_byte* p, uint32_t pos, int enco
 }
 
 // PPC "bl" (Bra.c:76-95): opcode 18 with AA=0, LK=1, big-endian word
-__device__ __forceinline__ void bra_ppc_word(bra_byte* p, uint32_t pos, int encoding) {
+template <typename B>
+__device__ __forceinline__ void bra_ppc_word(B* p, uint32_t pos, int encoding) {
   const uint32_t b0 = p[0], b3 = p[3];
   if ((b0 >> 2) != 0x12 || (b3 & 3) != 1) return;
   const uint32_t src = ((b0 & 3) << 24) | (uint32_t(p[1]) << 16) | (uint32_t(p[2]) << 8) | (b3 & ~3u);
@@ -60,7 +71,8 @@ __device__ __forceinline__ void bra_ppc_word(bra_byte* p, uint32_t pos, int enco
 }
 
 // SPARC "call" (Bra.c:107-130): 0x40 / 0x7F prefixes with a sign-consistent byte 1
-__device__ __forceinline__ void bra_sparc_word(bra_byte* p, uint32_t pos, int encoding) {
+template <typename B>
+__device__ __forceinline__ void bra_sparc_word(B* p, uint32_t pos, int encoding) {
   const uint32_t b0 = p[0], b1 = p[1];
   if (!((b0 == 0x40 && (b1 & 0xC0) == 0x00) || (b0 == 0x7F && (b1 & 0xC0) == 0xC0))) return;
   const uint32_t src = ((b0 << 24) | (b1 << 16) | (uint32_t(p[2]) << 8) | p[3]) << 2;
@@ -102,6 +114,59 @@ __device__ __forceinline__ void bra_ia64_bundle(bra_byte* p, uint32_t pos, int e
   }
 }
 
+__device__ __forceinline__ bool bra_armt_candidate(const bra_byte* p) {
+  return (p[1] & 0xF8) == 0xF0 && (p[3] & 0xF8) == 0xF8;
+}
+
+// ARMT BL pair at even offset i (pos = ip + i): Bra.c:42-62 for one position
+__device__ __forceinline__ void bra_armt_at(bra_byte* p, uint32_t pos, int encoding) {
+  if (!bra_armt_candidate(p)) return;
+  uint32_t src = ((uint32_t(p[1]) & 7u) << 19) | (uint32_t(p[0]) << 11) |
+                 ((uint32_t(p[3]) & 7u) << 8) | p[2];
+  src <<= 1;
+  uint32_t dest = encoding ? pos + 4 + src : src - (pos + 4);
+  dest >>= 1;
+  p[1] = uint8_t(0xF0 | ((dest >> 19) & 0x7));
+  p[0] = uint8_t(dest >> 11);
+  p[3] = uint8_t(0xF8 | ((dest >> 8) & 0x7));
+  p[2] = uint8_t(dest);
+}
+
+// what ARMT_Convert returns: one past the last position tested, + 2 when that
+// position converted (its skip); `units` = bra_done_units(kBraARMT, size)
+__device__ __forceinline__ uint64_t bra_armt_done(const bra_byte* data, uint64_t units) {
+  if (units == 0) return 0;
+  const uint64_t last = 2 * (units - 1);
+  return last + 2 + (bra_armt_candidate(data + last) ? 2 : 0);
+}
+
+// ARM / PPC / SPARC on a word held in a register (one 32-bit load, a store
+// only when the word changed): `p` 4-byte aligned
+__device__ __forceinline__ void bra_word_aligned(uint32_t kind, bra_byte* p, uint32_t pos,
+                                                 int encoding) {
+#ifdef LZGPU_HOST_EMU
+  uint32_t w;
+  __builtin_memcpy(&w, p, 4);
+#else
+  const uint32_t w = *(const __attribute__((address_space(1))) uint32_t*)p;
+#endif
+  uint8_t b[4] = {uint8_t(w), uint8_t(w >> 8), uint8_t(w >> 16), uint8_t(w >> 24)};
+  if (kind == kBraARM)
+    bra_arm_word(b, pos, encoding);
+  else if (kind == kBraPPC)
+    bra_ppc_word(b, pos, encoding);
+  else
+    bra_sparc_word(b, pos, encoding);
+  const uint32_t o = uint32_t(b[0]) | (uint32_t(b[1]) << 8) | (uint32_t(b[2]) << 16) |
+                     (uint32_t(b[3]) << 24);
+  if (o == w) return;
+#ifdef LZGPU_HOST_EMU
+  __builtin_memcpy(p, &o, 4);
+#else
+  *(__attribute__((address_space(1))) uint32_t*)p = o;
+#endif
+}
+
 // one unit of a word-parallel kind at byte offset i of a range starting at ip
 __device__ __forceinline__ void bra_unit_convert(uint32_t kind, bra_byte* p, uint32_t pos,
                                                  int encoding) {
@@ -109,6 +174,7 @@ __device__ __forceinline__ void bra_unit_convert(uint32_t kind, bra_byte* p, uin
     case kBraARM: bra_arm_word(p, pos, encoding); break;
     case kBraPPC: bra_ppc_word(p, pos, encoding); break;
     case kBraSPARC: bra_sparc_word(p, pos, encoding); break;
+    case kBraARMT: bra_armt_at(p, pos, encoding); break;
     default: bra_ia64_bundle(p, pos, encoding); break;
   }
 }

@@ -10,6 +10,8 @@
 //     block's whole output.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "bcj_device.h"
 #include "bra_device.h"
 #include "crc64_device.h"
@@ -98,12 +100,20 @@ __global__ void __launch_bounds__(256) lzgpu_bra_unit_kernel(
   const uint32_t u = bra_unit(kind);
   for (uint32_t r = blockIdx.y; r < n; r += gridDim.y) {
     const uint64_t units = bra_done_units(kind, len[r]);
-    if (blockIdx.x == 0 && threadIdx.x == 0) done[r] = units * u;
     bra_byte* base = (bra_byte*)(data + off[r]);
+    // ARMT: the candidate test reads only bytes no conversion changes (bra_device.h)
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+      done[r] = kind == kBraARMT ? bra_armt_done(base, units) : units * u;
     const uint32_t ip0 = ip[r];
-    for (uint64_t k = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; k < units;
-         k += uint64_t(gridDim.x) * blockDim.x)
-      bra_unit_convert(kind, base + k * u, ip0 + uint32_t(k * u), encoding);
+    const uint64_t k0 = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
+    const uint64_t step = uint64_t(gridDim.x) * blockDim.x;
+    if (u == 4 && ((uintptr_t)base & 3) == 0) {  // word kinds, aligned range: dword access
+      for (uint64_t k = k0; k < units; k += step)
+        bra_word_aligned(kind, base + k * 4, ip0 + uint32_t(k * 4), encoding);
+    } else {
+      for (uint64_t k = k0; k < units; k += step)
+        bra_unit_convert(kind, base + k * u, ip0 + uint32_t(k * u), encoding);
+    }
   }
 }
 
@@ -139,7 +149,7 @@ extern "C" int lzgpu_launch_bra(uint32_t kind, uint8_t* d_data, const uint64_t* 
                                 const uint64_t* d_len, const uint32_t* d_ip, uint64_t* d_done,
                                 uint32_t n, int encoding, hipStream_t stream) {
   if (n == 0) return 0;
-  if (kind == kBraARMT) {
+  if (kind == kBraARMT && getenv("LZGPU_ARMT_SERIAL")) {  // the lane-serial statement (A/B)
     hipLaunchKernelGGL(lzgpu_bra_armt_kernel, dim3((n + 63) / 64), dim3(64), 0, stream, d_data,
                        d_off, d_len, d_ip, d_done, n, encoding);
   } else {

@@ -170,11 +170,18 @@ uint64_t emu_bcj_x86(uint8_t* data, uint64_t size, uint32_t ip, uint32_t* state,
 // The branch-converter kernels' code on one buffer, unit by unit in lane
 // order (lzgpu_bra_unit_kernel / lzgpu_bra_armt_kernel).
 uint64_t emu_bra(uint32_t kind, uint8_t* data, uint64_t size, uint32_t ip, int encoding) {
-  if (kind == kBraARMT) return bra_armt(data, size, ip, encoding);
+  if (kind == 0x108) return bra_armt(data, size, ip, encoding);  // the serial statement
   const uint32_t u = bra_unit(kind);
   const uint64_t units = bra_done_units(kind, size);
-  for (uint64_t k = 0; k < units; ++k) bra_unit_convert(kind, data + k * u, ip + uint32_t(k * u), encoding);
-  return units * u;
+  const uint64_t done = kind == kBraARMT ? bra_armt_done(data, units) : units * u;
+  const bool words = u == 4 && ((uintptr_t)data & 3) == 0;  // the kernel's aligned path
+  for (uint64_t k = 0; k < units; ++k) {
+    if (words)
+      bra_word_aligned(kind, data + k * u, ip + uint32_t(k * u), encoding);
+    else
+      bra_unit_convert(kind, data + k * u, ip + uint32_t(k * u), encoding);
+  }
+  return done;
 }
 
 // lzgpu_delta_kernel's lanes for one range: read all state bytes, run the residues, rewrite state.

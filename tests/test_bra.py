@@ -85,6 +85,18 @@ def test_emu_bra_matches_reference(emu):
         assert buf.raw[:c["len"]] == _get(d, c["out"], c["len"]), c
 
 
+def test_emu_armt_serial_statement_matches_reference(emu):
+    """The lane-serial ARMT scan (bra_armt, Bra.c:33-66 as written) and the
+    per-position kernel agree with the reference on every ARMT fixture."""
+    d = fixtures()
+    for c in d["bra"]:
+        if c["kind"] != "ARMT" or "chain" in c:
+            continue
+        buf = ctypes.create_string_buffer(_get(d, c["in"], c["len"]), max(c["len"], 1))
+        assert emu.emu_bra(0x108, buf, c["len"], c["ip"], c["encoding"]) == c["done"], c
+        assert buf.raw[:c["len"]] == _get(d, c["out"], c["len"]), c
+
+
 def test_emu_delta_matches_reference(emu):
     d = fixtures()
     for c in d["delta"]:
