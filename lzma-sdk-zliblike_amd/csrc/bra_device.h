@@ -221,6 +221,43 @@ __device__ inline uint8_t delta_residue(bra_byte* data, uint64_t size, uint32_t 
   return prev;
 }
 
+// Delta_Decode as a segmented scan: lane t of a workgroup takes residue
+// r = t % delta and segment g = t / delta of that residue's positions
+// (G = floor(256 / delta) segments of `chunk` positions each).  Pass 1 sums a
+// segment (mod 256); the carry into it is the residue's state byte plus the
+// sums of the earlier segments; pass 2 rewrites the segment as a running sum.
+struct DeltaSeg {
+  uint32_t r, g, G;
+  uint64_t m0, m1;  // positions r + m * delta, m in [m0, m1)
+};
+__host__ __device__ inline bool delta_seg(uint64_t size, uint32_t delta, uint32_t t, DeltaSeg* s) {
+  const uint32_t G = 256u / delta;
+  if (t >= delta * G) return false;
+  s->r = t % delta;
+  s->g = t / delta;
+  s->G = G;
+  const uint64_t mmax = (size + delta - 1) / delta;
+  const uint64_t chunk = (mmax + G - 1) / G;
+  const uint64_t mr = s->r < size ? (size - 1 - s->r) / delta + 1 : 0;
+  s->m0 = uint64_t(s->g) * chunk;
+  s->m1 = s->m0 + chunk < mr ? s->m0 + chunk : mr;
+  if (s->m0 > s->m1) s->m0 = s->m1;
+  return true;
+}
+__device__ inline uint8_t delta_seg_sum(const bra_byte* data, uint32_t delta, const DeltaSeg& s) {
+  uint32_t acc = 0;
+  for (uint64_t m = s.m0; m < s.m1; ++m) acc += data[s.r + m * delta];
+  return uint8_t(acc);
+}
+__device__ inline uint8_t delta_seg_apply(bra_byte* data, uint32_t delta, const DeltaSeg& s,
+                                          uint8_t carry) {
+  for (uint64_t m = s.m0; m < s.m1; ++m) {
+    carry = uint8_t(carry + data[s.r + m * delta]);
+    data[s.r + m * delta] = carry;
+  }
+  return carry;
+}
+
 // where residue r's returned byte goes in the new state: its last position q
 // in [size - delta, size) of (old state ++ data), i.e. state[q + delta - size]
 __host__ __device__ inline uint32_t delta_state_slot(uint64_t size, uint32_t delta, uint32_t r) {

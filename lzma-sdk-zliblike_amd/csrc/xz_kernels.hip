@@ -130,16 +130,33 @@ __global__ void __launch_bounds__(64) lzgpu_bra_armt_kernel(
 __global__ void __launch_bounds__(256) lzgpu_delta_kernel(
     uint8_t* __restrict__ data, const uint64_t* __restrict__ off, const uint64_t* __restrict__ len,
     const uint32_t* __restrict__ delta, uint8_t* __restrict__ state, uint32_t n, int encoding) {
+  __shared__ uint8_t st[256], sums[256];
   for (uint32_t r = blockIdx.x; r < n; r += gridDim.x) {
     const uint32_t d = delta[r];
     const uint64_t size = len[r];
     const uint32_t t = threadIdx.x;
-    uint8_t prev = 0;
-    if (t < d) prev = state[uint64_t(r) * 256 + t];
-    __syncthreads();  // every lane has read its state byte before any is rewritten
-    if (t < d) {
-      const uint8_t last = delta_residue((bra_byte*)(data + off[r]), size, d, t, prev, encoding);
-      state[uint64_t(r) * 256 + delta_state_slot(size, d, t)] = last;
+    if (t < d) st[t] = state[uint64_t(r) * 256 + t];
+    __syncthreads();  // every state byte read before any is rewritten
+    bra_byte* p = (bra_byte*)(data + off[r]);
+    if (encoding) {  // Delta_Encode: one lane per residue
+      if (t < d)
+        state[uint64_t(r) * 256 + delta_state_slot(size, d, t)] =
+            delta_residue(p, size, d, t, st[t], 1);
+    } else {  // Delta_Decode: segmented scan per residue
+      DeltaSeg sg;
+      const bool on = delta_seg(size, d, t, &sg);
+      if (on) sums[t] = delta_seg_sum(p, d, sg);
+      __syncthreads();
+      if (on) {
+        uint32_t carry = st[sg.r];
+        for (uint32_t g = 0; g < sg.g; ++g) carry += sums[sg.r + g * d];
+        const uint8_t last = delta_seg_apply(p, d, sg, uint8_t(carry));
+        // the residue's last byte: from the segment holding its last position,
+        // else (no positions) its state byte, kept by segment 0
+        const uint64_t mr = sg.r < size ? (size - 1 - sg.r) / d + 1 : 0;
+        if ((mr > 0 && sg.m0 < mr && sg.m1 == mr) || (mr == 0 && sg.g == 0))
+          state[uint64_t(r) * 256 + delta_state_slot(size, d, sg.r)] = last;
+      }
     }
     __syncthreads();
   }

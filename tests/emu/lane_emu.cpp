@@ -186,10 +186,28 @@ uint64_t emu_bra(uint32_t kind, uint8_t* data, uint64_t size, uint32_t ip, int e
 
 // lzgpu_delta_kernel's lanes for one range: read all state bytes, run the residues, rewrite state.
 void emu_delta(uint8_t* state, uint32_t delta, uint8_t* data, uint64_t size, int encoding) {
-  uint8_t prev[256], last[256];
-  for (uint32_t t = 0; t < delta; ++t) prev[t] = state[t];
-  for (uint32_t t = 0; t < delta; ++t) last[t] = delta_residue(data, size, delta, t, prev[t], encoding);
-  for (uint32_t t = 0; t < delta; ++t) state[delta_state_slot(size, delta, t)] = last[t];
+  uint8_t st[256], sums[256];
+  for (uint32_t t = 0; t < delta; ++t) st[t] = state[t];
+  if (encoding) {
+    for (uint32_t t = 0; t < delta; ++t)
+      state[delta_state_slot(size, delta, t)] = delta_residue(data, size, delta, t, st[t], 1);
+    return;
+  }
+  DeltaSeg sg[256];
+  bool on[256];
+  for (uint32_t t = 0; t < 256; ++t) {
+    on[t] = delta_seg(size, delta, t, &sg[t]);
+    if (on[t]) sums[t] = delta_seg_sum(data, delta, sg[t]);
+  }
+  for (uint32_t t = 0; t < 256; ++t) {
+    if (!on[t]) continue;
+    uint32_t carry = st[sg[t].r];
+    for (uint32_t g = 0; g < sg[t].g; ++g) carry += sums[sg[t].r + g * delta];
+    const uint8_t last = delta_seg_apply(data, delta, sg[t], uint8_t(carry));
+    const uint64_t mr = sg[t].r < size ? (size - 1 - sg[t].r) / delta + 1 : 0;
+    if ((mr > 0 && sg[t].m0 < mr && sg[t].m1 == mr) || (mr == 0 && sg[t].g == 0))
+      state[delta_state_slot(size, delta, sg[t].r)] = last;
+  }
 }
 
 }  // extern "C"
