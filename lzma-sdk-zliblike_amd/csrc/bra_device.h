@@ -258,6 +258,44 @@ __device__ inline uint8_t delta_seg_apply(bra_byte* data, uint32_t delta, const 
   return carry;
 }
 
+// Delta_Decode for d | 16 as a tile scan over 16-byte lane vectors (two u64
+// halves, little-endian byte order = position order).  Byte-wise adds are SWAR
+// (no carry between bytes); a lane's inclusive prefix at distance d is log-step
+// x += x << 8d; its contribution to later lanes is its top d bytes repeated
+// with period d (d | 16 keeps every lane's byte j on residue (start + j) mod d).
+struct V16 {
+  uint64_t lo, hi;
+};
+__host__ __device__ inline uint64_t add8(uint64_t a, uint64_t b) {
+  const uint64_t H = 0x8080808080808080ull;
+  return ((a & ~H) + (b & ~H)) ^ ((a ^ b) & H);
+}
+__host__ __device__ inline V16 vadd8(V16 a, V16 b) { return V16{add8(a.lo, b.lo), add8(a.hi, b.hi)}; }
+__host__ __device__ inline V16 vshl_bytes(V16 a, uint32_t n) {  // toward higher positions, n < 16
+  if (n == 0) return a;
+  if (n >= 8) return V16{0, a.lo << (8 * (n - 8))};
+  return V16{a.lo << (8 * n), (a.hi << (8 * n)) | (a.lo >> (64 - 8 * n))};
+}
+__host__ __device__ inline V16 delta_lane_prefix(V16 x, uint32_t d) {
+  for (uint32_t s = d; s < 16; s <<= 1) x = vadd8(x, vshl_bytes(x, s));
+  return x;
+}
+// top d bytes of a lane prefix repeated with period d (bytes 16-d .. 15)
+__host__ __device__ inline V16 delta_lane_total(V16 pre, uint32_t d) {
+  uint8_t b[16], t[16];
+  for (int j = 0; j < 8; ++j) {
+    b[j] = uint8_t(pre.lo >> (8 * j));
+    b[8 + j] = uint8_t(pre.hi >> (8 * j));
+  }
+  for (uint32_t j = 0; j < 16; ++j) t[j] = b[16 - d + (j % d)];
+  V16 o{0, 0};
+  for (int j = 0; j < 8; ++j) {
+    o.lo |= uint64_t(t[j]) << (8 * j);
+    o.hi |= uint64_t(t[8 + j]) << (8 * j);
+  }
+  return o;
+}
+
 // where residue r's returned byte goes in the new state: its last position q
 // in [size - delta, size) of (old state ++ data), i.e. state[q + delta - size]
 __host__ __device__ inline uint32_t delta_state_slot(uint64_t size, uint32_t delta, uint32_t r) {

@@ -130,7 +130,8 @@ __global__ void __launch_bounds__(64) lzgpu_bra_armt_kernel(
 __global__ void __launch_bounds__(256) lzgpu_delta_kernel(
     uint8_t* __restrict__ data, const uint64_t* __restrict__ off, const uint64_t* __restrict__ len,
     const uint32_t* __restrict__ delta, uint8_t* __restrict__ state, uint32_t n, int encoding) {
-  __shared__ uint8_t st[256], sums[256];
+  __shared__ uint8_t st[256], sums[256], last[16];
+  __shared__ V16 lanes[256];
   for (uint32_t r = blockIdx.x; r < n; r += gridDim.x) {
     const uint32_t d = delta[r];
     const uint64_t size = len[r];
@@ -142,6 +143,74 @@ __global__ void __launch_bounds__(256) lzgpu_delta_kernel(
       if (t < d)
         state[uint64_t(r) * 256 + delta_state_slot(size, d, t)] =
             delta_residue(p, size, d, t, st[t], 1);
+    } else if (d <= 16 && (d & (d - 1)) == 0) {  // Delta_Decode, d | 16: tile scan
+      // head bytes up to a 16-byte aligned address: lane 0, serially
+      const uintptr_t a0 = (uintptr_t)p;
+      uint64_t h = (16 - (a0 & 15)) & 15;
+      if (h > size) h = size;
+      if (t == 0) {
+        for (uint32_t q = 0; q < d; ++q) last[q] = st[q];
+        for (uint64_t q = 0; q < h; ++q) {
+          const uint32_t rq = uint32_t(q % d);
+          last[rq] = uint8_t(last[rq] + p[q]);
+          p[q] = last[rq];
+        }
+      }
+      __syncthreads();
+      V16 C{0, 0};  // byte j: last output of residue (h + j) mod d
+      for (uint32_t j = 0; j < 16; ++j) {
+        const uint64_t b = last[(h + j) % d];
+        if (j < 8)
+          C.lo |= b << (8 * j);
+        else
+          C.hi |= b << (8 * (j - 8));
+      }
+      typedef __attribute__((address_space(1))) uint64_t g64;
+      for (uint64_t base = h; base < size; base += 4096) {
+        const uint64_t pos = base + 16 * uint64_t(t);
+        V16 x{0, 0};
+        if (pos + 16 <= size) {
+          x.lo = *(g64*)(p + pos);
+          x.hi = *(g64*)(p + pos + 8);
+        } else {
+          for (uint64_t q = pos; q < size; ++q) {
+            const uint64_t b = p[q];
+            const uint32_t j = uint32_t(q - pos);
+            if (j < 8)
+              x.lo |= b << (8 * j);
+            else
+              x.hi |= b << (8 * (j - 8));
+          }
+        }
+        const V16 pre = delta_lane_prefix(x, d);
+        lanes[t] = delta_lane_total(pre, d);
+        __syncthreads();
+        for (uint32_t o = 1; o < 256; o <<= 1) {  // inclusive scan of the lane totals
+          V16 v = lanes[t];
+          if (t >= o) v = vadd8(v, lanes[t - o]);
+          __syncthreads();
+          lanes[t] = v;
+          __syncthreads();
+        }
+        const V16 excl = t ? lanes[t - 1] : V16{0, 0};
+        const V16 o = vadd8(vadd8(pre, excl), C);
+        if (pos + 16 <= size) {
+          *(g64*)(p + pos) = o.lo;
+          *(g64*)(p + pos + 8) = o.hi;
+        } else {
+          for (uint64_t q = pos; q < size; ++q) {
+            const uint32_t j = uint32_t(q - pos);
+            p[q] = uint8_t((j < 8 ? o.lo >> (8 * j) : o.hi >> (8 * (j - 8))));
+          }
+        }
+        C = vadd8(C, lanes[255]);
+        __syncthreads();  // lanes[] is rewritten by the next tile
+      }
+      if (t < d) {  // residue t's last byte sits at C byte (t - h) mod d
+        const uint32_t j = uint32_t((t + d - h % d) % d);
+        const uint8_t b = uint8_t(j < 8 ? C.lo >> (8 * j) : C.hi >> (8 * (j - 8)));
+        state[uint64_t(r) * 256 + delta_state_slot(size, d, t)] = b;
+      }
     } else {  // Delta_Decode: segmented scan per residue
       DeltaSeg sg;
       const bool on = delta_seg(size, d, t, &sg);

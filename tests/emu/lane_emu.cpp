@@ -193,6 +193,50 @@ void emu_delta(uint8_t* state, uint32_t delta, uint8_t* data, uint64_t size, int
       state[delta_state_slot(size, delta, t)] = delta_residue(data, size, delta, t, st[t], 1);
     return;
   }
+  if (delta <= 16 && (delta & (delta - 1)) == 0) {  // lzgpu_delta_kernel's tile scan
+    const uint32_t d = delta;
+    uint64_t h = (16 - ((uintptr_t)data & 15)) & 15;
+    if (h > size) h = size;
+    uint8_t last[16];
+    for (uint32_t q = 0; q < d; ++q) last[q] = st[q];
+    for (uint64_t q = 0; q < h; ++q) {
+      last[q % d] = uint8_t(last[q % d] + data[q]);
+      data[q] = last[q % d];
+    }
+    V16 C{0, 0};
+    for (uint32_t j = 0; j < 16; ++j) {
+      const uint64_t b = last[(h + j) % d];
+      if (j < 8) C.lo |= b << (8 * j); else C.hi |= b << (8 * (j - 8));
+    }
+    for (uint64_t base = h; base < size; base += 4096) {
+      V16 pre[256], incl[256];
+      for (uint32_t t = 0; t < 256; ++t) {
+        const uint64_t pos = base + 16 * uint64_t(t);
+        V16 x{0, 0};
+        for (uint64_t q = pos; q < size && q < pos + 16; ++q) {
+          const uint32_t j = uint32_t(q - pos);
+          if (j < 8) x.lo |= uint64_t(data[q]) << (8 * j); else x.hi |= uint64_t(data[q]) << (8 * (j - 8));
+        }
+        pre[t] = delta_lane_prefix(x, d);
+        const V16 tot = delta_lane_total(pre[t], d);
+        incl[t] = t ? vadd8(incl[t - 1], tot) : tot;
+      }
+      for (uint32_t t = 0; t < 256; ++t) {
+        const uint64_t pos = base + 16 * uint64_t(t);
+        const V16 o = vadd8(vadd8(pre[t], t ? incl[t - 1] : V16{0, 0}), C);
+        for (uint64_t q = pos; q < size && q < pos + 16; ++q) {
+          const uint32_t j = uint32_t(q - pos);
+          data[q] = uint8_t(j < 8 ? o.lo >> (8 * j) : o.hi >> (8 * (j - 8)));
+        }
+      }
+      C = vadd8(C, incl[255]);
+    }
+    for (uint32_t t = 0; t < d; ++t) {
+      const uint32_t j = uint32_t((t + d - h % d) % d);
+      state[delta_state_slot(size, d, t)] = uint8_t(j < 8 ? C.lo >> (8 * j) : C.hi >> (8 * (j - 8)));
+    }
+    return;
+  }
   DeltaSeg sg[256];
   bool on[256];
   for (uint32_t t = 0; t < 256; ++t) {

@@ -50,7 +50,7 @@ def emu():
     lib.emu_bra.argtypes = [ctypes.c_uint32, ctypes.c_char_p, ctypes.c_uint64, ctypes.c_uint32,
                             ctypes.c_int]
     lib.emu_delta.restype = None
-    lib.emu_delta.argtypes = [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_char_p, ctypes.c_uint64,
+    lib.emu_delta.argtypes = [ctypes.c_char_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_uint64,
                               ctypes.c_int]
     return lib
 
@@ -105,6 +105,14 @@ def test_emu_delta_matches_reference(emu):
         emu.emu_delta(st, c["delta"], buf, c["len"], c["encoding"])
         assert buf.raw[:c["len"]] == _get(d, c["out"], c["len"]), c
         assert st.raw == _get(d, c["state_out"], 256), c
+        # the tile scan's head: the same case at every start alignment mod 16
+        for shift in (1, 5, 15):
+            st = ctypes.create_string_buffer(_get(d, c["state_in"], 256), 256)
+            big = ctypes.create_string_buffer(b"\0" * shift + _get(d, c["in"], c["len"]),
+                                              shift + max(c["len"], 1))
+            emu.emu_delta(st, c["delta"], ctypes.byref(big, shift), c["len"], c["encoding"])
+            assert big.raw[shift:shift + c["len"]] == _get(d, c["out"], c["len"]), (c, shift)
+            assert st.raw == _get(d, c["state_out"], 256), (c, shift)
 
 
 def test_batch_entry_points_exported():
