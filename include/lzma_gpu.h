@@ -216,9 +216,11 @@ size_t LzmaGpu_PlanBatch(LzmaGpuStreamDesc *descs, size_t n, uint32_t *order);
  * n_classes launches by table width (class k: classes[k].n consecutive lanes,
  * per-stream probability tables in LDS, lanes_per_group streams per
  * workgroup); order[n_lds, n) runs on the generic kernel (tables in the
- * global workspace: lc + lp too wide for LDS).  Environment overrides for
- * experiments: LZGPU_KERNEL=global|lds, LZGPU_LANES=<streams per workgroup>,
- * LZGPU_GROUPS=<workgroups per CU>, LZGPU_OCC=<1|2|4|6|8 waves per SIMD>,
+ * global workspace: lc + lp too wide for LDS).  Per-call overrides:
+ * LzmaGpu_PlanBatchOpt.  PlanBatchEx reads experiment overrides from the
+ * environment on every call: LZGPU_KERNEL=global|throughput|latency|coop,
+ * LZGPU_LANES=<streams per workgroup>, LZGPU_GROUPS=<workgroups per CU>,
+ * LZGPU_OCC=<1|2|4 waves per SIMD>, LZGPU_CUS, LZGPU_COOP=0|1,
  * LZGPU_PERSIST=0 (one stream per lane), LZGPU_CLASSES=1 (one LDS launch).
  * workspace_bytes includes the LDS launches' work counters at queue_offset
  * (zeroed by every DecodeBatchEx launch on its stream). */
@@ -252,6 +254,40 @@ typedef struct LzmaGpuPlan {
 
 SRes LzmaGpu_PlanBatchEx(LzmaGpuStreamDesc *descs, size_t n, uint32_t *order, LzmaGpuPlan *plan);
 
+/* Per-call planner options (LzmaGpu_PlanBatchOpt).  Zero = the planner's own
+ * choice for every field; the environment is not read.  `kernel` forces the
+ * instantiation every LDS-eligible class runs on:
+ *   THROUGHPUT  placement 0x105 (per-symbol tables in LDS), up to 32 streams
+ *               per wave -- the config-3 kernel, whatever the batch size;
+ *   LATENCY     placement 0x1BF, one stream per wave (lanes_per_group may
+ *               widen it);
+ *   COOP        placement 0x1BF, one stream per 32-lane wave, literal trees
+ *               decided cooperatively (wave-speculation kernel);
+ *   GLOBAL      every stream on the generic kernel (tables in global memory).
+ * A class whose latency-placement table exceeds the LDS limit keeps the
+ * throughput placement.  cus: CUs to size the plan for (0 = the device's). */
+#define LZMA_GPU_KERNEL_AUTO 0
+#define LZMA_GPU_KERNEL_THROUGHPUT 1
+#define LZMA_GPU_KERNEL_LATENCY 2
+#define LZMA_GPU_KERNEL_COOP 3
+#define LZMA_GPU_KERNEL_GLOBAL 4
+typedef struct LzmaGpuPlanOptions {
+  uint32_t kernel;          /* LZMA_GPU_KERNEL_* */
+  uint32_t cus;             /* 0 = current device's CU count (256 without a device) */
+  uint32_t lanes_per_group; /* 0 = planner; else streams per workgroup (<= 64) */
+  uint32_t groups_per_cu;   /* 0 = planner */
+  uint32_t waves_per_simd;  /* 0 = planner; else register budget 1|2|4 */
+  uint32_t persistent;      /* 0 = default (on), 1 = on, 2 = off (one stream per lane) */
+  uint32_t coop;            /* AUTO only: 0 = by streams per CU, 1 = always, 2 = never */
+  uint32_t one_class;       /* 1: all LDS-eligible streams in one launch */
+} LzmaGpuPlanOptions;
+
+/* LzmaGpu_PlanBatchEx with explicit options (opt == NULL: as PlanBatchEx,
+ * whose defaults take the LZGPU_* experiment variables of the environment,
+ * read per call).  SZ_ERROR_PARAM on an unknown kernel value. */
+SRes LzmaGpu_PlanBatchOpt(LzmaGpuStreamDesc *descs, size_t n, uint32_t *order, LzmaGpuPlan *plan,
+                          const LzmaGpuPlanOptions *opt);
+
 /* Decode a planned batch (order is required: the plan's lane partition). */
 SRes LzmaGpu_DecodeBatchEx(const LzmaGpuPlan *plan, const LzmaGpuStreamDesc *d_descs,
                            const uint32_t *d_order, const Byte *d_src, Byte *d_dst,
@@ -270,6 +306,12 @@ SRes LzmaGpu_DecodeBatch(const LzmaGpuStreamDesc *d_descs, const uint32_t *d_ord
 SRes LzmaGpu_DecodeBatchHost(const LzmaGpuStreamDesc *descs, size_t n, const Byte *src,
                              size_t src_bytes, Byte *dst, size_t dst_bytes,
                              LzmaGpuResult *results);
+/* The same with planner options (NULL = PlanBatchEx defaults); the plan used
+ * is returned through plan_out when given. */
+SRes LzmaGpu_DecodeBatchHostOpt(const LzmaGpuStreamDesc *descs, size_t n, const Byte *src,
+                                size_t src_bytes, Byte *dst, size_t dst_bytes,
+                                LzmaGpuResult *results, const LzmaGpuPlanOptions *opt,
+                                LzmaGpuPlan *plan_out);
 
 /* Split an LZMA2 stream into its independently decodable blocks: a block
  * starts at every chunk that resets the dictionary (control 0x01 or

@@ -680,11 +680,54 @@ size_t LzmaGpu_PlanBatch(LzmaGpuStreamDesc* descs, size_t n, uint32_t* order) {
   return size_t(bytes);
 }
 
-// CUs the planner sizes for (MI355X: 256; LZGPU_CUS overrides)
-static const uint32_t kPlanCUs = uint32_t(env_int("LZGPU_CUS", 256));
+// CUs the planner sizes for: the current device's, else MI355X's 256.
+static uint32_t device_cus() {
+  int dev = 0, v = 0, cnt = 0;
+  if (hipGetDeviceCount(&cnt) != hipSuccess || cnt <= 0) return 256;
+  if (hipGetDevice(&dev) != hipSuccess) return 256;
+  if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0)
+    return 256;
+  return uint32_t(v);
+}
 
-// Launch shape of one LDS class: `stride` cells per stream, `count` streams.
+// Planner defaults with the experiment overrides of the environment, read at
+// call time (LZGPU_KERNEL=global|throughput|latency|coop, LZGPU_MASK=1|2,
+// LZGPU_COOP=0|1, LZGPU_CUS, LZGPU_LANES, LZGPU_GROUPS, LZGPU_OCC,
+// LZGPU_PERSIST=0, LZGPU_CLASSES=1).  Only LzmaGpu_PlanBatchEx reads them;
+// LzmaGpu_PlanBatchOpt takes its options from the caller alone.
+static LzmaGpuPlanOptions env_options() {
+  LzmaGpuPlanOptions o;
+  memset(&o, 0, sizeof o);
+  const char* kv = getenv("LZGPU_KERNEL");
+  if (env_int("LZGPU_KERNEL_GLOBAL", 0) || (kv && strcmp(kv, "global") == 0))
+    o.kernel = LZMA_GPU_KERNEL_GLOBAL;
+  else if (kv && strcmp(kv, "throughput") == 0)
+    o.kernel = LZMA_GPU_KERNEL_THROUGHPUT;
+  else if (kv && strcmp(kv, "latency") == 0)
+    o.kernel = LZMA_GPU_KERNEL_LATENCY;
+  else if (kv && strcmp(kv, "coop") == 0)
+    o.kernel = LZMA_GPU_KERNEL_COOP;
+  const int mask = env_int("LZGPU_MASK", 0), coop = env_int("LZGPU_COOP", -1);
+  if (o.kernel == LZMA_GPU_KERNEL_AUTO) {
+    if (mask == 1) o.kernel = LZMA_GPU_KERNEL_THROUGHPUT;
+    if (mask == 2) o.kernel = coop == 1 ? LZMA_GPU_KERNEL_COOP : LZMA_GPU_KERNEL_LATENCY;
+  }
+  o.coop = coop < 0 ? 0u : (coop ? 1u : 2u);
+  o.cus = uint32_t(std::max(0, env_int("LZGPU_CUS", 0)));
+  o.lanes_per_group = uint32_t(std::max(0, env_int("LZGPU_LANES", 0)));
+  o.groups_per_cu = uint32_t(std::max(0, env_int("LZGPU_GROUPS", 0)));
+  o.waves_per_simd = uint32_t(std::max(0, env_int("LZGPU_OCC", 0)));
+  o.persistent = env_int("LZGPU_PERSIST", 1) ? 0u : 2u;
+  o.one_class = env_int("LZGPU_CLASSES", 0) == 1 ? 1u : 0u;
+  return o;
+}
+
+// Launch shape of one LDS class: `stride` cells per stream, `count` streams,
+// `cus` CUs.  `regime`: 0 = by the batch (throughput when LDS holds >= 64
+// streams per CU and the batch fills them), 1 = throughput shape forced,
+// 2 = latency shape (one stream per wave) forced.
 static LzmaGpuLdsClass plan_lds_class(uint32_t stride, uint64_t count, uint32_t mask,
+                                      uint32_t cus, int regime, const LzmaGpuPlanOptions& o,
                                       bool* latency = nullptr) {
   LzmaGpuLdsClass c;
   memset(&c, 0, sizeof c);
@@ -693,9 +736,9 @@ static LzmaGpuLdsClass plan_lds_class(uint32_t stride, uint64_t count, uint32_t 
   const uint32_t lds_per_cu = 160 * 1024;
   const uint32_t per_cu = std::max<uint32_t>(1, lds_per_cu / (stride * 2));  // streams/CU
   uint32_t occ = 4;
-  const int occ_over = env_int("LZGPU_OCC", 0);
+  const uint32_t occ_over = o.waves_per_simd;
   if (occ_over == 1 || occ_over == 2 || occ_over == 4 || occ_over == 6 || occ_over == 8)
-    occ = uint32_t(occ_over);
+    occ = occ_over;
   // Two regimes (profiles/r01_variants v17-v28):
   //  * throughput -- LDS holds >= 64 streams per CU and the batch fills them:
   //    up to 32 streams per wave with at least 8 waves per CU (64K x 4 KiB:
@@ -713,23 +756,24 @@ static LzmaGpuLdsClass plan_lds_class(uint32_t stride, uint64_t count, uint32_t 
     while (v & (v - 1)) v &= v - 1;
     return v;
   };
-  const uint64_t per_cu_batch = (count + kPlanCUs - 1) / kPlanCUs;
+  const uint64_t per_cu_batch = (count + cus - 1) / cus;
+  const bool thr = regime == 1 || (regime == 0 && per_cu >= 64 && per_cu_batch >= 64);
   uint32_t lanes = 1, groups = 16;
-  if (latency) *latency = !(per_cu >= 64 && per_cu_batch >= 64);
-  if (per_cu >= 64 && per_cu_batch >= 64) {
-    lanes = std::min<uint32_t>(32, pow2floor(per_cu / 8));
-    groups = pow2floor(std::min<uint32_t>(per_cu / lanes, 16));
+  if (latency) *latency = !thr;
+  if (thr) {
+    lanes = std::max<uint32_t>(1, std::min<uint32_t>(32, pow2floor(std::max<uint32_t>(1, per_cu / 8))));
+    groups = pow2floor(std::max<uint32_t>(1, std::min<uint32_t>(per_cu / lanes, 16)));
   } else {
     groups = pow2floor(std::min<uint32_t>(per_cu, 16));
   }
-  const int over = env_int("LZGPU_LANES", 0);
-  if (over > 0 && over <= 64 && uint32_t(over) * stride * 2 <= lds_per_cu) {
-    lanes = uint32_t(over);
-    groups = pow2floor(std::min<uint32_t>(per_cu / lanes, 16));
+  const uint32_t over = o.lanes_per_group;
+  if (over > 0 && over <= 64 && over * stride * 2 <= lds_per_cu) {
+    lanes = over;
+    groups = pow2floor(std::max<uint32_t>(1, std::min<uint32_t>(per_cu / lanes, 16)));
   }
   if (occ_over) groups = std::min<uint32_t>(groups, 4 * occ);
-  const int g_over = env_int("LZGPU_GROUPS", 0);
-  if (g_over > 0 && uint32_t(g_over) * lanes <= per_cu) groups = uint32_t(g_over);
+  const uint32_t g_over = o.groups_per_cu;
+  if (g_over > 0 && g_over * lanes <= per_cu) groups = g_over;
   c.n = count;
   c.lanes_per_group = lanes;
   c.lds_cells_per_lane = stride;
@@ -750,19 +794,19 @@ static int lds_bucket(uint32_t cells) {
   return 3;
 }
 
-SRes LzmaGpu_PlanBatchEx(LzmaGpuStreamDesc* descs, size_t n, uint32_t* order,
-                         LzmaGpuPlan* plan) {
+static SRes plan_batch(LzmaGpuStreamDesc* descs, size_t n, uint32_t* order, LzmaGpuPlan* plan,
+                       const LzmaGpuPlanOptions& o) {
   if (!order || !plan) return SZ_ERROR_PARAM;
+  if (o.kernel > LZMA_GPU_KERNEL_GLOBAL) return SZ_ERROR_PARAM;
   memset(plan, 0, sizeof *plan);
   std::vector<uint32_t> w, w_lat;
   plan->workspace_bytes = plan_workspace(descs, n, &w, &w_lat);
   plan->n = n;
+  const uint32_t cus = o.cus ? o.cus : device_cus();
   // LDS-eligible: lo table <= 16384 cells (32 KiB, >= 5 streams per CU)
   const uint32_t kMaxLdsCells = 16384;
-  const int force = env_int("LZGPU_KERNEL_GLOBAL", 0);
-  const char* kv = getenv("LZGPU_KERNEL");
-  const bool global_only = force || (kv && strcmp(kv, "global") == 0);
-  const bool one_class = env_int("LZGPU_CLASSES", 0) == 1;
+  const bool global_only = o.kernel == LZMA_GPU_KERNEL_GLOBAL;
+  const bool one_class = o.one_class != 0;
   std::vector<uint32_t> bucket_idx[LZMA_GPU_MAX_CLASSES], glob_idx;
   uint32_t bucket_stride[LZMA_GPU_MAX_CLASSES] = {0, 0, 0, 0};
   for (size_t i = 0; i < n; ++i) {
@@ -793,22 +837,26 @@ SRes LzmaGpu_PlanBatchEx(LzmaGpuStreamDesc* descs, size_t n, uint32_t* order,
     // throughput placement first; a class that lands in the latency regime is
     // re-planned with the latency placement (more tables in LDS, few streams)
     bool lat = false;
+    const int regime = o.kernel == LZMA_GPU_KERNEL_THROUGHPUT ? 1 : 0;
     LzmaGpuLdsClass c = plan_lds_class(bucket_stride[b], bucket_idx[b].size(), LZGPU_LDS_MASK,
-                                       &lat);
-    const int mask_over = env_int("LZGPU_MASK", 0);  // 1: throughput, 2: latency placement
-    if ((lat && mask_over != 1) || mask_over == 2) {
+                                       cus, regime, o, &lat);
+    const bool want_lat = o.kernel == LZMA_GPU_KERNEL_LATENCY || o.kernel == LZMA_GPU_KERNEL_COOP ||
+                          (o.kernel == LZMA_GPU_KERNEL_AUTO && lat);
+    if (want_lat) {
       uint32_t stride_lat = 0;
       for (uint32_t i : bucket_idx[b]) stride_lat = std::max(stride_lat, w_lat[i]);
       if (stride_lat <= kMaxLdsCells) {
-        c = plan_lds_class(stride_lat, bucket_idx[b].size(), LZGPU_LDS_MASK_LAT);
+        c = plan_lds_class(stride_lat, bucket_idx[b].size(), LZGPU_LDS_MASK_LAT, cus,
+                           o.kernel == LZMA_GPU_KERNEL_AUTO ? 0 : 2, o);
         // few streams per CU: the wave-cooperative kernel (all 32 lanes on one
         // stream, literal trees decided by lane speculation) -- config 4
         // 1.71 -> 2.85 GB/s and the xz leg 1.45 -> 2.36 at 4 streams per CU;
         // at 16 per CU (config 2) the single-lane waves are faster (5.9 vs 5.2)
-        const uint64_t per_cu_batch = (bucket_idx[b].size() + kPlanCUs - 1) / kPlanCUs;
-        const int coop = env_int("LZGPU_COOP", -1);
-        if (c.lanes_per_group == 1 && (coop == 1 || (coop < 0 && per_cu_batch <= 8)))
-          c.lds_mask = LZGPU_LDS_MASK_LAT | lzgpu::kCoopBit;
+        const uint64_t per_cu_batch = (bucket_idx[b].size() + cus - 1) / cus;
+        const bool coop = o.kernel == LZMA_GPU_KERNEL_COOP ||
+                          (o.kernel == LZMA_GPU_KERNEL_AUTO &&
+                           (o.coop == 1 || (o.coop == 0 && per_cu_batch <= 8)));
+        if (c.lanes_per_group == 1 && coop) c.lds_mask = LZGPU_LDS_MASK_LAT | lzgpu::kCoopBit;
       }
     }
     plan->classes[plan->n_classes++] = c;
@@ -823,11 +871,22 @@ SRes LzmaGpu_PlanBatchEx(LzmaGpuStreamDesc* descs, size_t n, uint32_t* order,
   }
   std::stable_sort(glob_idx.begin(), glob_idx.end(), by_len);
   for (uint32_t i : glob_idx) order[k++] = i;
-  plan->persistent = env_int("LZGPU_PERSIST", 1) ? 1u : 0u;
+  plan->persistent = o.persistent == 2 ? 0u : 1u;
   // the LDS launches' work counters, after the probability slices
   plan->queue_offset = (plan->workspace_bytes + 63) & ~uint64_t(63);
   plan->workspace_bytes = plan->queue_offset + 64 * LZMA_GPU_MAX_CLASSES;
   return SZ_OK;
+}
+
+SRes LzmaGpu_PlanBatchEx(LzmaGpuStreamDesc* descs, size_t n, uint32_t* order,
+                         LzmaGpuPlan* plan) {
+  return plan_batch(descs, n, order, plan, env_options());
+}
+
+SRes LzmaGpu_PlanBatchOpt(LzmaGpuStreamDesc* descs, size_t n, uint32_t* order, LzmaGpuPlan* plan,
+                          const LzmaGpuPlanOptions* opt) {
+  if (!opt) return plan_batch(descs, n, order, plan, env_options());
+  return plan_batch(descs, n, order, plan, *opt);
 }
 
 SRes LzmaGpu_DecodeBatchEx(const LzmaGpuPlan* plan, const LzmaGpuStreamDesc* d_descs,
@@ -845,7 +904,7 @@ SRes LzmaGpu_DecodeBatchEx(const LzmaGpuPlan* plan, const LzmaGpuStreamDesc* d_d
     (void)hipGetDevice(&dev);
     cus = (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
               ? v
-              : int(kPlanCUs);
+              : 256;
   }
   uint64_t first = 0;
   for (uint32_t k = 0; k < plan->n_classes; ++k) {
@@ -888,15 +947,20 @@ SRes LzmaGpu_DecodeBatch(const LzmaGpuStreamDesc* d_descs, const uint32_t* d_ord
   return SZ_OK;
 }
 
-SRes LzmaGpu_DecodeBatchHost(const LzmaGpuStreamDesc* descs, size_t n, const Byte* src,
-                             size_t src_bytes, Byte* dst, size_t dst_bytes,
-                             LzmaGpuResult* results) {
+SRes LzmaGpu_DecodeBatchHostOpt(const LzmaGpuStreamDesc* descs, size_t n, const Byte* src,
+                                size_t src_bytes, Byte* dst, size_t dst_bytes,
+                                LzmaGpuResult* results, const LzmaGpuPlanOptions* opt,
+                                LzmaGpuPlan* plan_out) {
   if (!ensure_device()) return SZ_ERROR_FAIL;
   if (n == 0) return SZ_OK;
   std::vector<LzmaGpuStreamDesc> d(descs, descs + n);
   std::vector<uint32_t> order(n);
   LzmaGpuPlan plan;
-  LzmaGpu_PlanBatchEx(d.data(), n, order.data(), &plan);
+  {
+    const SRes pr = LzmaGpu_PlanBatchOpt(d.data(), n, order.data(), &plan, opt);
+    if (pr != SZ_OK) return pr;
+  }
+  if (plan_out) *plan_out = plan;
   const size_t ws = size_t(plan.workspace_bytes);
   void *d_src = nullptr, *d_dst = nullptr, *d_ws = nullptr, *d_desc = nullptr, *d_order = nullptr,
        *d_res = nullptr;
@@ -937,6 +1001,13 @@ SRes LzmaGpu_DecodeBatchHost(const LzmaGpuStreamDesc* descs, size_t n, const Byt
   (void)hipFree(d_order);
   (void)hipFree(d_res);
   return r;
+}
+
+SRes LzmaGpu_DecodeBatchHost(const LzmaGpuStreamDesc* descs, size_t n, const Byte* src,
+                             size_t src_bytes, Byte* dst, size_t dst_bytes,
+                             LzmaGpuResult* results) {
+  return LzmaGpu_DecodeBatchHostOpt(descs, n, src, src_bytes, dst, dst_bytes, results, nullptr,
+                                    nullptr);
 }
 
 size_t Lzma2Gpu_SplitBlocks(const Byte* src, size_t src_len, uint64_t* src_off,

@@ -88,6 +88,27 @@ class Plan(ctypes.Structure):
                 ("classes", LdsClass * 4)]
 
 
+class PlanOptions(ctypes.Structure):
+    """LzmaGpuPlanOptions (include/lzma_gpu.h): per-call planner overrides."""
+    _fields_ = [("kernel", ctypes.c_uint32), ("cus", ctypes.c_uint32),
+                ("lanes_per_group", ctypes.c_uint32), ("groups_per_cu", ctypes.c_uint32),
+                ("waves_per_simd", ctypes.c_uint32), ("persistent", ctypes.c_uint32),
+                ("coop", ctypes.c_uint32), ("one_class", ctypes.c_uint32)]
+
+
+KERNELS = {"auto": 0, "throughput": 1, "latency": 2, "coop": 3, "global": 4}
+
+
+def plan_options(kernel="auto", **kw):
+    """PlanOptions from a kernel name ('auto', 'throughput', 'latency', 'coop',
+    'global') and any other LzmaGpuPlanOptions field by name."""
+    o = PlanOptions()
+    o.kernel = KERNELS[kernel]
+    for k, v in kw.items():
+        setattr(o, k, v)
+    return o
+
+
 class Session(ctypes.Structure):
     """LzmaGpuSession: a device-resident decoder (include/lzma_gpu.h)."""
     _fields_ = [("lc", ctypes.c_uint32), ("lp", ctypes.c_uint32), ("pb", ctypes.c_uint32),
@@ -142,6 +163,7 @@ assert ctypes.sizeof(XzBlock) == 104
 assert ctypes.sizeof(SzFolder) == 80 and ctypes.sizeof(SzFile) == 48
 assert ctypes.sizeof(StreamDesc) == 48 and ctypes.sizeof(Result) == 24
 assert ctypes.sizeof(Session) == 192 and ctypes.sizeof(Plan) == 184
+assert ctypes.sizeof(PlanOptions) == 32
 assert ctypes.sizeof(CLzmaDec) == 136
 
 _P = ctypes.c_void_p
@@ -168,6 +190,8 @@ _sig = {
     "LzmaGpu_PlanBatchEx": (ctypes.c_int, [ctypes.POINTER(StreamDesc), ctypes.c_size_t, _P, ctypes.POINTER(Plan)]),
     "LzmaGpu_DecodeBatchEx": (ctypes.c_int, [ctypes.POINTER(Plan), _P, _P, _P, _P, _P, _P, _P]),
     "LzmaGpu_DecodeBatchHost": (ctypes.c_int, [ctypes.POINTER(StreamDesc), ctypes.c_size_t, _P, ctypes.c_size_t, _P, ctypes.c_size_t, ctypes.POINTER(Result)]),
+    "LzmaGpu_PlanBatchOpt": (ctypes.c_int, [ctypes.POINTER(StreamDesc), ctypes.c_size_t, _P, ctypes.POINTER(Plan), ctypes.POINTER(PlanOptions)]),
+    "LzmaGpu_DecodeBatchHostOpt": (ctypes.c_int, [ctypes.POINTER(StreamDesc), ctypes.c_size_t, _P, ctypes.c_size_t, _P, ctypes.c_size_t, ctypes.POINTER(Result), ctypes.POINTER(PlanOptions), ctypes.POINTER(Plan)]),
     "Lzma2Gpu_SplitBlocks": (ctypes.c_size_t, [_P, ctypes.c_size_t, _P, _P, _P, ctypes.c_size_t]),
     "LzmaGpu_SessionProbsBytes": (ctypes.c_size_t, [ctypes.c_char_p, ctypes.c_uint]),
     "LzmaGpu_SessionInit": (ctypes.c_int, [ctypes.POINTER(Session), ctypes.c_char_p, ctypes.c_uint, _P, _P, ctypes.c_size_t]),
@@ -336,13 +360,21 @@ def make_descs(items):
     return arr
 
 
-def decode_batch_host(descs, src, dst_bytes):
-    """Decode a batch from host buffers.  Returns (res, results[ctypes], dst bytes)."""
+def decode_batch_host(descs, src, dst_bytes, opts=None, plan_out=None):
+    """Decode a batch from host buffers.  Returns (res, results[ctypes], dst bytes).
+    opts: PlanOptions (None = the planner's defaults); plan_out: a Plan to receive
+    the plan that ran."""
     n = len(descs)
     res = (Result * max(n, 1))()
     s = _buf(src)
     d = ctypes.create_string_buffer(max(dst_bytes, 1))
-    r = _lib.LzmaGpu_DecodeBatchHost(descs, n, s, len(src), d, dst_bytes, res)
+    if opts is None and plan_out is None:
+        r = _lib.LzmaGpu_DecodeBatchHost(descs, n, s, len(src), d, dst_bytes, res)
+    else:
+        r = _lib.LzmaGpu_DecodeBatchHostOpt(descs, n, s, len(src), d, dst_bytes, res,
+                                            ctypes.byref(opts) if opts is not None else None,
+                                            ctypes.byref(plan_out) if plan_out is not None
+                                            else None)
     return r, res, d.raw[:dst_bytes]
 
 
@@ -351,12 +383,16 @@ def plan(descs, order=None):
     return _lib.LzmaGpu_PlanBatch(descs, len(descs), order)
 
 
-def plan_ex(descs):
-    """LzmaGpu_PlanBatchEx: returns (Plan, order[ctypes uint32 array])."""
+def plan_ex(descs, opts=None):
+    """LzmaGpu_PlanBatchEx (or LzmaGpu_PlanBatchOpt when opts is a PlanOptions):
+    returns (Plan, order[ctypes uint32 array])."""
     n = len(descs)
     order = (ctypes.c_uint32 * max(n, 1))()
     p = Plan()
-    r = _lib.LzmaGpu_PlanBatchEx(descs, n, order, ctypes.byref(p))
+    if opts is None:
+        r = _lib.LzmaGpu_PlanBatchEx(descs, n, order, ctypes.byref(p))
+    else:
+        r = _lib.LzmaGpu_PlanBatchOpt(descs, n, order, ctypes.byref(p), ctypes.byref(opts))
     if r != SZ_OK:
         raise RuntimeError(f"LzmaGpu_PlanBatchEx failed: {r}")
     return p, order

@@ -1,6 +1,15 @@
 import os
 import sys
 
+# torch first: its HIP runtime (torch/lib/libamdhip64.so) is then the one
+# liblzmagpu.so binds to, so tests that stage device buffers with torch and
+# call the C ABI share one runtime.  Loaded the other way round, torch sees
+# no device.
+try:
+    import torch  # noqa: F401
+except ImportError:
+    pass
+
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 

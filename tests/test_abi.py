@@ -147,3 +147,41 @@ def test_plan_batch_workspace_and_order():
     assert (pb_.n_classes, cb.n, cb.lds_cells_per_lane, cb.lds_mask) == (1, 65536, 316, 0x105)
     assert (cb.lanes_per_group, cb.groups_per_cu, cb.waves_per_simd) == (32, 8, 2)
     assert plan.queue_offset % 64 == 0 and plan.workspace_bytes >= plan.queue_offset + 256
+
+
+def test_plan_options_force_each_instantiation():
+    """LzmaGpu_PlanBatchOpt forces the kernel per call (no process environment):
+    the tests use it to run the goldens through every instantiation."""
+    import lzmagpu as L
+    items = [dict(src_off=0, src_len=100, dst_off=4096 * i, dst_cap=4096,
+                  props=b"\x00\x00\x10\x00\x00" if i % 3 else b"\x5d\x00\x00\x01\x00")
+             for i in range(300)]
+    items.append(dict(src_off=0, src_len=100, dst_off=0, dst_cap=100, props=bytes([16]), kind=1))
+    descs = L.make_descs(items)
+    COOP = 0x80000000
+    masks = {}
+    for k in ("auto", "throughput", "latency", "coop", "global"):
+        p, order = L.plan_ex(descs, L.plan_options(k, cus=4))
+        assert sorted(order[i] for i in range(len(items))) == list(range(len(items)))
+        masks[k] = [p.classes[c].lds_mask for c in range(p.n_classes)]
+        lanes = [p.classes[c].lanes_per_group for c in range(p.n_classes)]
+        if k == "throughput":
+            assert set(masks[k]) == {0x105} and max(lanes) == 32
+        elif k == "latency":
+            assert set(masks[k]) == {0x1BF} and set(lanes) == {1}
+        elif k == "coop":
+            assert set(masks[k]) == {0x1BF | COOP}
+        elif k == "global":
+            assert p.n_lds == 0 and p.n_classes == 0
+    # 200 narrow streams over 4 CUs = 50 per CU: latency regime by the planner
+    assert masks["auto"] and 0x105 not in masks["auto"]
+    # more CUs: <= 8 streams per CU, the cooperative kernel
+    p, _ = L.plan_ex(descs, L.plan_options("auto", cus=256))
+    assert all(p.classes[c].lds_mask & COOP for c in range(p.n_classes))
+    p, _ = L.plan_ex(descs, L.plan_options("auto", cus=256, coop=2))
+    assert not any(p.classes[c].lds_mask & COOP for c in range(p.n_classes))
+    bad = L.plan_options("auto")
+    bad.kernel = 9
+    order = (ctypes.c_uint32 * len(items))()
+    assert L.lib.LzmaGpu_PlanBatchOpt(descs, len(items), order, ctypes.byref(L.Plan()),
+                                      ctypes.byref(bad)) == L.SZ_ERROR_PARAM

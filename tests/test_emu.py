@@ -7,6 +7,7 @@ import ctypes
 import os
 import random
 import subprocess
+import tempfile
 
 import pytest
 
@@ -55,7 +56,12 @@ EMU_VARIANTS = {
 
 @pytest.fixture(scope="module", params=sorted(EMU_VARIANTS))
 def emu(request):
-    out = EMU_SO if request.param == "default" else EMU_SO.replace(".so", f"_{request.param}.so")
+    # variant builds go to the temp dir: only the default build stays in-tree
+    # (the GPU suite's test_bra compares against it), the rest never ship
+    vdir = os.path.join(tempfile.gettempdir(), "lzgpu_emu_variants")
+    os.makedirs(vdir, exist_ok=True)
+    out = EMU_SO if request.param == "default" else os.path.join(
+        vdir, f"liblane_emu_{request.param}.so")
     subprocess.run(["make", "-s", "-f", "tests/emu/Makefile", f"EMU_OUT={out}",
                     f"EMU_FLAGS={EMU_VARIANTS[request.param]}"], cwd=native.ROOT, check=True)
     lib = ctypes.CDLL(out)
