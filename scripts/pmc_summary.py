@@ -30,6 +30,9 @@ def main():
             per[c].append(v)
         for c, v in per.items():
             out["counters"][c] = sum(v) / len(v)
+    bs = os.path.join(d, "binary.sha256")
+    if os.path.exists(bs):
+        out["binary"] = "liblzmagpu.so sha256 " + open(bs).read().split()[0][:16]
     ks = os.path.join(d, "kt", "kt_kernel_stats.csv")
     if os.path.exists(ks):
         for r in csv.DictReader(open(ks)):

@@ -9,7 +9,8 @@ R="$GRAFT_REPO_ROOT"
 OUT="$R/gpurun_out/prof_$TAG"
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-BARGS="--no-cpu-baseline $*"
+BARGS="--no-cpu-baseline --no-e2e --no-crc $*"
+sha256sum "$R/lzma-sdk-zliblike_amd/lib/liblzmagpu.so" > "$OUT/binary.sha256"
 rocprofv3 -L > "$OUT/counters_list.txt" 2>&1 || true
 echo "== kernel trace"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o kt --output-format csv -- \

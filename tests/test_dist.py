@@ -143,3 +143,41 @@ def test_shard_helpers_single_process():
     parts = [D.shard_by_weight(w, 2, r) for r in range(2)]
     assert parts[0][0] == 0 and parts[0][0] + parts[0][1] == parts[1][0]
     assert parts[1][0] + parts[1][1] == len(w)
+
+
+def _bench_line(cmd):
+    import json
+    import subprocess
+    env = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout  # rank 0 prints ONE JSON line
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("scaling", ["weak", "strong"])
+def test_bench_gpus_flag_spawns_ranks(scaling):
+    """`bench.py --gpus 2` on its own starts 2 rank processes (RANK/WORLD_SIZE set
+    before any GPU call) and reports n_gpus = 2; --dry-run runs the launcher,
+    sharding and reductions on gloo without decoding."""
+    line = _bench_line([sys.executable, "bench.py", "--gpus", "2", "--dry-run", "--steps", "2",
+                        "--scaling", scaling])
+    assert line["n_gpus"] == 2 and line["world"] == 2 and line["scaling"] == scaling
+    ranks = line["ranks"]
+    assert [r["rank"] for r in ranks] == [0, 1]
+    assert ranks[0]["first"] + ranks[0]["streams"] == ranks[1]["first"]
+    want = 65536 * (2 if scaling == "weak" else 1)
+    assert line["streams_total"] == want == sum(r["streams"] for r in ranks)
+
+
+def test_bench_under_torch_distributed_run():
+    """The driver's launch: python -m torch.distributed.run --nproc-per-node 2
+    --master-addr 127.0.0.1 bench.py --gpus 2 (ranks from the environment)."""
+    line = _bench_line([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node", "2", "--master-addr", "127.0.0.1",
+                        "--master-port", str(_free_port()), "bench.py", "--gpus", "2",
+                        "--dry-run", "--steps", "2"])
+    assert line["n_gpus"] == 2 and line["world"] == 2 and line["streams_total"] == 131072
