@@ -235,8 +235,11 @@ typedef struct LzmaGpuLdsClass {
   uint32_t groups_per_cu;
   uint32_t waves_per_simd;
   uint32_t lds_mask;      /* which probability sections live in LDS */
-  uint32_t reserved;
+  uint32_t flags;         /* LZMA_GPU_CLASS_*: set by the planner */
 } LzmaGpuLdsClass;
+/* the class holds LZMA2 items: launched on the kernel build with the LZMA2 chunk
+ * walker (without it the LZMA-only build runs, fewer registers) */
+#define LZMA_GPU_CLASS_HAS_LZMA2 1u
 
 typedef struct LzmaGpuPlan {
   uint64_t workspace_bytes;
@@ -280,7 +283,14 @@ typedef struct LzmaGpuPlanOptions {
   uint32_t persistent;      /* 0 = default (on), 1 = on, 2 = off (one stream per lane) */
   uint32_t coop;            /* AUTO only: 0 = by streams per CU, 1 = always, 2 = never */
   uint32_t one_class;       /* 1: all LDS-eligible streams in one launch */
+  uint32_t flags;           /* LZMA_GPU_PLAN_* bits */
+  uint32_t reserved;
 } LzmaGpuPlanOptions;
+/* per-lane LDS slices 8-byte aligned (default: an odd number of dwords, so that
+ * 32 lanes reading the same cell index hit 32 different LDS banks) */
+#define LZMA_GPU_PLAN_SLICE_ALIGN8 1u
+/* every class on the kernel build with the LZMA2 chunk walker (A/B only) */
+#define LZMA_GPU_PLAN_KERNEL_LZMA2 2u
 
 /* LzmaGpu_PlanBatchEx with explicit options (opt == NULL: as PlanBatchEx,
  * whose defaults take the LZGPU_* experiment variables of the environment,

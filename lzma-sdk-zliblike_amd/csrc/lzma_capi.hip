@@ -719,6 +719,8 @@ static LzmaGpuPlanOptions env_options() {
   o.waves_per_simd = uint32_t(std::max(0, env_int("LZGPU_OCC", 0)));
   o.persistent = env_int("LZGPU_PERSIST", 1) ? 0u : 2u;
   o.one_class = env_int("LZGPU_CLASSES", 0) == 1 ? 1u : 0u;
+  o.flags = (env_int("LZGPU_SLICE_ALIGN8", 0) ? LZMA_GPU_PLAN_SLICE_ALIGN8 : 0u) |
+            (env_int("LZGPU_KERNEL_LZMA2", 0) ? LZMA_GPU_PLAN_KERNEL_LZMA2 : 0u);
   return o;
 }
 
@@ -732,7 +734,16 @@ static LzmaGpuLdsClass plan_lds_class(uint32_t stride, uint64_t count, uint32_t 
   LzmaGpuLdsClass c;
   memset(&c, 0, sizeof c);
   c.lds_mask = mask;
-  stride = (stride + 3) & ~3u;  // 8-byte aligned per-lane slices
+  // Per-lane slice: an odd number of dwords, so that the 32 lanes of a wave
+  // reading the same cell index (literal-tree top levels, IsRep of one state)
+  // fall in 32 different LDS banks (bank = dword mod 32 for 2- and 4-byte
+  // reads); 8-byte aligned slices (158 dwords at lc0/pb0) put lanes l and
+  // l + 16 in one bank.  Cells are read 2 or 4 bytes at a time: 4-byte
+  // aligned slices suffice.
+  if (o.flags & LZMA_GPU_PLAN_SLICE_ALIGN8)
+    stride = (stride + 3) & ~3u;
+  else
+    stride = ((stride + 1) & ~1u) | 2u;  // cells = 2 mod 4: odd dword count
   const uint32_t lds_per_cu = 160 * 1024;
   const uint32_t per_cu = std::max<uint32_t>(1, lds_per_cu / (stride * 2));  // streams/CU
   uint32_t occ = 4;
@@ -859,6 +870,12 @@ static SRes plan_batch(LzmaGpuStreamDesc* descs, size_t n, uint32_t* order, Lzma
         if (c.lanes_per_group == 1 && coop) c.lds_mask = LZGPU_LDS_MASK_LAT | lzgpu::kCoopBit;
       }
     }
+    if (o.flags & LZMA_GPU_PLAN_KERNEL_LZMA2) c.flags |= LZMA_GPU_CLASS_HAS_LZMA2;
+    for (uint32_t i : bucket_idx[b])
+      if (descs[i].kind == LZMA_GPU_KIND_LZMA2) {
+        c.flags |= LZMA_GPU_CLASS_HAS_LZMA2;
+        break;
+      }
     plan->classes[plan->n_classes++] = c;
     plan->n_lds += c.n;
     if (c.n > best) {
@@ -917,7 +934,7 @@ SRes LzmaGpu_DecodeBatchEx(const LzmaGpuPlan* plan, const LzmaGpuStreamDesc* d_d
     if (lzgpu_launch_decode_lds(d_descs, d_order + first, uint32_t(c.n), d_src, d_dst, ws,
                                 d_results, c.lanes_per_group, c.lds_cells_per_lane,
                                 c.waves_per_simd, c.groups_per_cu, max_groups, queue, c.lds_mask,
-                                st) != 0) {
+                                c.flags, st) != 0) {
       set_error("LDS decode kernel launch failed");
       return SZ_ERROR_FAIL;
     }

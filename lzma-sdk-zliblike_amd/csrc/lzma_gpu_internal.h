@@ -17,7 +17,7 @@ extern "C" int lzgpu_launch_decode_lds(const LzmaGpuStreamDesc* d_descs, const u
                                        uint32_t stride, uint32_t waves_per_simd,
                                        uint32_t groups_per_cu, uint32_t max_groups,
                                        uint32_t* d_queue, uint32_t lds_mask,
-                                       hipStream_t stream);
+                                       uint32_t class_flags, hipStream_t stream);
 extern "C" int lzgpu_launch_crc_arrays(const uint8_t* d_data, const uint64_t* d_off,
                                        const uint64_t* d_len, uint32_t n,
                                        const uint32_t* d_chunk_base,

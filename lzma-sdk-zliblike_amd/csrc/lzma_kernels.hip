@@ -39,7 +39,10 @@ __global__ void __launch_bounds__(64) lzgpu_decode_batch_kernel(
 // launcher zeroes), so no lane idles behind a slower neighbour in its wave
 // and the chip drains without a partial last round of workgroups.  Every
 // lane exits once the queue passes n.
-template <int W, uint32_t M>
+// K2: the build carries the LZMA2 chunk walker (classes with LZMA2 items); the
+// LZMA-only build needs fewer registers (169 vs 202 VGPRs at W = 2, 21 vs 153
+// spilled at W = 4), so classes without LZMA2 items launch it.
+template <int W, uint32_t M, bool K2>
 __global__ void __launch_bounds__(64, W) lzgpu_decode_lds_kernel(
     const LzmaGpuStreamDesc* __restrict__ descs, const uint32_t* __restrict__ order, uint32_t n,
     const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, uint16_t* __restrict__ ws,
@@ -51,7 +54,7 @@ __global__ void __launch_bounds__(64, W) lzgpu_decode_lds_kernel(
   while (idx < n) {
     const uint32_t id = order ? order[idx] : idx;
     const LzmaGpuStreamDesc d = descs[id];
-    results[id] = lane_decode_lds<M>(d, src, dst, ws, lo, stride);
+    results[id] = lane_decode_lds<M, K2>(d, src, dst, ws, lo, stride);
     idx = lanes_total + atomicAdd(queue, 1u);
   }
 }
@@ -61,7 +64,7 @@ __global__ void __launch_bounds__(64, W) lzgpu_decode_lds_kernel(
 // flow and memory traffic are those of one lane -- except the literal tree,
 // whose levels are decided several at a time by speculating over the lanes
 // (spec_stage in lzma_device.h).  Lane 0 takes the next stream from the queue.
-template <int W, uint32_t M>
+template <int W, uint32_t M, bool K2>
 __global__ void __launch_bounds__(32, W) lzgpu_decode_coop_kernel(
     const LzmaGpuStreamDesc* __restrict__ descs, const uint32_t* __restrict__ order, uint32_t n,
     const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, uint16_t* __restrict__ ws,
@@ -72,7 +75,7 @@ __global__ void __launch_bounds__(32, W) lzgpu_decode_coop_kernel(
   while (idx < n) {
     const uint32_t id = order ? order[idx] : idx;
     const LzmaGpuStreamDesc d = descs[id];
-    const LzmaGpuResult r = lane_decode_lds<M>(d, src, dst, ws, lo, stride);
+    const LzmaGpuResult r = lane_decode_lds<M, K2>(d, src, dst, ws, lo, stride);
     uint32_t next = 0;
     if (threadIdx.x == 0) {
       results[id] = r;
@@ -102,7 +105,7 @@ extern "C" int lzgpu_launch_decode_batch(const LzmaGpuStreamDesc* d_descs, const
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-template <int W, uint32_t M>
+template <int W, uint32_t M, bool K2>
 static int launch_lds(const LzmaGpuStreamDesc* d_descs, const uint32_t* d_order, uint32_t n,
                       const uint8_t* d_src, uint8_t* d_dst, uint16_t* d_ws,
                       LzmaGpuResult* d_results, uint32_t lanes, uint32_t stride,
@@ -110,7 +113,7 @@ static int launch_lds(const LzmaGpuStreamDesc* d_descs, const uint32_t* d_order,
                       hipStream_t stream) {
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(lzgpu_decode_lds_kernel<W, M>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(lzgpu_decode_lds_kernel<W, M, K2>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
   }
@@ -124,20 +127,20 @@ static int launch_lds(const LzmaGpuStreamDesc* d_descs, const uint32_t* d_order,
   }
   uint32_t grid = (n + lanes - 1) / lanes;
   if (max_groups && grid > max_groups) grid = max_groups;
-  auto kfn = lzgpu_decode_lds_kernel<W, M>;
+  auto kfn = lzgpu_decode_lds_kernel<W, M, K2>;
   hipLaunchKernelGGL(kfn, dim3(grid), dim3(lanes), lds, stream, d_descs,
                      d_order, n, d_src, d_dst, d_ws, d_results, stride, d_queue);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-template <int W, uint32_t M>
+template <int W, uint32_t M, bool K2>
 static int launch_coop(const LzmaGpuStreamDesc* d_descs, const uint32_t* d_order, uint32_t n,
                        const uint8_t* d_src, uint8_t* d_dst, uint16_t* d_ws,
                        LzmaGpuResult* d_results, uint32_t stride, uint32_t groups_per_cu,
                        uint32_t max_groups, uint32_t* d_queue, hipStream_t stream) {
   static bool attr_set = false;
   if (!attr_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(lzgpu_decode_coop_kernel<W, M>),
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(lzgpu_decode_coop_kernel<W, M, K2>),
                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr_set = true;
   }
@@ -149,26 +152,53 @@ static int launch_coop(const LzmaGpuStreamDesc* d_descs, const uint32_t* d_order
   }
   uint32_t grid = n;
   if (max_groups && grid > max_groups) grid = max_groups;
-  auto kfn = lzgpu_decode_coop_kernel<W, M>;
+  auto kfn = lzgpu_decode_coop_kernel<W, M, K2>;
   hipLaunchKernelGGL(kfn, dim3(grid), dim3(32), lds, stream, d_descs, d_order, n, d_src, d_dst,
                      d_ws, d_results, stride, d_queue);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-template <uint32_t M>
+template <uint32_t M, bool K2>
 static int launch_lds_w(const LzmaGpuStreamDesc* d_descs, const uint32_t* d_order, uint32_t n,
                         const uint8_t* d_src, uint8_t* d_dst, uint16_t* d_ws,
                         LzmaGpuResult* d_results, uint32_t lanes, uint32_t stride,
                         uint32_t waves_per_simd, uint32_t groups_per_cu, uint32_t max_groups,
                         uint32_t* d_queue, hipStream_t stream) {
   if (waves_per_simd <= 1)
-    return launch_lds<1, M>(d_descs, d_order, n, d_src, d_dst, d_ws, d_results, lanes, stride,
-                            groups_per_cu, max_groups, d_queue, stream);
+    return launch_lds<1, M, K2>(d_descs, d_order, n, d_src, d_dst, d_ws, d_results, lanes, stride,
+                                groups_per_cu, max_groups, d_queue, stream);
   if (waves_per_simd == 2)
-    return launch_lds<2, M>(d_descs, d_order, n, d_src, d_dst, d_ws, d_results, lanes, stride,
-                            groups_per_cu, max_groups, d_queue, stream);
-  return launch_lds<4, M>(d_descs, d_order, n, d_src, d_dst, d_ws, d_results, lanes, stride,
-                          groups_per_cu, max_groups, d_queue, stream);
+    return launch_lds<2, M, K2>(d_descs, d_order, n, d_src, d_dst, d_ws, d_results, lanes, stride,
+                                groups_per_cu, max_groups, d_queue, stream);
+  return launch_lds<4, M, K2>(d_descs, d_order, n, d_src, d_dst, d_ws, d_results, lanes, stride,
+                              groups_per_cu, max_groups, d_queue, stream);
+}
+
+template <bool K2>
+static int launch_class(const LzmaGpuStreamDesc* d_descs, const uint32_t* d_order, uint32_t n,
+                        const uint8_t* d_src, uint8_t* d_dst, uint16_t* d_ws,
+                        LzmaGpuResult* d_results, uint32_t lanes, uint32_t stride,
+                        uint32_t waves_per_simd, uint32_t groups_per_cu, uint32_t max_groups,
+                        uint32_t* d_queue, uint32_t lds_mask, hipStream_t stream) {
+  if (lds_mask == LZGPU_LDS_MASK)
+    return launch_lds_w<LZGPU_LDS_MASK, K2>(d_descs, d_order, n, d_src, d_dst, d_ws, d_results,
+                                            lanes, stride, waves_per_simd, groups_per_cu,
+                                            max_groups, d_queue, stream);
+  if (lds_mask == (LZGPU_LDS_MASK_LAT | kCoopBit)) {
+    // one wave per workgroup: register budget by workgroups per SIMD
+    constexpr uint32_t MC = LZGPU_LDS_MASK_LAT | kCoopBit;
+    const uint32_t w = (groups_per_cu + 3) / 4;
+    if (w <= 2)
+      return launch_coop<2, MC, K2>(d_descs, d_order, n, d_src, d_dst, d_ws, d_results, stride,
+                                    groups_per_cu, max_groups, d_queue, stream);
+    return launch_coop<4, MC, K2>(d_descs, d_order, n, d_src, d_dst, d_ws, d_results, stride,
+                                  groups_per_cu, max_groups, d_queue, stream);
+  }
+  if (lds_mask == LZGPU_LDS_MASK_LAT)
+    return launch_lds_w<LZGPU_LDS_MASK_LAT, K2>(d_descs, d_order, n, d_src, d_dst, d_ws,
+                                                d_results, lanes, stride, waves_per_simd,
+                                                groups_per_cu, max_groups, d_queue, stream);
+  return -1;  // no kernel built for this placement
 }
 
 extern "C" int lzgpu_launch_decode_lds(const LzmaGpuStreamDesc* d_descs, const uint32_t* d_order,
@@ -176,28 +206,15 @@ extern "C" int lzgpu_launch_decode_lds(const LzmaGpuStreamDesc* d_descs, const u
                                        uint16_t* d_ws, LzmaGpuResult* d_results, uint32_t lanes,
                                        uint32_t stride, uint32_t waves_per_simd,
                                        uint32_t groups_per_cu, uint32_t max_groups,
-                                       uint32_t* d_queue, uint32_t lds_mask, hipStream_t stream) {
+                                       uint32_t* d_queue, uint32_t lds_mask,
+                                       uint32_t class_flags, hipStream_t stream) {
   if (n == 0) return 0;
-  if (lds_mask == LZGPU_LDS_MASK)
-    return launch_lds_w<LZGPU_LDS_MASK>(d_descs, d_order, n, d_src, d_dst, d_ws, d_results, lanes,
-                                        stride, waves_per_simd, groups_per_cu, max_groups,
-                                        d_queue, stream);
-  if (lds_mask == (LZGPU_LDS_MASK_LAT | kCoopBit)) {
-    // one wave per workgroup: register budget by workgroups per SIMD
-    const uint32_t w = (groups_per_cu + 3) / 4;
-    if (w <= 2)
-      return launch_coop<2, LZGPU_LDS_MASK_LAT | kCoopBit>(d_descs, d_order, n, d_src, d_dst,
-                                                            d_ws, d_results, stride, groups_per_cu,
-                                                            max_groups, d_queue, stream);
-    return launch_coop<4, LZGPU_LDS_MASK_LAT | kCoopBit>(d_descs, d_order, n, d_src, d_dst, d_ws,
-                                                          d_results, stride, groups_per_cu,
-                                                          max_groups, d_queue, stream);
-  }
-  if (lds_mask == LZGPU_LDS_MASK_LAT)
-    return launch_lds_w<LZGPU_LDS_MASK_LAT>(d_descs, d_order, n, d_src, d_dst, d_ws, d_results,
-                                            lanes, stride, waves_per_simd, groups_per_cu,
-                                            max_groups, d_queue, stream);
-  return -1;  // no kernel built for this placement
+  if (class_flags & LZMA_GPU_CLASS_HAS_LZMA2)
+    return launch_class<true>(d_descs, d_order, n, d_src, d_dst, d_ws, d_results, lanes, stride,
+                              waves_per_simd, groups_per_cu, max_groups, d_queue, lds_mask,
+                              stream);
+  return launch_class<false>(d_descs, d_order, n, d_src, d_dst, d_ws, d_results, lanes, stride,
+                             waves_per_simd, groups_per_cu, max_groups, d_queue, lds_mask, stream);
 }
 
 extern "C" int lzgpu_launch_session(LzgpuSession* d_sess, uint32_t n, hipStream_t stream) {

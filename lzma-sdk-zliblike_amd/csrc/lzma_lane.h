@@ -97,7 +97,7 @@ __host__ __device__ __forceinline__ uint32_t lzma2_lds_cells(uint32_t m) {
 // One LZMA (or LZMA2) batch item with the LDS-placed sections (LZGPU_LDS_MASK)
 // in the lane's LDS slice (lo_cap cells) and the others in its global
 // workspace slice.  The planner only routes items here whose LDS part fits.
-template <uint32_t M = LZGPU_LDS_MASK>
+template <uint32_t M = LZGPU_LDS_MASK, bool K2 = true>
 __device__ __forceinline__ LzmaGpuResult lane_decode_lds(const LzmaGpuStreamDesc& d,
                                                          const uint8_t* __restrict__ src,
                                                          uint8_t* __restrict__ dst,
@@ -108,10 +108,11 @@ __device__ __forceinline__ LzmaGpuResult lane_decode_lds(const LzmaGpuStreamDesc
   r.dest_len = 0;
   r.src_len = 0;
   if (d.kind == LZMA_GPU_KIND_LZMA2) {
-#ifdef LZGPU_HACK_NO2
- r.res=1; return r;
-#endif
-
+    if constexpr (!K2) {
+      // an LZMA2 item in a class the plan marked LZMA-only: a caller-built plan
+      r.res = kErrParam;
+      return r;
+    } else {
     // chunks may switch lc/lp/pb (lc + lp <= 4): the slice holds the widest layout
     if (d.probs_off == LZMA_GPU_NO_WORKSPACE || lzma2_lds_cells(M) > lo_cap) {
       r.res = (d.props[0] > 40) ? kErrUnsupported : kErrMem;
@@ -139,6 +140,7 @@ __device__ __forceinline__ LzmaGpuResult lane_decode_lds(const LzmaGpuStreamDesc
     r.dest_len = p.dec.pos;
     r.src_len = sl;
     return r;
+    }
   }
   if (d.src_len < 5) {
     r.res = kErrInputEof;

@@ -76,7 +76,7 @@ class LdsClass(ctypes.Structure):
     _fields_ = [("n", ctypes.c_uint64), ("lanes_per_group", ctypes.c_uint32),
                 ("lds_cells_per_lane", ctypes.c_uint32), ("groups_per_cu", ctypes.c_uint32),
                 ("waves_per_simd", ctypes.c_uint32), ("lds_mask", ctypes.c_uint32),
-                ("reserved", ctypes.c_uint32)]
+                ("flags", ctypes.c_uint32)]
 
 
 class Plan(ctypes.Structure):
@@ -93,7 +93,8 @@ class PlanOptions(ctypes.Structure):
     _fields_ = [("kernel", ctypes.c_uint32), ("cus", ctypes.c_uint32),
                 ("lanes_per_group", ctypes.c_uint32), ("groups_per_cu", ctypes.c_uint32),
                 ("waves_per_simd", ctypes.c_uint32), ("persistent", ctypes.c_uint32),
-                ("coop", ctypes.c_uint32), ("one_class", ctypes.c_uint32)]
+                ("coop", ctypes.c_uint32), ("one_class", ctypes.c_uint32),
+                ("flags", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
 
 
 KERNELS = {"auto": 0, "throughput": 1, "latency": 2, "coop": 3, "global": 4}
@@ -163,7 +164,7 @@ assert ctypes.sizeof(XzBlock) == 104
 assert ctypes.sizeof(SzFolder) == 80 and ctypes.sizeof(SzFile) == 48
 assert ctypes.sizeof(StreamDesc) == 48 and ctypes.sizeof(Result) == 24
 assert ctypes.sizeof(Session) == 192 and ctypes.sizeof(Plan) == 184
-assert ctypes.sizeof(PlanOptions) == 32
+assert ctypes.sizeof(PlanOptions) == 40
 assert ctypes.sizeof(CLzmaDec) == 136
 
 _P = ctypes.c_void_p

@@ -135,8 +135,13 @@ def test_plan_batch_workspace_and_order():
     assert plan.n_classes == 2
     c0, c1 = plan.classes[0], plan.classes[1]
     COOP = 0x80000000  # one stream per workgroup: the wave-cooperative kernel
-    assert (c0.n, c0.lds_cells_per_lane, c0.lds_mask) == (1, 56 + 324 + 256, 0x1BF | COOP)
-    assert (c1.n, c1.lds_cells_per_lane, c1.lds_mask) == (1, 56 * 4 + 324 + (256 << 3), 0x1BF | COOP)
+
+    def odd_dwords(cells):  # per-lane slices: an odd number of dwords (LDS banks)
+        return ((cells + 1) & ~1) | 2
+
+    assert (c0.n, c0.lds_cells_per_lane, c0.lds_mask) == (1, odd_dwords(56 + 324 + 256), 0x1BF | COOP)
+    assert (c1.n, c1.lds_cells_per_lane, c1.lds_mask) == (1, odd_dwords(56 * 4 + 324 + (256 << 3)),
+                                                          0x1BF | COOP)
     assert (c0.lanes_per_group, c0.groups_per_cu) == (1, 16)
     # a full-size batch is in the throughput regime: placement 0x105 (IsMatch,
     # IsRep/G0/G1/G2, plain literal tree) = 12 * 2^pb + 48 + 0x100 << (lc+lp) cells
@@ -144,8 +149,12 @@ def test_plan_batch_workspace_and_order():
                              props=b"\x00\x00\x10\x00\x00") for i in range(65536)])
     pb_, _ = L.plan_ex(big)
     cb = pb_.classes[0]
-    assert (pb_.n_classes, cb.n, cb.lds_cells_per_lane, cb.lds_mask) == (1, 65536, 316, 0x105)
+    assert (pb_.n_classes, cb.n, cb.lds_cells_per_lane, cb.lds_mask) == (1, 65536, 318, 0x105)
     assert (cb.lanes_per_group, cb.groups_per_cu, cb.waves_per_simd) == (32, 8, 2)
+    assert (cb.lds_cells_per_lane // 2) % 2 == 1  # 159 dwords: 32 lanes, 32 banks
+    # LZMA_GPU_PLAN_SLICE_ALIGN8: the round-1 8-byte aligned slices (158 dwords)
+    pa, _ = L.plan_ex(big, L.plan_options("auto", flags=1))
+    assert pa.classes[0].lds_cells_per_lane == 316
     assert plan.queue_offset % 64 == 0 and plan.workspace_bytes >= plan.queue_offset + 256
 
 
