@@ -14,6 +14,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <exception>
 #include <numeric>
 #include <string>
 #include <vector>
@@ -665,7 +666,7 @@ static uint64_t plan_workspace(LzmaGpuStreamDesc* descs, size_t n, std::vector<u
   return off * 2;
 }
 
-size_t LzmaGpu_PlanBatch(LzmaGpuStreamDesc* descs, size_t n, uint32_t* order) {
+static size_t plan_simple(LzmaGpuStreamDesc* descs, size_t n, uint32_t* order) {
   std::vector<uint32_t> w;
   const uint64_t bytes = plan_workspace(descs, n, &w);
   if (order) {
@@ -678,6 +679,15 @@ size_t LzmaGpu_PlanBatch(LzmaGpuStreamDesc* descs, size_t n, uint32_t* order) {
     for (size_t i = 0; i < n; ++i) order[i] = idx[i];
   }
   return size_t(bytes);
+}
+
+size_t LzmaGpu_PlanBatch(LzmaGpuStreamDesc* descs, size_t n, uint32_t* order) {
+  try {
+    return plan_simple(descs, n, order);
+  } catch (const std::exception&) {
+    set_error("plan: host allocation failed");
+    return 0;
+  }
 }
 
 // CUs the planner sizes for: the current device's, else MI355X's 256.
@@ -895,15 +905,25 @@ static SRes plan_batch(LzmaGpuStreamDesc* descs, size_t n, uint32_t* order, Lzma
   return SZ_OK;
 }
 
+// C ABI: no exception crosses it (host allocation failure -> SZ_ERROR_MEM).
+static SRes plan_batch_nothrow(LzmaGpuStreamDesc* descs, size_t n, uint32_t* order,
+                               LzmaGpuPlan* plan, const LzmaGpuPlanOptions& o) {
+  try {
+    return plan_batch(descs, n, order, plan, o);
+  } catch (const std::exception&) {
+    set_error("plan: host allocation failed");
+    return SZ_ERROR_MEM;
+  }
+}
+
 SRes LzmaGpu_PlanBatchEx(LzmaGpuStreamDesc* descs, size_t n, uint32_t* order,
                          LzmaGpuPlan* plan) {
-  return plan_batch(descs, n, order, plan, env_options());
+  return plan_batch_nothrow(descs, n, order, plan, env_options());
 }
 
 SRes LzmaGpu_PlanBatchOpt(LzmaGpuStreamDesc* descs, size_t n, uint32_t* order, LzmaGpuPlan* plan,
                           const LzmaGpuPlanOptions* opt) {
-  if (!opt) return plan_batch(descs, n, order, plan, env_options());
-  return plan_batch(descs, n, order, plan, *opt);
+  return plan_batch_nothrow(descs, n, order, plan, opt ? *opt : env_options());
 }
 
 SRes LzmaGpu_DecodeBatchEx(const LzmaGpuPlan* plan, const LzmaGpuStreamDesc* d_descs,
@@ -964,10 +984,10 @@ SRes LzmaGpu_DecodeBatch(const LzmaGpuStreamDesc* d_descs, const uint32_t* d_ord
   return SZ_OK;
 }
 
-SRes LzmaGpu_DecodeBatchHostOpt(const LzmaGpuStreamDesc* descs, size_t n, const Byte* src,
-                                size_t src_bytes, Byte* dst, size_t dst_bytes,
-                                LzmaGpuResult* results, const LzmaGpuPlanOptions* opt,
-                                LzmaGpuPlan* plan_out) {
+static SRes decode_batch_host(const LzmaGpuStreamDesc* descs, size_t n, const Byte* src,
+                              size_t src_bytes, Byte* dst, size_t dst_bytes,
+                              LzmaGpuResult* results, const LzmaGpuPlanOptions* opt,
+                              LzmaGpuPlan* plan_out) {
   if (!ensure_device()) return SZ_ERROR_FAIL;
   if (n == 0) return SZ_OK;
   std::vector<LzmaGpuStreamDesc> d(descs, descs + n);
@@ -1018,6 +1038,18 @@ SRes LzmaGpu_DecodeBatchHostOpt(const LzmaGpuStreamDesc* descs, size_t n, const 
   (void)hipFree(d_order);
   (void)hipFree(d_res);
   return r;
+}
+
+SRes LzmaGpu_DecodeBatchHostOpt(const LzmaGpuStreamDesc* descs, size_t n, const Byte* src,
+                                size_t src_bytes, Byte* dst, size_t dst_bytes,
+                                LzmaGpuResult* results, const LzmaGpuPlanOptions* opt,
+                                LzmaGpuPlan* plan_out) {
+  try {
+    return decode_batch_host(descs, n, src, src_bytes, dst, dst_bytes, results, opt, plan_out);
+  } catch (const std::exception&) {
+    set_error("batch: host allocation failed");
+    return SZ_ERROR_MEM;
+  }
 }
 
 SRes LzmaGpu_DecodeBatchHost(const LzmaGpuStreamDesc* descs, size_t n, const Byte* src,
@@ -1140,9 +1172,16 @@ size_t CrcGpu_PlanChunks(const uint64_t* caps, size_t n, uint32_t* chunk_base,
 
 size_t LzmaGpu_Crc32Plan(const LzmaGpuStreamDesc* descs, size_t n, uint32_t* chunk_base,
                          uint32_t* chunk_range) {
-  std::vector<uint64_t> caps(n);
-  for (size_t i = 0; i < n; ++i) caps[i] = descs[i].dst_cap;
-  return CrcGpu_PlanChunks(caps.data(), n, chunk_base, chunk_range);
+  uint64_t total = 0;
+  for (size_t i = 0; i < n; ++i) {
+    const uint64_t c = (descs[i].dst_cap + lzgpu::kCrcChunk - 1) / lzgpu::kCrcChunk;
+    if (total + c > 0xFFFFFFFFull) return size_t(-1);
+    if (chunk_base) chunk_base[i] = uint32_t(total);
+    if (chunk_range)
+      for (uint64_t k = 0; k < c; ++k) chunk_range[total + k] = uint32_t(i);
+    total += c;
+  }
+  return size_t(total);
 }
 
 SRes CrcGpu_Batch(const Byte* d_data, const uint64_t* d_off, const uint64_t* d_len, size_t n,

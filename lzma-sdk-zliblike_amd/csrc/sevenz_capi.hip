@@ -16,6 +16,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <exception>
 #include <vector>
 
 #include "lzma_gpu_internal.h"
@@ -218,6 +219,9 @@ SRes read_pack_info(Sd& s, uint64_t* data_offset, Ar& a) {
   RINOK7(rd_num(s, data_offset));
   RINOK7(rd_num32(s, &n));
   RINOK7(wait_attr(s, kSize));
+  // every pack size takes >= 1 header byte: a count beyond the bytes left
+  // cannot be read (the reference's MY_ALLOC would ask for n * 8 bytes first)
+  if (n > s.n) return SZ_ERROR_ARCHIVE;
   a.pack_sizes.assign(n, 0);
   for (uint32_t i = 0; i < n; ++i) RINOK7(rd_num(s, &a.pack_sizes[i]));
   for (;;) {
@@ -306,6 +310,7 @@ SRes read_unpack_info(Sd& s, Ar& a) {
   RINOK7(wait_attr(s, kFolder));
   RINOK7(rd_num32(s, &nf));
   RINOK7(rd_switch(s));
+  if (nf > s.n) return SZ_ERROR_ARCHIVE;  // a folder takes >= 1 header byte
   a.folders.assign(nf, Folder());
   for (uint32_t i = 0; i < nf; ++i) RINOK7(next_folder(s, a.folders[i]));
   RINOK7(wait_attr(s, kCodersUnpackSize));
@@ -349,6 +354,9 @@ SRes read_substreams(Sd& s, Ar& a, SubStreams& ss) {
     if (t == kCRC || t == kSize || t == kEnd) break;
     RINOK7(skip_data(s));
   }
+  // a folder's substreams after its first each need a size (>= 1 header byte):
+  // more than that cannot be described by the bytes left
+  if (uint64_t(ss.n) > uint64_t(s.n) + a.folders.size()) return SZ_ERROR_ARCHIVE;
   ss.sizes.assign(ss.n, 0);
   ss.defined.assign(ss.n, 0);
   ss.digests.assign(ss.n, 0);
@@ -508,6 +516,9 @@ SRes read_header(Archive& x, Sd& s) {
   if (t != kFilesInfo) return SZ_ERROR_ARCHIVE;
   uint32_t nf;
   RINOK7(rd_num32(s, &nf));
+  // file properties cost >= 1 bit per file (kEmptyStream) or >= 2 bytes (names);
+  // a count the header bytes left cannot describe is malformed, not allocated
+  if (uint64_t(nf) > 8 * uint64_t(s.n) + 64) return SZ_ERROR_ARCHIVE;
   x.files.assign(nf, FileItem());
   std::vector<Byte> empty_stream, empty_file, defined;
   uint32_t n_empty = 0;
@@ -833,7 +844,7 @@ SRes open_checked(const Byte* arc, size_t size, Archive& x) {
 
 }  // namespace
 
-SRes LzmaGpu_7zOpen(const Byte* archive, size_t size, LzmaGpu7zFolder* folders, size_t folder_cap,
+static SRes sz_open(const Byte* archive, size_t size, LzmaGpu7zFolder* folders, size_t folder_cap,
                     size_t* n_folders, LzmaGpu7zFile* files, size_t file_cap, size_t* n_files,
                     UInt16* names, size_t names_cap, size_t* names_len, UInt64* unpack_total) {
   Archive x;
@@ -900,7 +911,7 @@ SRes LzmaGpu_7zOpen(const Byte* archive, size_t size, LzmaGpu7zFolder* folders, 
   return SZ_OK;
 }
 
-SRes LzmaGpu_7zExtract(Byte* dest, SizeT* destLen, const Byte* archive, size_t size,
+static SRes sz_extract(Byte* dest, SizeT* destLen, const Byte* archive, size_t size,
                        SRes* file_res, size_t file_cap) {
   const SizeT cap = *destLen;
   *destLen = 0;
@@ -1008,4 +1019,29 @@ SRes LzmaGpu_7zExtract(Byte* dest, SizeT* destLen, const Byte* archive, size_t s
   }
   *destLen = SizeT(total);
   return first;
+}
+
+// C ABI: no exception crosses it.  Host allocation failures (a header that
+// asks for more than the host has) return SZ_ERROR_MEM, as the reference's
+// MY_ALLOC / Buf_Create do (7zIn.c:496, 659, 1215).
+SRes LzmaGpu_7zOpen(const Byte* archive, size_t size, LzmaGpu7zFolder* folders, size_t folder_cap,
+                    size_t* n_folders, LzmaGpu7zFile* files, size_t file_cap, size_t* n_files,
+                    UInt16* names, size_t names_cap, size_t* names_len, UInt64* unpack_total) {
+  try {
+    return sz_open(archive, size, folders, folder_cap, n_folders, files, file_cap, n_files, names,
+                   names_cap, names_len, unpack_total);
+  } catch (const std::exception&) {
+    set_error("7z: host allocation failed");
+    return SZ_ERROR_MEM;
+  }
+}
+
+SRes LzmaGpu_7zExtract(Byte* dest, SizeT* destLen, const Byte* archive, size_t size,
+                       SRes* file_res, size_t file_cap) {
+  try {
+    return sz_extract(dest, destLen, archive, size, file_res, file_cap);
+  } catch (const std::exception&) {
+    set_error("7z: host allocation failed");
+    return SZ_ERROR_MEM;
+  }
 }

@@ -15,6 +15,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
+#include <exception>
 #include <vector>
 
 #include "lzma_gpu_internal.h"
@@ -303,7 +304,7 @@ SRes index_file(const Byte* f, size_t size, std::vector<LzmaGpuXzBlock>* blocks,
 
 }  // namespace
 
-SRes LzmaGpu_XzIndex(const Byte* file, size_t size, LzmaGpuXzBlock* blocks, size_t cap,
+static SRes xz_index(const Byte* file, size_t size, LzmaGpuXzBlock* blocks, size_t cap,
                      size_t* n_blocks, uint64_t* unpack_total) {
   std::vector<LzmaGpuXzBlock> v;
   uint64_t total = 0;
@@ -511,7 +512,7 @@ UInt64 Crc64Calc(const void* data, size_t size) {
   return out;
 }
 
-SRes LzmaGpu_XzDecode(Byte* dest, SizeT* destLen, const Byte* file, size_t size,
+static SRes xz_decode(Byte* dest, SizeT* destLen, const Byte* file, size_t size,
                       int64_t* bad_block) {
   const SizeT cap = *destLen;
   *destLen = 0;
@@ -688,4 +689,25 @@ SRes LzmaGpu_XzDecode(Byte* dest, SizeT* destLen, const Byte* file, size_t size,
     }
   *destLen = SizeT(total);
   return SZ_OK;
+}
+
+// C ABI: no exception crosses it (host allocation failure -> SZ_ERROR_MEM).
+SRes LzmaGpu_XzIndex(const Byte* file, size_t size, LzmaGpuXzBlock* blocks, size_t cap,
+                     size_t* n_blocks, uint64_t* unpack_total) {
+  try {
+    return xz_index(file, size, blocks, cap, n_blocks, unpack_total);
+  } catch (const std::exception&) {
+    set_error("xz: host allocation failed");
+    return SZ_ERROR_MEM;
+  }
+}
+
+SRes LzmaGpu_XzDecode(Byte* dest, SizeT* destLen, const Byte* file, size_t size,
+                      int64_t* bad_block) {
+  try {
+    return xz_decode(dest, destLen, file, size, bad_block);
+  } catch (const std::exception&) {
+    set_error("xz: host allocation failed");
+    return SZ_ERROR_MEM;
+  }
 }

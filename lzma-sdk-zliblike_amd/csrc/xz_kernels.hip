@@ -136,6 +136,10 @@ __global__ void __launch_bounds__(256) lzgpu_delta_kernel(
     const uint32_t d = delta[r];
     const uint64_t size = len[r];
     const uint32_t t = threadIdx.x;
+    // a distance outside 1..256 (Delta.h: DELTA_STATE_SIZE) is not a delta
+    // filter: the range is left as it is (uniform over the workgroup, before
+    // any barrier -- d = 0 would otherwise never leave the prefix loop)
+    if (d == 0 || d > 256) continue;
     if (t < d) st[t] = state[uint64_t(r) * 256 + t];
     __syncthreads();  // every state byte read before any is rewritten
     bra_byte* p = (bra_byte*)(data + off[r]);

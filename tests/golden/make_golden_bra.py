@@ -116,8 +116,11 @@ def main():
 
     delta = []
     rng = random.Random(5)
-    for d in (1, 2, 3, 4, 7, 16, 100, 255, 256):
-        for n in sorted({0, 1, d - 1, d, d + 1, 3 * d + 2, 5000}):
+    # 8 and 32 last (keeps the earlier cases' random draws): d = 8 is a tile-scan
+    # distance (one x += x << 64 step), 32 the segmented scan just above it
+    for d in (1, 2, 3, 4, 7, 16, 100, 255, 256, 8, 32):
+        extra = {20000, 20003} if d in (8, 32) else set()
+        for n in sorted({0, 1, d - 1, d, d + 1, 3 * d + 2, 5000} | extra):
             if n < 0:
                 continue
             for enc in (0, 1):

@@ -51,7 +51,7 @@ def main():
         files.append((f"{name} start_offset {so:#x} + LZMA2, crc32", lzma.compress(
             d[:40001], format=lzma.FORMAT_XZ, check=lzma.CHECK_CRC32,
             filters=[{"id": fid, "start_offset": so}, LZ2]), d[:40001], [(fid, so)]))
-    for dist in (1, 2, 4, 7, 256):
+    for dist in (1, 2, 4, 7, 256, 8, 32):
         d = text[:60000 + dist]
         files.append((f"Delta dist {dist} + LZMA2, sha256", lzma.compress(
             d, format=lzma.FORMAT_XZ, check=lzma.CHECK_SHA256,

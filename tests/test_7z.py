@@ -24,6 +24,7 @@ import native
 
 GOLDEN = os.path.join(native.ROOT, "tests", "golden")
 sys.path.insert(0, os.path.join(native.ROOT, "lzma-sdk-zliblike_amd"))
+sys.path.insert(0, os.path.join(native.ROOT, "tests"))
 
 
 def fixtures():
@@ -109,6 +110,37 @@ def test_open_rejects_malformed(L):
     empty = b"7z\xbc\xaf\x27\x1c\x00\x04" + struct.pack("<I", zlib.crc32(start)) + start
     r, folders, files, _, total = L.sz_open(empty)
     assert (r, folders, files, total) == (0, [], [], 0)
+
+
+def _with_header(hdr):
+    """A 7z archive whose next header is `hdr` (signature header with CRCs)."""
+    start = struct.pack("<QQI", 0, len(hdr), zlib.crc32(hdr))
+    return b"7z\xbc\xaf\x27\x1c\x00\x04" + struct.pack("<I", zlib.crc32(start)) + start + hdr
+
+
+def test_open_huge_counts_do_not_allocate(L):
+    """Counts read from an untrusted header (folders, pack streams, substreams,
+    files: up to 2^31 - 1) must not size host allocations the header bytes cannot
+    back: SZ_ERROR_ARCHIVE, never an escaping std::bad_alloc (ADVICE r01)."""
+    import sevenzwrite as W
+    big = W.number(0x7FFFFFFF)
+    cases = {
+        # kHeader kMainStreamsInfo kUnpackInfo kFolder <nf> external=0
+        "folders": bytes([0x01, 0x04, 0x07, 0x0B]) + big + b"\x00",
+        # kHeader kMainStreamsInfo kPackInfo <pos 0> <n> kSize
+        "pack sizes": bytes([0x01, 0x04, 0x06, 0x00]) + big + bytes([0x09, 0x01]),
+        # kHeader kFilesInfo <n>
+        "files": bytes([0x01, 0x05]) + big + b"\x00",
+    }
+    for name, hdr in cases.items():
+        r = L.sz_open(_with_header(hdr))[0]
+        assert r == 16, (name, r)  # SZ_ERROR_ARCHIVE
+    # one folder claiming 2^31 - 1 substreams with no sizes behind them
+    one = W.coder(W.M_COPY, b"")
+    hdr = (bytes([0x01, 0x04, 0x06, 0x00, 0x01, 0x09, 0x05, 0x00, 0x07, 0x0B, 0x01, 0x00])
+           + b"\x01" + one + bytes([0x0C, 0x05, 0x00, 0x08, 0x0D]) + big + b"\x00\x00")
+    r = L.sz_open(_with_header(hdr))[0]
+    assert r in (16, 4), r
 
 
 @pytest.mark.gpu

@@ -262,3 +262,76 @@ def test_gpu_bra_large_batch_matches_host_build(L, emu):
         got = data.cpu().numpy()
         assert (got != raw).any(), kind
         assert np.array_equal(got, want), kind
+
+
+def _delta_decode_np(data, d, state):
+    """Delta.c Delta_Decode (Delta.c:42-62) restated with numpy: residue r of the
+    output is its state byte plus the running sum of its input bytes (mod 256);
+    the new state holds the last d output bytes, oldest first."""
+    out = np.empty_like(data)
+    n = len(data)
+    st = np.frombuffer(state, np.uint8)
+    hist = np.concatenate([st[:d], np.zeros(0, np.uint8)])
+    for r in range(d):
+        seq = data[r::d].astype(np.uint64)
+        out[r::d] = ((np.cumsum(seq) + int(hist[r])) & 0xFF).astype(np.uint8)
+    new = np.concatenate([st[:d], out])[-d:] if n else st[:d]
+    full = np.frombuffer(state, np.uint8).copy()
+    full[:d] = new
+    return out, full.tobytes()
+
+
+@pytest.mark.gpu
+def test_gpu_delta_large_batch_vs_numpy(L):
+    """512 x 64 KiB ranges (the tile scan over 16 tiles, the segmented scan), d in
+    {1, 2, 4, 8, 16, 3, 255, 32}, range starts at every residue mod 16, random
+    states -- against numpy's per-residue running sums, not the kernel's own host
+    build.  Ranges with d = 0 and d = 300 are left untouched (and the call returns)."""
+    import torch
+    n, size = 512, 65536
+    rng = np.random.default_rng(11)
+    ds = [1, 2, 4, 8, 16, 3, 255, 32]
+    offs, pos = [], 0
+    for i in range(n):
+        pos += 1 + (i % 16)
+        offs.append(pos)
+        pos += size
+    raw = rng.integers(0, 256, pos + 64, dtype=np.uint8)
+    dl = np.array([ds[i % len(ds)] for i in range(n)], np.uint32)
+    dl[100], dl[200] = 0, 300
+    states = rng.integers(0, 256, 256 * n, dtype=np.uint8)
+    data = _dev(torch, raw)
+    off = _dev(torch, np.array(offs, np.uint64).view(np.int64))
+    ln = _dev(torch, np.full(n, size, np.uint64).view(np.int64))
+    dd = _dev(torch, dl.view(np.int32))
+    st = _dev(torch, states)
+    assert L.delta_batch_device(data.data_ptr(), off.data_ptr(), ln.data_ptr(), dd.data_ptr(),
+                                st.data_ptr(), n, 0) == 0
+    torch.cuda.synchronize()
+    got, sto = data.cpu().numpy(), st.cpu().numpy()
+    for i in range(n):
+        o = offs[i]
+        s_in = states[256 * i:256 * i + 256].tobytes()
+        if dl[i] in (0, 300):
+            assert np.array_equal(got[o:o + size], raw[o:o + size]), i
+            assert sto[256 * i:256 * i + 256].tobytes() == s_in, i
+            continue
+        want, want_st = _delta_decode_np(raw[o:o + size], int(dl[i]), s_in)
+        assert np.array_equal(got[o:o + size], want), (i, dl[i], o % 16)
+        assert sto[256 * i:256 * i + 256].tobytes() == want_st, (i, dl[i])
+
+
+def test_numpy_delta_restatement_matches_reference():
+    """The numpy Delta_Decode the large GPU test checks against is pinned to every
+    reference-decoded delta fixture (d = 1 .. 256, including 8 and 32)."""
+    d = fixtures()
+    seen = set()
+    for c in d["delta"]:
+        if c["encoding"]:
+            continue
+        out, st = _delta_decode_np(np.frombuffer(_get(d, c["in"], c["len"]), np.uint8),
+                                   c["delta"], _get(d, c["state_in"], 256))
+        assert out.tobytes() == _get(d, c["out"], c["len"]), c
+        assert st == _get(d, c["state_out"], 256), c
+        seen.add(c["delta"])
+    assert {8, 32} <= seen
