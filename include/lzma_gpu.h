@@ -457,6 +457,23 @@ SRes BraGpu_Batch(unsigned kind, Byte *d_data, const uint64_t *d_off, const uint
 SRes DeltaGpu_Batch(Byte *d_data, const uint64_t *d_off, const uint64_t *d_len,
                     const uint32_t *d_delta, Byte *d_state, size_t n, int encoding, void *stream);
 
+/* BCJ2 (Bcj2.c:28-128), the four-stream x86 branch decoder of 7z: buf0 = main
+ * stream, buf1 = CALL targets, buf2 = JMP / Jcc targets, buf3 = the range-coded
+ * "converted" bits.  Bcj2_Decode replaces Bcj2.h:54-59 (host buffers, computed
+ * on the GPU; buf0 may overlap outBuf as Bcj2.h:36-39 allows): SZ_OK or
+ * SZ_ERROR_DATA as the reference, SZ_ERROR_FAIL without a device.
+ * Bcj2Gpu_Batch: one lane per job, all pointers device memory, d_res[i] = the
+ * SRes of job i; asynchronous on `stream`. */
+typedef struct Bcj2GpuJob {   /* 80 bytes */
+  const Byte *buf0, *buf1, *buf2, *buf3;
+  uint64_t size0, size1, size2, size3;
+  Byte *out;
+  uint64_t out_size;
+} Bcj2GpuJob;
+int Bcj2_Decode(const Byte *buf0, SizeT size0, const Byte *buf1, SizeT size1, const Byte *buf2,
+                SizeT size2, const Byte *buf3, SizeT size3, Byte *outBuf, SizeT outSize);
+SRes Bcj2Gpu_Batch(const Bcj2GpuJob *d_jobs, size_t n, int32_t *d_res, void *stream);
+
 /* CRC-64 (XzCrc64.c, poly 0xC96C5795D7870F42).  Crc64Calc drop-in replaces
  * XzCrc64.h:20 / XzCrc64.c:30 (host buffer, GPU compute; 0 without a device).
  * The batch form mirrors CrcGpu_Batch with 2048-byte chunks planned by

@@ -36,6 +36,8 @@ extern "C" int lzgpu_launch_bcj_x86(uint8_t* d_data, const uint64_t* d_off, cons
 extern "C" int lzgpu_launch_bra(uint32_t kind, uint8_t* d_data, const uint64_t* d_off,
                                 const uint64_t* d_len, const uint32_t* d_ip, uint64_t* d_done,
                                 uint32_t n, int encoding, hipStream_t stream);
+extern "C" int lzgpu_launch_bcj2(const Bcj2GpuJob* d_jobs, uint32_t n, int32_t* d_res,
+                                 hipStream_t stream);
 extern "C" int lzgpu_launch_delta(uint8_t* d_data, const uint64_t* d_off, const uint64_t* d_len,
                                   const uint32_t* d_delta, uint8_t* d_state, uint32_t n,
                                   int encoding, hipStream_t stream);

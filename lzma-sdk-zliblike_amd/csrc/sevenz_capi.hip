@@ -590,19 +590,49 @@ SRes read_header(Archive& x, Sd& s) {
   return fill(x);
 }
 
-// One folder's decode job (SzFolder_Decode2's 1- and 2-coder shapes)
-struct Job {
+// One coder of a folder that produces bytes from a pack stream (Copy / LZMA /
+// LZMA2): its input range in the archive, its output size and where it goes.
+struct Unit {
   uint64_t pack_off = 0, pack_size = 0, avail = 0, unpack = 0, dst_off = 0;
   uint64_t method = 0;
   std::vector<Byte> props;
+  bool tmp = false;    // output in the BCJ2 temp buffer, not the folder output
+  SRes pre = SZ_OK;    // checks before decoding (props, Copy sizes, truncation)
+  SRes res = SZ_OK;    // after decoding
+};
+
+// One folder's decode job: SzFolder_Decode2 (7zDec.c:335-471).  units[0] is the
+// main coder of the 1- and 2-coder shapes; a BCJ2 folder has three units in
+// coder order 0, 1, 2 (JMP stream, CALL stream, main stream) and its range-
+// coder stream (pack stream 1) read raw from the archive.
+struct Job {
+  uint64_t pack_off = 0, pack_size = 0, unpack = 0, dst_off = 0;
+  std::vector<Unit> units;
   bool x86 = false;
   bool arm = false;
+  bool bcj2 = false;
+  uint64_t rc_off = 0, rc_size = 0, rc_avail = 0;
   SRes res = SZ_OK;
 };
 
-// CheckSupportedFolder (7zDec.c:269-322) + the coder checks SzDecodeLzma /
-// SzDecodeLzma2 make before decoding.  BCJ2 folders pass the reference's
-// check but are not built here: SZ_ERROR_UNSUPPORTED.
+// A coder's checks before it decodes: SzDecodeCopy / SzDecodeLzma /
+// SzDecodeLzma2 (7zDec.c:127-241) as far as they fail without decoding.
+static void unit_checks(Unit& u) {
+  u.pre = SZ_OK;
+  if (u.method == kCopy) {
+    if (u.pack_size != u.unpack) u.pre = SZ_ERROR_DATA;
+    else if (u.avail < u.pack_size) u.pre = SZ_ERROR_INPUT_EOF;
+  } else if (u.method == kLzma) {
+    // LzmaProps_Decode (LzmaDec.c:898-922)
+    if (u.props.size() < 5 || u.props[0] >= 9 * 5 * 5) u.pre = SZ_ERROR_UNSUPPORTED;
+  } else {
+    // SzDecodeLzma2 (7zDec.c:181-183) + Lzma2Dec_GetOldProps (Lzma2Dec.c:69)
+    if (u.props.size() != 1) u.pre = SZ_ERROR_DATA;
+    else if (u.props[0] > 40) u.pre = SZ_ERROR_UNSUPPORTED;
+  }
+}
+
+// CheckSupportedFolder (7zDec.c:269-322) and the job of each folder shape.
 Job make_job(const Archive& x, const Ar& a, uint32_t fi, uint64_t start, const Byte*, size_t size) {
   Job j;
   const Folder& f = a.folders[fi];
@@ -614,6 +644,30 @@ Job make_job(const Archive& x, const Ar& a, uint32_t fi, uint64_t start, const B
   const size_t nc = f.coders.size();
   j.res = SZ_ERROR_UNSUPPORTED;
   if (nc < 1 || nc > 4 || !main_ok(f.coders[0])) return j;
+  const uint32_t ps = x.folder_start_pack.empty() ? 0 : x.folder_start_pack[fi];
+  auto pack_size = [&](uint32_t k) {
+    return ps + k < a.pack_sizes.size() ? a.pack_sizes[ps + k] : uint64_t(0);
+  };
+  // pack stream k of the folder starts behind streams 0..k-1 (GetSum, 7zDec.c:325)
+  auto pack_at = [&](uint32_t k) {
+    uint64_t o = start;
+    for (uint32_t i = 0; i < k; ++i) o += pack_size(i);
+    return o;
+  };
+  auto avail = [&](uint64_t off, uint64_t n) {
+    return off >= size ? uint64_t(0) : std::min<uint64_t>(n, size - off);
+  };
+  auto unit = [&](const Coder& c, uint32_t si, uint64_t unpack) {
+    Unit u;
+    u.method = c.method;
+    u.props = c.props;
+    u.pack_size = pack_size(si);
+    u.pack_off = pack_at(si);
+    u.avail = avail(u.pack_off, u.pack_size);
+    u.unpack = unpack;
+    unit_checks(u);
+    return u;
+  };
   if (nc == 1) {
     if (f.pack_streams.size() != 1 || f.pack_streams[0] != 0 || !f.bind.empty()) return j;
   } else if (nc == 2) {
@@ -627,103 +681,219 @@ Job make_job(const Archive& x, const Ar& a, uint32_t fi, uint64_t start, const B
       j.arm = true;  // CASE_BRA_CONV(ARM), 7zDec.c:449
     else
       return j;
+  } else if (nc == 4) {
+    // IS_BCJ2 and the only bind layout the reference accepts (7zDec.c:303-319)
+    const Coder& b = f.coders[3];
+    if (!main_ok(f.coders[1]) || !main_ok(f.coders[2]) || b.method != kBcj2 || b.nin != 4 ||
+        b.nout != 1)
+      return j;
+    static const uint32_t kPs[4] = {2, 6, 1, 0};
+    static const uint32_t kBin[3] = {5, 4, 3}, kBout[3] = {0, 1, 2};
+    if (f.pack_streams.size() != 4 || f.bind.size() != 3) return j;
+    for (int k = 0; k < 4; ++k)
+      if (f.pack_streams[k] != kPs[k]) return j;
+    for (int k = 0; k < 3; ++k)
+      if (f.bind[k].in != kBin[k] || f.bind[k].out != kBout[k]) return j;
+    if (f.unpack_sizes.size() < 4) return j;
+    j.bcj2 = true;
+    // coder ci reads pack stream {3, 2, 0}[ci] (7zDec.c:356-359)
+    static const uint32_t kSi[3] = {3, 2, 0};
+    for (uint32_t ci = 0; ci < 3; ++ci) {
+      j.units.push_back(unit(f.coders[ci], kSi[ci], f.unpack_sizes[ci]));
+      j.units.back().tmp = ci < 2;
+    }
+    j.rc_off = pack_at(1);
+    j.rc_size = pack_size(1);
+    j.rc_avail = avail(j.rc_off, j.rc_size);
+    j.pack_off = j.units[2].pack_off;  // the main stream's coder
+    j.pack_size = j.units[2].pack_size;
+    j.res = SZ_OK;
+    return j;
   } else {
-    return j;  // the BCJ2 layout (4 coders): not built here
+    return j;
   }
-  (void)kBcj2;
-  const Coder& c = f.coders[0];
-  j.method = c.method;
-  j.props = c.props;
-  const uint32_t ps = x.folder_start_pack.empty() ? 0 : x.folder_start_pack[fi];
-  j.pack_size = ps < a.pack_sizes.size() ? a.pack_sizes[ps] : 0;
-  j.pack_off = start;
-  j.avail = start >= size ? 0 : std::min<uint64_t>(j.pack_size, size - start);
-  j.res = SZ_OK;
-  if (c.method == kCopy) {
-    if (j.pack_size != j.unpack) j.res = SZ_ERROR_DATA;
-    else if (j.avail < j.pack_size) j.res = SZ_ERROR_INPUT_EOF;
-  } else if (c.method == kLzma) {
-    // LzmaProps_Decode (LzmaDec.c:898-922)
-    if (c.props.size() < 5 || c.props[0] >= 9 * 5 * 5) j.res = SZ_ERROR_UNSUPPORTED;
-  } else {
-    // SzDecodeLzma2 (7zDec.c:181-183) + Lzma2Dec_GetOldProps (Lzma2Dec.c:69)
-    if (c.props.size() != 1) j.res = SZ_ERROR_DATA;
-    else if (c.props[0] > 40) j.res = SZ_ERROR_UNSUPPORTED;
-  }
+  j.units.push_back(unit(f.coders[0], 0, j.unpack));
+  j.pack_off = j.units[0].pack_off;
+  j.pack_size = j.units[0].pack_size;
+  j.res = j.units[0].pre;
   return j;
+}
+
+// Bytes of BCJ2 temp output (the CALL and JMP streams) a job list needs.
+uint64_t bcj2_temp_bytes(const std::vector<Job>& jobs) {
+  uint64_t t = 0;
+  for (const Job& j : jobs)
+    if (j.bcj2)
+      for (const Unit& u : j.units)
+        if (u.tmp) t += u.unpack;
+  return t;
+}
+
+// SzDecodeLzma / SzDecodeLzma2 acceptance (7zDec.c:161-168, 209-216): the
+// whole output, the whole pack stream, a finished status
+static SRes accept(const Unit& u, const LzmaGpuResult& q) {
+  if (q.res != SZ_OK) return q.res;
+  const bool status_ok = u.method == kLzma ? (q.status == LZMA_STATUS_FINISHED_WITH_MARK ||
+                                              q.status == LZMA_STATUS_MAYBE_FINISHED_WITHOUT_MARK)
+                                           : q.status == LZMA_STATUS_FINISHED_WITH_MARK;
+  if (q.dest_len != u.unpack || q.src_len != u.avail || u.avail != u.pack_size || !status_ok)
+    return SZ_ERROR_DATA;
+  return SZ_OK;
+}
+
+// Decodes a list of units whose outputs go to `dst` (device) in one batch.
+static SRes decode_units(std::vector<Unit*>& us, const Byte* d_arc, Byte* dst) {
+  std::vector<LzmaGpuStreamDesc> descs;
+  std::vector<Unit*> which;
+  for (Unit* u : us) {
+    if (u->method == kCopy) {
+      if (u->unpack && !hip_ok(hipMemcpyAsync(dst + u->dst_off, d_arc + u->pack_off, u->unpack,
+                                              hipMemcpyDeviceToDevice, nullptr),
+                               "7z copy coder"))
+        return SZ_ERROR_FAIL;
+      u->res = SZ_OK;
+      continue;
+    }
+    LzmaGpuStreamDesc d;
+    memset(&d, 0, sizeof d);
+    d.src_off = u->pack_off;
+    d.src_len = u->avail;
+    d.dst_off = u->dst_off;
+    d.dst_cap = u->unpack;
+    d.finish_mode = LZMA_FINISH_END;
+    if (u->method == kLzma) {
+      memcpy(d.props, u->props.data(), 5);
+      d.props_size = 5;
+      d.kind = LZMA_GPU_KIND_LZMA;
+    } else {
+      d.props[0] = u->props[0];
+      d.props_size = 1;
+      d.kind = LZMA_GPU_KIND_LZMA2;
+    }
+    descs.push_back(d);
+    which.push_back(u);
+  }
+  const size_t n = descs.size();
+  if (n == 0) return SZ_OK;
+  std::vector<LzmaGpuResult> res(n);
+  std::vector<uint32_t> order(n);
+  LzmaGpuPlan plan;
+  SRes r = LzmaGpu_PlanBatchEx(descs.data(), n, order.data(), &plan);
+  if (r != SZ_OK) return r;
+  DevArr<Byte> d_ws;
+  DevArr<LzmaGpuStreamDesc> d_desc;
+  DevArr<uint32_t> d_order;
+  DevArr<LzmaGpuResult> d_res;
+  if (!d_ws.alloc(plan.workspace_bytes) || !d_desc.alloc(n) || !d_order.alloc(n) ||
+      !d_res.alloc(n)) {
+    set_error("7z: device allocation failed");
+    return SZ_ERROR_MEM;
+  }
+  if (!hip_ok(hipMemcpy(d_desc.p, descs.data(), n * sizeof(LzmaGpuStreamDesc),
+                        hipMemcpyHostToDevice), "7z H2D") ||
+      !hip_ok(hipMemcpy(d_order.p, order.data(), n * 4, hipMemcpyHostToDevice), "7z H2D"))
+    return SZ_ERROR_FAIL;
+  if ((r = LzmaGpu_DecodeBatchEx(&plan, d_desc.p, d_order.p, d_arc, dst, d_ws.p, d_res.p,
+                                 nullptr)) != SZ_OK)
+    return r;
+  if (!hip_ok(hipDeviceSynchronize(), "7z decode") ||
+      !hip_ok(hipMemcpy(res.data(), d_res.p, n * sizeof(LzmaGpuResult), hipMemcpyDeviceToHost),
+              "7z D2H"))
+    return SZ_ERROR_FAIL;
+  for (size_t k = 0; k < n; ++k) which[k]->res = accept(*which[k], res[k]);
+  return SZ_OK;
 }
 
 // Runs the folder jobs on the GPU from the archive already in d_arc, output
 // at each job's dst_off in d_dst; sets each job's res to SzFolder_Decode's.
-SRes run_jobs(std::vector<Job>& jobs, const Byte* d_arc, Byte* d_dst) {
-  std::vector<LzmaGpuStreamDesc> descs;
-  std::vector<size_t> which;
+// d_dst holds bcj2_temp_bytes(jobs) more bytes behind the folder outputs
+// (at dst_bytes): the BCJ2 folders' CALL and JMP streams.
+SRes run_jobs(std::vector<Job>& jobs, const Byte* d_arc, Byte* d_dst, uint64_t dst_bytes) {
+  std::vector<Unit*> units;
   std::vector<uint64_t> bcj_off, bcj_len, arm_off, arm_len;
-  for (size_t i = 0; i < jobs.size(); ++i) {
-    Job& j = jobs[i];
+  uint64_t tmp = dst_bytes;
+  for (Job& j : jobs) {
     if (j.res != SZ_OK) continue;
-    if (j.method == kCopy) {
-      if (j.unpack && !hip_ok(hipMemcpyAsync(d_dst + j.dst_off, d_arc + j.pack_off, j.unpack,
-                                             hipMemcpyDeviceToDevice, nullptr),
-                              "7z copy folder"))
-        return SZ_ERROR_FAIL;
-    } else {
-      LzmaGpuStreamDesc d;
-      memset(&d, 0, sizeof d);
-      d.src_off = j.pack_off;
-      d.src_len = j.avail;
-      d.dst_off = j.dst_off;
-      d.dst_cap = j.unpack;
-      d.finish_mode = LZMA_FINISH_END;
-      if (j.method == kLzma) {
-        memcpy(d.props, j.props.data(), 5);
-        d.props_size = 5;
-        d.kind = LZMA_GPU_KIND_LZMA;
-      } else {
-        d.props[0] = j.props[0];
-        d.props_size = 1;
-        d.kind = LZMA_GPU_KIND_LZMA2;
+    if (!j.bcj2) {
+      Unit& u = j.units[0];
+      u.dst_off = j.dst_off;
+      units.push_back(&u);
+      if (j.x86 && j.unpack) {
+        bcj_off.push_back(j.dst_off);
+        bcj_len.push_back(j.unpack);
       }
-      descs.push_back(d);
-      which.push_back(i);
+      if (j.arm && j.unpack) {
+        arm_off.push_back(j.dst_off);
+        arm_len.push_back(j.unpack);
+      }
+      continue;
     }
-    if (j.x86 && j.unpack) {
-      bcj_off.push_back(j.dst_off);
-      bcj_len.push_back(j.unpack);
-    }
-    if (j.arm && j.unpack) {
-      arm_off.push_back(j.dst_off);
-      arm_len.push_back(j.unpack);
+    // SzFolder_Decode2 stops at the first failing coder, in coder order; the
+    // main stream coder (2) first checks that its output fits (7zDec.c:370)
+    for (uint32_t ci = 0; ci < 3; ++ci) {
+      Unit& u = j.units[ci];
+      if (ci == 2 && u.unpack > j.unpack) break;
+      if (u.pre != SZ_OK) break;
+      if (u.tmp) {
+        u.dst_off = tmp;
+        tmp += u.unpack;
+      } else {
+        u.dst_off = j.dst_off + (j.unpack - u.unpack);  // the tail of the folder output
+      }
+      units.push_back(&u);
     }
   }
-  const size_t n = descs.size(), nb = bcj_off.size();
-  std::vector<LzmaGpuResult> res(n);
-  if (n) {
-    std::vector<uint32_t> order(n);
-    LzmaGpuPlan plan;
-    SRes r = LzmaGpu_PlanBatchEx(descs.data(), n, order.data(), &plan);
-    if (r != SZ_OK) return r;
-    DevArr<Byte> d_ws;
-    DevArr<LzmaGpuStreamDesc> d_desc;
-    DevArr<uint32_t> d_order;
-    DevArr<LzmaGpuResult> d_res;
-    if (!d_ws.alloc(plan.workspace_bytes) || !d_desc.alloc(n) || !d_order.alloc(n) ||
-        !d_res.alloc(n)) {
-      set_error("7z: device allocation failed");
-      return SZ_ERROR_MEM;
+  RINOK7(decode_units(units, d_arc, d_dst));
+  // BCJ2 folders: the first failure in coder order, else the rc stream and
+  // Bcj2_Decode (7zDec.c:423-441)
+  std::vector<Bcj2GpuJob> b2;
+  std::vector<Job*> b2_job;
+  for (Job& j : jobs) {
+    if (j.res != SZ_OK) continue;
+    if (!j.bcj2) {
+      j.res = j.units[0].res;
+      continue;
     }
-    if (!hip_ok(hipMemcpy(d_desc.p, descs.data(), n * sizeof(LzmaGpuStreamDesc),
-                          hipMemcpyHostToDevice), "7z H2D") ||
-        !hip_ok(hipMemcpy(d_order.p, order.data(), n * 4, hipMemcpyHostToDevice), "7z H2D"))
-      return SZ_ERROR_FAIL;
-    if ((r = LzmaGpu_DecodeBatchEx(&plan, d_desc.p, d_order.p, d_arc, d_dst, d_ws.p, d_res.p,
-                                   nullptr)) != SZ_OK)
-      return r;
-    if (!hip_ok(hipDeviceSynchronize(), "7z decode") ||
-        !hip_ok(hipMemcpy(res.data(), d_res.p, n * sizeof(LzmaGpuResult), hipMemcpyDeviceToHost),
-                "7z D2H"))
-      return SZ_ERROR_FAIL;
+    SRes r = SZ_OK;
+    for (uint32_t ci = 0; ci < 3 && r == SZ_OK; ++ci) {
+      const Unit& u = j.units[ci];
+      if (ci == 2 && u.unpack > j.unpack) r = SZ_ERROR_PARAM;
+      else if (u.pre != SZ_OK) r = u.pre;
+      else r = u.res;
+    }
+    if (r == SZ_OK && j.rc_avail < j.rc_size) r = SZ_ERROR_INPUT_EOF;  // SzDecodeCopy
+    j.res = r;
+    if (r != SZ_OK) continue;
+    Bcj2GpuJob q;
+    q.buf0 = d_dst + j.units[2].dst_off;
+    q.size0 = j.units[2].unpack;
+    q.buf1 = d_dst + j.units[1].dst_off;  // CALL stream: coder 1 (tempBuf[0])
+    q.size1 = j.units[1].unpack;
+    q.buf2 = d_dst + j.units[0].dst_off;  // JMP stream: coder 0 (tempBuf[1])
+    q.size2 = j.units[0].unpack;
+    q.buf3 = d_arc + j.rc_off;
+    q.size3 = j.rc_size;
+    q.out = d_dst + j.dst_off;
+    q.out_size = j.unpack;
+    b2.push_back(q);
+    b2_job.push_back(&j);
   }
+  if (!b2.empty()) {
+    const size_t n = b2.size();
+    DevArr<Bcj2GpuJob> d_jobs;
+    DevArr<int32_t> d_res;
+    std::vector<int32_t> res(n);
+    if (!d_jobs.alloc(n) || !d_res.alloc(n)) return SZ_ERROR_MEM;
+    if (!hip_ok(hipMemcpy(d_jobs.p, b2.data(), n * sizeof(Bcj2GpuJob), hipMemcpyHostToDevice),
+                "7z H2D"))
+      return SZ_ERROR_FAIL;
+    RINOK7(Bcj2Gpu_Batch(d_jobs.p, n, d_res.p, nullptr));
+    if (!hip_ok(hipDeviceSynchronize(), "7z BCJ2") ||
+        !hip_ok(hipMemcpy(res.data(), d_res.p, n * 4, hipMemcpyDeviceToHost), "7z D2H"))
+      return SZ_ERROR_FAIL;
+    for (size_t k = 0; k < n; ++k) b2_job[k]->res = res[k];
+  }
+  const size_t nb = bcj_off.size();
   if (nb) {  // x86_Convert(outBuffer, outSize, 0, &state0, 0) per BCJ folder
     DevArr<uint64_t> d64;
     DevArr<uint32_t> d32;
@@ -755,22 +925,6 @@ SRes run_jobs(std::vector<Job>& jobs, const Byte* d_arc, Byte* d_dst) {
     SRes r = BraGpu_Batch(7, d_dst, d64.p, d64.p + na, d32.p, d64.p + 2 * na, na, 0, nullptr);
     if (r != SZ_OK) return r;
     if (!hip_ok(hipDeviceSynchronize(), "7z ARM")) return SZ_ERROR_FAIL;
-  }
-  // SzDecodeLzma / SzDecodeLzma2 acceptance (7zDec.c:161-168, 209-216): the
-  // whole output, the whole pack stream, a finished status
-  for (size_t k = 0; k < n; ++k) {
-    Job& j = jobs[which[k]];
-    const LzmaGpuResult& q = res[k];
-    if (q.res != SZ_OK) {
-      j.res = q.res;
-      continue;
-    }
-    const bool status_ok = j.method == kLzma
-                               ? (q.status == LZMA_STATUS_FINISHED_WITH_MARK ||
-                                  q.status == LZMA_STATUS_MAYBE_FINISHED_WITHOUT_MARK)
-                               : q.status == LZMA_STATUS_FINISHED_WITH_MARK;
-    if (q.dest_len != j.unpack || q.src_len != j.avail || j.avail != j.pack_size || !status_ok)
-      j.res = SZ_ERROR_DATA;
   }
   return SZ_OK;
 }
@@ -813,15 +967,20 @@ SRes open_archive(const Byte* arc, size_t size, Archive& x) {
     if (jobs[0].res != SZ_OK) return jobs[0].res;
     unpacked.resize(size_t(f.unpack_size()));
     if (!ensure_device()) return SZ_ERROR_FAIL;
-    // only the header's pack stream goes to the device
-    const uint64_t at = jobs[0].pack_off, nbytes = jobs[0].avail;
-    jobs[0].pack_off = 0;
+    // only the header's pack stream goes to the device (a BCJ2-packed header:
+    // the archive)
+    const bool one = !jobs[0].bcj2;
+    const uint64_t at = one ? jobs[0].units[0].pack_off : 0;
+    const uint64_t nbytes = one ? jobs[0].units[0].avail : uint64_t(size);
+    if (one) jobs[0].units[0].pack_off = 0;
     DevArr<Byte> d_arc, d_out;
-    if (!d_arc.alloc(size_t(nbytes)) || !d_out.alloc(unpacked.size())) return SZ_ERROR_MEM;
+    if (!d_arc.alloc(size_t(nbytes)) ||
+        !d_out.alloc(unpacked.size() + size_t(bcj2_temp_bytes(jobs))))
+      return SZ_ERROR_MEM;
     if (nbytes && !hip_ok(hipMemcpy(d_arc.p, arc + at, size_t(nbytes), hipMemcpyHostToDevice),
                           "7z H2D"))
       return SZ_ERROR_FAIL;
-    RINOK7(run_jobs(jobs, d_arc.p, d_out.p));
+    RINOK7(run_jobs(jobs, d_arc.p, d_out.p, unpacked.size()));
     if (jobs[0].res != SZ_OK) return jobs[0].res;
     if (!unpacked.empty() &&
         !hip_ok(hipMemcpy(unpacked.data(), d_out.p, unpacked.size(), hipMemcpyDeviceToHost),
@@ -945,13 +1104,13 @@ static SRes sz_extract(Byte* dest, SizeT* destLen, const Byte* archive, size_t s
   if (nf) {
     if (!ensure_device()) return SZ_ERROR_FAIL;
     DevArr<Byte> d_arc, d_dst;
-    if (!d_arc.alloc(size) || !d_dst.alloc(total)) {
+    if (!d_arc.alloc(size) || !d_dst.alloc(total + bcj2_temp_bytes(jobs))) {
       set_error("7z: device allocation failed");
       return SZ_ERROR_MEM;
     }
     if (!hip_ok(hipMemcpy(d_arc.p, archive, size, hipMemcpyHostToDevice), "7z H2D"))
       return SZ_ERROR_FAIL;
-    RINOK7(run_jobs(jobs, d_arc.p, d_dst.p));
+    RINOK7(run_jobs(jobs, d_arc.p, d_dst.p, total));
     // CRC-32 of every decoded folder with a CRC and of every file range
     std::vector<uint64_t> off, len;
     std::vector<int64_t> tag;  // >= 0: folder, < 0: ~file

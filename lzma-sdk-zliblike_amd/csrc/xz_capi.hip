@@ -484,6 +484,82 @@ SRes DeltaGpu_Batch(Byte* d_data, const uint64_t* d_off, const uint64_t* d_len,
   return SZ_OK;
 }
 
+SRes Bcj2Gpu_Batch(const Bcj2GpuJob* d_jobs, size_t n, int32_t* d_res, void* stream) {
+  if (!ensure_device()) return SZ_ERROR_FAIL;
+  if (n > 0xFFFFFFFFull) return SZ_ERROR_PARAM;
+  if (lzgpu_launch_bcj2(d_jobs, uint32_t(n), d_res, static_cast<hipStream_t>(stream)) != 0) {
+    set_error("BCJ2 kernel launch failed");
+    return SZ_ERROR_FAIL;
+  }
+  return SZ_OK;
+}
+
+// Bcj2_Decode over host buffers: the four streams and the output go to the
+// device (buf0 inside outBuf, as 7zDec.c:367-372 places it, stays inside the
+// device copy of outBuf at the same offset), one lane decodes, the output
+// comes back.
+static int bcj2_host(const Byte* buf0, SizeT size0, const Byte* buf1, SizeT size1,
+                     const Byte* buf2, SizeT size2, const Byte* buf3, SizeT size3, Byte* outBuf,
+                     SizeT outSize) {
+  if (!ensure_device()) return SZ_ERROR_FAIL;
+  const uintptr_t o0 = uintptr_t(outBuf), o1 = o0 + outSize, b0 = uintptr_t(buf0);
+  const bool inside = size0 && b0 >= o0 && b0 < o1;
+  // device layout: [out (+ main tail beyond it) | buf0 | buf1 | buf2 | buf3]
+  const uint64_t out_room = inside ? std::max<uint64_t>(outSize, (b0 - o0) + size0) : outSize;
+  const uint64_t off0 = out_room, off1 = off0 + (inside ? 0 : size0), off2 = off1 + size1,
+                 off3 = off2 + size2, total = off3 + size3;
+  DevArr<Byte> d;
+  DevArr<Bcj2GpuJob> dj;
+  DevArr<int32_t> dr;
+  if (!d.alloc(size_t(total)) || !dj.alloc(1) || !dr.alloc(1)) {
+    set_error("Bcj2_Decode: device allocation failed");
+    return SZ_ERROR_MEM;
+  }
+  auto up = [&](uint64_t at, const Byte* p, uint64_t n) {
+    return n == 0 || hip_ok(hipMemcpy(d.p + at, p, size_t(n), hipMemcpyHostToDevice), "Bcj2 H2D");
+  };
+  bool ok = true;
+  if (inside) {
+    // the host bytes of outBuf (main stream included) and any main tail beyond it
+    ok = up(0, outBuf, outSize);
+    if (ok && (b0 - o0) + size0 > outSize)
+      ok = up(outSize, reinterpret_cast<const Byte*>(o1), (b0 - o0) + size0 - outSize);
+  } else {
+    // bytes the decoder does not write (an error exit) keep the caller's values
+    ok = up(0, outBuf, outSize) && up(off0, buf0, size0);
+  }
+  ok = ok && up(off1, buf1, size1) && up(off2, buf2, size2) && up(off3, buf3, size3);
+  if (!ok) return SZ_ERROR_FAIL;
+  Bcj2GpuJob j;
+  j.buf0 = inside ? d.p + (b0 - o0) : d.p + off0;
+  j.buf1 = d.p + off1;
+  j.buf2 = d.p + off2;
+  j.buf3 = d.p + off3;
+  j.size0 = size0;
+  j.size1 = size1;
+  j.size2 = size2;
+  j.size3 = size3;
+  j.out = d.p;
+  j.out_size = outSize;
+  int32_t r = SZ_ERROR_FAIL;
+  if (!hip_ok(hipMemcpy(dj.p, &j, sizeof j, hipMemcpyHostToDevice), "Bcj2 H2D") ||
+      Bcj2Gpu_Batch(dj.p, 1, dr.p, nullptr) != SZ_OK || !hip_ok(hipDeviceSynchronize(), "Bcj2") ||
+      !hip_ok(hipMemcpy(&r, dr.p, 4, hipMemcpyDeviceToHost), "Bcj2 D2H") ||
+      (outSize && !hip_ok(hipMemcpy(outBuf, d.p, outSize, hipMemcpyDeviceToHost), "Bcj2 D2H")))
+    return SZ_ERROR_FAIL;
+  return r;
+}
+
+int Bcj2_Decode(const Byte* buf0, SizeT size0, const Byte* buf1, SizeT size1, const Byte* buf2,
+                SizeT size2, const Byte* buf3, SizeT size3, Byte* outBuf, SizeT outSize) {
+  try {
+    return bcj2_host(buf0, size0, buf1, size1, buf2, size2, buf3, size3, outBuf, outSize);
+  } catch (const std::exception&) {
+    set_error("Bcj2_Decode: host allocation failed");
+    return SZ_ERROR_MEM;
+  }
+}
+
 UInt64 Crc64Calc(const void* data, size_t size) {
   if (!ensure_device()) return 0;
   if (size == 0) return 0;

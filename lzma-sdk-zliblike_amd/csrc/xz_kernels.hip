@@ -12,6 +12,8 @@
 
 #include <cstdlib>
 
+#include "../../include/lzma_gpu.h"
+#include "bcj2_device.h"
 #include "bcj_device.h"
 #include "bra_device.h"
 #include "crc64_device.h"
@@ -233,6 +235,29 @@ __global__ void __launch_bounds__(256) lzgpu_delta_kernel(
     }
     __syncthreads();
   }
+}
+
+// BCJ2 (Bcj2.c:28-128): one lane per job, the 258 probabilities in the
+// lane's LDS slice; the main stream may be the tail of the job's output.
+__global__ void __launch_bounds__(64) lzgpu_bcj2_kernel(const Bcj2GpuJob* __restrict__ jobs,
+                                                       uint32_t n, int32_t* __restrict__ res) {
+  __shared__ uint16_t probs[64 * 258];
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  typedef __attribute__((address_space(3))) uint16_t lds16;
+  typedef __attribute__((address_space(1))) uint8_t gb;
+  lds16* p = (lds16*)probs + threadIdx.x * 258;
+  const Bcj2GpuJob j = jobs[i];
+  res[i] = bcj2_decode((const gb*)j.buf0, j.size0, (const gb*)j.buf1, j.size1, (const gb*)j.buf2,
+                       j.size2, (const gb*)j.buf3, j.size3, (gb*)j.out, j.out_size, p);
+}
+
+extern "C" int lzgpu_launch_bcj2(const Bcj2GpuJob* d_jobs, uint32_t n, int32_t* d_res,
+                                 hipStream_t stream) {
+  if (n == 0) return 0;
+  hipLaunchKernelGGL(lzgpu_bcj2_kernel, dim3((n + 63) / 64), dim3(64), 0, stream, d_jobs, n,
+                     d_res);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
 extern "C" int lzgpu_launch_bra(uint32_t kind, uint8_t* d_data, const uint64_t* d_off,

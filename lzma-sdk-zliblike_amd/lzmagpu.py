@@ -140,6 +140,14 @@ class XzBlock(ctypes.Structure):
                 ("filter_prop", ctypes.c_uint32 * 3)]
 
 
+class Bcj2Job(ctypes.Structure):
+    """Bcj2GpuJob (include/lzma_gpu.h): one BCJ2 decode, device pointers."""
+    _fields_ = [("buf0", ctypes.c_void_p), ("buf1", ctypes.c_void_p), ("buf2", ctypes.c_void_p),
+                ("buf3", ctypes.c_void_p), ("size0", ctypes.c_uint64), ("size1", ctypes.c_uint64),
+                ("size2", ctypes.c_uint64), ("size3", ctypes.c_uint64), ("out", ctypes.c_void_p),
+                ("out_size", ctypes.c_uint64)]
+
+
 class SzFolder(ctypes.Structure):
     """LzmaGpu7zFolder (include/lzma_gpu.h): one folder of an opened 7z archive."""
     _fields_ = [("pack_off", ctypes.c_uint64), ("pack_size", ctypes.c_uint64),
@@ -160,7 +168,7 @@ class SzFile(ctypes.Structure):
                 ("name_len", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
 
 
-assert ctypes.sizeof(XzBlock) == 104
+assert ctypes.sizeof(XzBlock) == 104 and ctypes.sizeof(Bcj2Job) == 80
 assert ctypes.sizeof(SzFolder) == 80 and ctypes.sizeof(SzFile) == 48
 assert ctypes.sizeof(StreamDesc) == 48 and ctypes.sizeof(Result) == 24
 assert ctypes.sizeof(Session) == 192 and ctypes.sizeof(Plan) == 184
@@ -216,6 +224,8 @@ _sig = {
     "Delta_Decode": (None, [_P, ctypes.c_uint, _P, ctypes.c_size_t]),
     "BraGpu_Batch": (ctypes.c_int, [ctypes.c_uint, _P, _P, _P, _P, _P, ctypes.c_size_t, ctypes.c_int, _P]),
     "DeltaGpu_Batch": (ctypes.c_int, [_P, _P, _P, _P, _P, ctypes.c_size_t, ctypes.c_int, _P]),
+    "Bcj2_Decode": (ctypes.c_int, [_P, ctypes.c_size_t, _P, ctypes.c_size_t, _P, ctypes.c_size_t, _P, ctypes.c_size_t, _P, ctypes.c_size_t]),
+    "Bcj2Gpu_Batch": (ctypes.c_int, [_P, ctypes.c_size_t, _P, _P]),
     "Crc64Calc": (ctypes.c_uint64, [_P, ctypes.c_size_t]),
     "Crc64Gpu_Batch": (ctypes.c_int, [_P, _P, _P, ctypes.c_size_t, _P, _P, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_uint64, _P, _P, _P]),
     "LzmaGpu_XzIndex": (ctypes.c_int, [_P, ctypes.c_size_t, ctypes.POINTER(XzBlock), ctypes.c_size_t, _sp, ctypes.POINTER(ctypes.c_uint64)]),
@@ -515,6 +525,29 @@ def bra_batch_device(kind, d_data, d_off, d_len, d_ip, d_done, n, encoding=0, st
 def delta_batch_device(d_data, d_off, d_len, d_delta, d_state, n, encoding=0, stream=0):
     """DeltaGpu_Batch over raw device pointers (ints)."""
     return _lib.DeltaGpu_Batch(d_data, d_off, d_len, d_delta, d_state, n, encoding, stream or None)
+
+
+def Bcj2_Decode(main, call, jump, rc, out_size, overlap=False, fill=0xA5):
+    """Bcj2.c Bcj2_Decode on the GPU over host buffers: (res, output buffer).
+    The output buffer starts as `fill` bytes; overlap: the main stream sits at
+    its tail (the 7zDec.c:367-372 layout)."""
+    out = ctypes.create_string_buffer(bytes([fill]) * max(out_size, 1), max(out_size, 1))
+    bufs = [_buf(x) for x in (call, jump, rc)]
+    if overlap:
+        at = out_size - len(main)
+        ctypes.memmove(ctypes.addressof(out) + at, bytes(main), len(main))
+        m = ctypes.addressof(out) + at
+    else:
+        mb = _buf(main)
+        m = ctypes.addressof(mb)
+    r = _lib.Bcj2_Decode(m, len(main), bufs[0], len(call), bufs[1], len(jump), bufs[2], len(rc),
+                         out, out_size)
+    return r, out.raw[:out_size]
+
+
+def bcj2_batch_device(d_jobs, n, d_res, stream=0):
+    """Bcj2Gpu_Batch over a device array of n Bcj2Job."""
+    return _lib.Bcj2Gpu_Batch(d_jobs, n, d_res, stream or None)
 
 
 def Crc64Calc(data):

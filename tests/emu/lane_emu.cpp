@@ -13,6 +13,7 @@
 #include "../../lzma-sdk-zliblike_amd/csrc/crc32_device.h"
 #include "../../lzma-sdk-zliblike_amd/csrc/crc64_device.h"
 #include "../../lzma-sdk-zliblike_amd/csrc/bcj_device.h"
+#include "../../lzma-sdk-zliblike_amd/csrc/bcj2_device.h"
 #include "../../lzma-sdk-zliblike_amd/csrc/bra_device.h"
 
 using namespace lzgpu;
@@ -165,6 +166,14 @@ void emu_crc64_ranges(const uint8_t* data, const uint64_t* off, const uint64_t* 
 // loads aligned 16-byte blocks holding a valid byte: callers pad buffers.
 uint64_t emu_bcj_x86(uint8_t* data, uint64_t size, uint32_t ip, uint32_t* state, int encoding) {
   return bcj_x86(data, size, ip, state, encoding);
+}
+
+// lzgpu_bcj2_kernel's lane (bcj2_decode) on host buffers; probabilities in a
+// lane-private array as the kernel's LDS slice.
+int emu_bcj2(const uint8_t* b0, uint64_t s0, const uint8_t* b1, uint64_t s1, const uint8_t* b2,
+             uint64_t s2, const uint8_t* b3, uint64_t s3, uint8_t* out, uint64_t out_size) {
+  uint16_t probs[258];
+  return bcj2_decode(b0, s0, b1, s1, b2, s2, b3, s3, out, out_size, probs);
 }
 
 // The branch-converter kernels' code on one buffer, unit by unit in lane

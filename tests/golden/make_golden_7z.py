@@ -6,13 +6,16 @@ Run in the build container only (needs oracle/_ref/libref.so from
 
     python tests/golden/make_golden_7z.py
 
-Archives are written here (lzma-sdk-zliblike_amd/sevenzwrite.py) around
+Archives are written here (tests/sevenzwrite.py) around
 coder data from liblzma (LZMA1 with end marker, LZMA2) and from the
 reference encoder (LzmaEnc.c, no end marker): single and multi-folder
 archives, Copy / LZMA / LZMA2 / BCJ x86 + LZMA folders, folder and file
 CRCs, empty files and directories, LZMA- and LZMA2-encoded headers, and
 corrupt variants (signature, start header CRC, next header CRC, file CRC,
-coder data, trailing pack bytes, truncation, an unsupported coder).  For
+coder data, trailing pack bytes, truncation, an unsupported coder), and BCJ2
+folders (streams from tests/bcj2enc.py: LZMA / LZMA2 / Copy coders, every or
+no branch converted, encoded header) with their failure modes (short rc or
+CALL stream, flipped rc byte, archive cut in the rc stream, PARAM).  For
 every archive the reference's open result, per-file extract result and
 size, the extracted bytes (files that extract OK, in file order) and the
 raw UTF-16LE name buffer are recorded.
@@ -100,6 +103,23 @@ def archives():
         [W.Folder(files("a2", ad[:50000]), method=W.M_LZMA2, arm=True),
          W.Folder(files("b2", xd[:30000]), bcj=True)])))
 
+    # BCJ2 folders (7zDec.c:412-440): streams from tests/bcj2enc.py
+    import bcj2enc
+    x2 = bcj2enc.x86_like(740, 120000)
+    A.append(("BCJ2 (LZMA x3), 3 files, folder CRC", W.archive(
+        [W.Bcj2Folder(files("j", x2[:40000], x2[40000:100000], x2[100000:]), crc=True)])))
+    A.append(("BCJ2 (Copy JMP, Copy CALL, LZMA2 main), every branch converted", W.archive(
+        [W.Bcj2Folder(files("j2", x2[:70000]), methods=(W.M_COPY, W.M_COPY, W.M_LZMA2),
+                      convert=lambda p, o, rel: True)])))
+    A.append(("BCJ2 + LZMA + Copy folders, encoded header", W.archive(
+        [W.Folder(files("k1", text[:20000])),
+         W.Bcj2Folder(files("k2", x2[:50000], x2[50000:60000]), methods=(W.M_LZMA2, W.M_LZMA, W.M_LZMA)),
+         W.Folder(files("k3", rnd[:4000]), method=W.M_COPY, crc=True)], encode_header=True)))
+    A.append(("BCJ2 with no branch converted, 1 file", W.archive(
+        [W.Bcj2Folder(files("j3", x2[:30000]), convert=lambda p, o, rel: False)])))
+    A.append(("BCJ2 over text (no branch opcodes)", W.archive(
+        [W.Bcj2Folder(files("j4", text[:25000]))])))
+
     base = A[6][1]  # 5 folders
 
     def flip(b, at, mask=1):
@@ -147,6 +167,22 @@ def archives():
     C.append(("LZMA props byte >= 225", W.archive(
         [W.Folder(files("x", text[:800])), W.Folder(files("y", text[:900]), packed=packed,
                                                     props=props_bad)])))
+    # BCJ2 failures: the rc stream short (Bcj2_Decode's RC_TEST), a Copy CALL
+    # stream short (SzDecodeCopy size check), an rc bit flipped, the archive
+    # cut inside the rc stream, the main coder larger than the folder (PARAM)
+    C.append(("BCJ2: rc stream 3 bytes short", W.archive(
+        [W.Bcj2Folder(files("q1", x2[:50000]), cut=(1, 3))])))
+    C.append(("BCJ2: Copy CALL stream 4 bytes short", W.archive(
+        [W.Bcj2Folder(files("q2", x2[:50000]), methods=(W.M_COPY, W.M_COPY, W.M_LZMA),
+                      cut=(2, 4))])))
+    bf = W.Bcj2Folder(files("q3", x2[:50000]), crc=True)
+    arc = W.archive([W.Folder(files("q0", text[:3000])), bf])
+    rc_at = 32 + len(W.Folder(files("q0", text[:3000])).packed) + len(bf.pack_streams()[0])
+    C.append(("BCJ2: rc byte flipped (second folder)", flip(arc, rc_at + 40, 0x08)))
+    C.append(("BCJ2: archive cut inside the rc stream", arc[:rc_at + 10]))
+    bm = W.Bcj2Folder(files("q4", x2[:20000]))
+    bm.main_size_delta = len(bm.data)  # main stream coder larger than the folder output
+    C.append(("BCJ2: main coder unpack size > folder size", W.archive([bm])))
     return A, C
 
 

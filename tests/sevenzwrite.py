@@ -115,10 +115,69 @@ class Folder:
         n = len(self.data)
         return number(n) + (number(n) if self.bcj else b"")
 
+    def pack_streams(self):
+        return [self.packed]
+
+
+M_BCJ2 = 0x0303011B
+
+
+class Bcj2Folder:
+    """A BCJ2 folder in the only layout the 9.20 reader accepts
+    (CheckSupportedFolder, 7zDec.c:303-319): coders 0, 1, 2 = the JMP, CALL
+    and main streams (each Copy / LZMA / LZMA2), coder 3 = BCJ2 (4 in, 1 out);
+    pack streams in order: main (coder 2), the raw rc stream, CALL (coder 1),
+    JMP (coder 0).  The streams come from tests/bcj2enc.py.  `methods` gives
+    the (jump, call, main) coders; `cut` trims pack stream k by n bytes."""
+
+    def __init__(self, files, methods=(M_LZMA, M_LZMA, M_LZMA), crc=False, convert=None,
+                 cut=None, main_dict=1 << 16):
+        import bcj2enc
+        self.files, self.crc, self.bcj = files, crc, False
+        self.data = b"".join(d for _, d in files)
+        m, c, j, r = bcj2enc.encode(self.data, convert)
+        self.raw = (j, c, m)  # coder 0, 1, 2 outputs
+        self.rc = r
+        self.methods = methods
+        self.enc = []
+        for k, (meth, raw) in enumerate(zip(methods, self.raw)):
+            if meth == M_COPY:
+                self.enc.append((raw, b""))
+            else:
+                self.enc.append(encode(meth, raw, dict_size=main_dict if k == 2 else 1 << 16,
+                                       **({"lc": 0, "lp": 2} if k < 2 and meth == M_LZMA else {})))
+        streams = [self.enc[2][0], self.rc, self.enc[1][0], self.enc[0][0]]
+        if cut:
+            k, n = cut
+            streams[k] = streams[k][:len(streams[k]) - n]
+        self._packs = streams
+        self.packed = b"".join(streams)
+
+    def coders(self):
+        bid = method_id(M_BCJ2)
+        out = number(4)
+        for meth, (_, props) in zip(self.methods, self.enc):
+            out += coder(meth, props)
+        out += bytes([len(bid) | 0x10]) + bid + number(4) + number(1)
+        for i, o in ((5, 0), (4, 1), (3, 2)):   # bind pairs: in <- out
+            out += number(i) + number(o)
+        out += b"".join(number(x) for x in (2, 6, 1, 0))  # pack stream -> in index
+        return out
+
+    def unpack_sizes(self):
+        sizes = [len(x) for x in self.raw] + [len(self.data)]
+        if getattr(self, "main_size_delta", 0):
+            sizes[2] += self.main_size_delta
+        return b"".join(number(x) for x in sizes)
+
+    def pack_streams(self):
+        return self._packs
+
 
 def streams_info(folders, pack_pos, substreams=True):
-    out = bytes([PACK_INFO]) + number(pack_pos) + number(len(folders)) + bytes([SIZE])
-    out += b"".join(number(len(f.packed)) for f in folders) + bytes([END])
+    packs = [p for f in folders for p in f.pack_streams()]
+    out = bytes([PACK_INFO]) + number(pack_pos) + number(len(packs)) + bytes([SIZE])
+    out += b"".join(number(len(p)) for p in packs) + bytes([END])
     out += bytes([UNPACK_INFO, FOLDER]) + number(len(folders)) + b"\0"
     out += b"".join(f.coders() for f in folders)
     out += bytes([CODERS_UNPACK_SIZE]) + b"".join(f.unpack_sizes() for f in folders)

@@ -197,3 +197,39 @@ def test_gpu_7z_many_folders_round_trip(L):
     failed = {i for i, x in enumerate(fres[:len(plain)]) if x != 0}
     assert failed == {i for i, f in enumerate(files) if f.folder == 700}
     assert all(fres[i] in (1, 3) for i in failed)
+
+
+@pytest.mark.gpu
+def test_gpu_7z_bcj2_folders_round_trip(L):
+    """128 BCJ2 folders (three coders each in one decode batch, then one
+    Bcj2Gpu_Batch launch) beside 64 LZMA folders; a flipped rc byte in one BCJ2
+    folder fails exactly its files."""
+    import bcj2enc
+    import sevenzwrite as W
+    folders, plain = [], []
+    meths = [(W.M_LZMA, W.M_LZMA, W.M_LZMA), (W.M_COPY, W.M_COPY, W.M_LZMA2),
+             (W.M_LZMA2, W.M_LZMA, W.M_COPY)]
+    for i in range(192):
+        if i % 3 == 2:
+            fs = [(f"t{i}/a", native.gen("text", 9500 + i, 3000 + 17 * i))]
+            folders.append(W.Folder(fs))
+        else:
+            data = bcj2enc.x86_like(8000 + i, 2000 + (i * 977) % 30000)
+            cut = len(data) // 3
+            fs = [(f"x{i}/a", data[:cut]), (f"x{i}/b", data[cut:])]
+            folders.append(W.Bcj2Folder(fs, methods=meths[i % 3], crc=(i % 4 == 0)))
+        plain += [b for _, b in fs]
+    arc = W.archive(folders, encode_header=True)
+    r, fo, files, _, total = L.sz_open(arc)
+    assert r == 0 and len(fo) == 192 and all(f.supported == 0 for f in fo)
+    r, out, fres = L.SzExtract(arc, total)
+    assert r == 0 and all(x == 0 for x in fres[:len(plain)]), (r, set(fres[:len(plain)]))
+    assert [out[f.dst_off:f.dst_off + f.size] for f in files] == plain
+    # folder 100 is BCJ2 (100 % 3 == 1): flip a byte of its rc stream (pack stream 1)
+    f100 = folders[100]
+    start = 32 + sum(len(f.packed) for f in folders[:100]) + len(f100.pack_streams()[0])
+    bad = bytearray(arc)
+    bad[start + len(f100.pack_streams()[1]) // 2] ^= 0x10
+    r, out, fres = L.SzExtract(bytes(bad), total)
+    failed = {i for i, x in enumerate(fres[:len(plain)]) if x != 0}
+    assert failed <= {i for i, f in enumerate(files) if f.folder == 100}
