@@ -162,4 +162,76 @@ __device__ inline uint64_t bcj_x86(bcj_byte* data, uint64_t size, uint32_t ip, u
   return pos;
 }
 
+// ------------------------------------------------------------------ tiled form
+//
+// x86_Convert reads a byte only at or after the position it scans next, and
+// writes a converted operand (positions h+1..h+4) only behind that position
+// (the scan resumes at h+5): every byte it reads is still the original.  So
+// the E8/E9 positions of a range and their four operand bytes can be found
+// for a whole tile at once by every lane of a workgroup (lzgpu_bcj_x86_tile
+// _kernel), and the reference's decisions then run hit by hit over that list
+// -- bcj_hit below, one lane, with the state of x86_Convert's loop carried:
+// the position the scan resumes at, the last hit and prevMask.  Hits the list
+// holds before the resume position (inside a converted operand, or bytes an
+// earlier tile's conversion rewrote) are skipped, as the byte scan skips them.
+struct BcjRun {
+  uint64_t resume;    // bufferPos at the top of the reference's loop
+  uint64_t prev_pos;  // prevPosT (~0 before the first hit)
+  uint32_t mask;      // prevMask
+};
+
+// One E8/E9 at h (< size - 4) with operand bytes op = h+1 .. h+4 (byte h+1 in
+// bits 0-7): the reference's loop body (Bra86.c:33-84).  Returns true and the
+// new operand in *out when the hit converts.
+__device__ __forceinline__ bool bcj_hit(BcjRun& r, uint64_t h, uint32_t op, uint32_t ip,
+                                        int encoding, uint32_t* out) {
+  constexpr uint32_t kAllowed = 0x17u;  // kMaskToAllowedStatus as bits
+  auto bitnum = [](uint32_t m) -> uint32_t {
+    return m == 0 ? 0u : (m == 1 ? 1u : (m < 4 ? 2u : 3u));
+  };
+  const uint64_t gap = h - r.prev_pos;
+  if (gap > 3) {
+    r.mask = 0;
+  } else {
+    r.mask = (r.mask << (uint32_t(gap) - 1)) & 7u;
+    if (r.mask != 0) {
+      const uint32_t b = (op >> (8 * (3 - bitnum(r.mask)))) & 0xFFu;  // p[4 - bitnum]
+      if (!((kAllowed >> r.mask) & 1u) || bcj_test_ms(b)) {
+        r.prev_pos = h;
+        r.mask = ((r.mask << 1) & 7u) | 1u;
+        r.resume = h + 1;
+        return false;
+      }
+    }
+  }
+  r.prev_pos = h;
+  const uint32_t b4 = op >> 24;
+  if (!bcj_test_ms(b4)) {
+    r.mask = ((r.mask << 1) & 7u) | 1u;
+    r.resume = h + 1;
+    return false;
+  }
+  uint32_t src = op, dest;
+  const uint32_t at = ip + uint32_t(h);  // ip already + 5
+  for (;;) {
+    dest = encoding ? at + src : src - at;
+    if (r.mask == 0) break;
+    const uint32_t index = bitnum(r.mask) * 8;
+    const uint32_t b = (dest >> (24 - index)) & 0xFFu;
+    if (!bcj_test_ms(b)) break;
+    src = dest ^ ((1u << (32 - index)) - 1u);
+  }
+  *out = (dest & 0x00FFFFFFu) | ((~(((dest >> 24) & 1u) - 1u)) << 24);
+  r.resume = h + 5;
+  return true;
+}
+
+// The loop's end (Bra86.c:85-89): bytes processed and the state carried out.
+__device__ __forceinline__ uint64_t bcj_finish(const BcjRun& r, uint64_t limit, uint32_t* state) {
+  const uint64_t pos = r.resume > limit ? r.resume : limit;
+  const uint64_t gap = pos - r.prev_pos;
+  *state = (gap > 3) ? 0u : ((r.mask << (uint32_t(gap) - 1)) & 7u);
+  return pos;
+}
+
 }  // namespace lzgpu

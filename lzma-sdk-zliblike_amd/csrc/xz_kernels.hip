@@ -83,12 +83,113 @@ extern "C" int lzgpu_launch_crc64_arrays(const uint8_t* d_data, const uint64_t* 
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+// x86 BCJ, tiled (bcj_device.h, "tiled form"): one workgroup per range walks
+// it in 4 KiB tiles.  Every lane takes 16 bytes of the tile into LDS (plus the
+// four bytes behind the tile), finds its E8/E9 positions below size - 4, and
+// an LDS scan of the per-lane counts places their (position, operand) records
+// in tile order; lane 0 then runs the reference's decisions over the records
+// and writes the converted operands.  For text (no E8/E9) a tile costs its
+// loads and three barriers; branch-dense code is serial only per hit, not per
+// byte.
+constexpr uint32_t kBcjTile = 4096;
+
+__global__ void __launch_bounds__(256) lzgpu_bcj_x86_tile_kernel(
+    uint8_t* __restrict__ data, const uint64_t* __restrict__ off, const uint64_t* __restrict__ len,
+    const uint32_t* __restrict__ ip, uint32_t* __restrict__ state, uint64_t* __restrict__ done,
+    uint32_t n, int encoding) {
+  __shared__ __attribute__((aligned(16))) uint8_t tile[kBcjTile + 16];
+  __shared__ uint16_t rec_pos[kBcjTile];
+  __shared__ uint32_t rec_op[kBcjTile];
+  __shared__ uint32_t scan[256];
+  typedef __attribute__((address_space(1))) uint8_t gb;
+  typedef uint64_t u64a1 __attribute__((aligned(1)));
+  typedef uint32_t u32a1 __attribute__((aligned(1)));
+  const uint32_t t = threadIdx.x;
+  for (uint32_t r = blockIdx.x; r < n; r += gridDim.x) {
+    const uint64_t size = len[r];
+    gb* p = (gb*)(data + off[r]);
+    if (size < 5) {  // x86_Convert returns 0, state untouched
+      if (t == 0) done[r] = 0;
+      continue;
+    }
+    const uint64_t limit = size - 4;
+    BcjRun run;  // lane 0's
+    run.resume = 0;
+    run.prev_pos = ~uint64_t(0);
+    run.mask = state[r] & 7u;
+    const uint32_t ip5 = ip[r] + 5;
+    for (uint64_t tb = 0; tb < limit; tb += kBcjTile) {
+      // the tile's bytes [tb, tb + 4096 + 4) that lie in the range
+      const uint64_t a = tb + 16 * uint64_t(t);
+      if (a + 16 <= size) {
+        const uint64_t lo = *(const __attribute__((address_space(1))) u64a1*)(p + a);
+        const uint64_t hi = *(const __attribute__((address_space(1))) u64a1*)(p + a + 8);
+        *(uint64_t*)(tile + 16 * t) = lo;
+        *(uint64_t*)(tile + 16 * t + 8) = hi;
+      } else {
+        for (uint32_t k = 0; k < 16; ++k) tile[16 * t + k] = a + k < size ? p[a + k] : 0;
+      }
+      if (t < 4) {
+        const uint64_t q = tb + kBcjTile + t;
+        tile[kBcjTile + t] = q < size ? p[q] : 0;
+      }
+      __syncthreads();
+      // this lane's hits: E8 / E9 at positions below limit
+      uint32_t hits = 0;  // bit k: byte 16 t + k is a hit
+      for (uint32_t k = 0; k < 16; ++k)
+        if ((tile[16 * t + k] & 0xFEu) == 0xE8u && a + k < limit) hits |= 1u << k;
+      const uint32_t cnt = uint32_t(__builtin_popcount(hits));
+      scan[t] = cnt;
+      __syncthreads();
+      for (uint32_t o = 1; o < 256; o <<= 1) {  // inclusive scan of the counts
+        const uint32_t v = t >= o ? scan[t - o] : 0u;
+        __syncthreads();
+        scan[t] += v;
+        __syncthreads();
+      }
+      uint32_t w = scan[t] - cnt;
+      while (hits) {
+        const uint32_t k = uint32_t(__builtin_ctz(hits));
+        hits &= hits - 1;
+        const uint32_t j = 16 * t + k;
+        rec_pos[w] = uint16_t(j);
+        rec_op[w] = uint32_t(tile[j + 1]) | (uint32_t(tile[j + 2]) << 8) |
+                    (uint32_t(tile[j + 3]) << 16) | (uint32_t(tile[j + 4]) << 24);
+        ++w;
+      }
+      const uint32_t total = scan[255];
+      __syncthreads();
+      if (t == 0) {
+        for (uint32_t i = 0; i < total; ++i) {
+          const uint64_t h = tb + rec_pos[i];
+          if (h < run.resume) continue;
+          uint32_t v;
+          if (bcj_hit(run, h, rec_op[i], ip5, encoding, &v))
+            *(__attribute__((address_space(1))) u32a1*)(p + h + 1) = v;
+        }
+      }
+      __syncthreads();  // the conversions are visible to the next tile's loads
+    }
+    if (t == 0) {
+      uint32_t st;
+      done[r] = bcj_finish(run, limit, &st);
+      state[r] = st;
+    }
+  }
+}
+
 extern "C" int lzgpu_launch_bcj_x86(uint8_t* d_data, const uint64_t* d_off, const uint64_t* d_len,
                                     const uint32_t* d_ip, uint32_t* d_state, uint64_t* d_done,
                                     uint32_t n, int encoding, hipStream_t stream) {
   if (n == 0) return 0;
-  hipLaunchKernelGGL(lzgpu_bcj_x86_kernel, dim3((n + 63) / 64), dim3(64), 0, stream, d_data, d_off,
-                     d_len, d_ip, d_state, d_done, n, encoding);
+  if (getenv("LZGPU_BCJ_SERIAL")) {  // the lane-serial statement (A/B)
+    hipLaunchKernelGGL(lzgpu_bcj_x86_kernel, dim3((n + 63) / 64), dim3(64), 0, stream, d_data,
+                       d_off, d_len, d_ip, d_state, d_done, n, encoding);
+  } else {
+    const uint32_t grid = n < 65536 ? n : 65536;
+    hipLaunchKernelGGL(lzgpu_bcj_x86_tile_kernel, dim3(grid), dim3(256), 0, stream, d_data, d_off,
+                       d_len, d_ip, d_state, d_done, n, encoding);
+  }
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 

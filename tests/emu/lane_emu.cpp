@@ -168,6 +168,40 @@ uint64_t emu_bcj_x86(uint8_t* data, uint64_t size, uint32_t ip, uint32_t* state,
   return bcj_x86(data, size, ip, state, encoding);
 }
 
+// lzgpu_bcj_x86_tile_kernel on one range, its phases run in order on the host:
+// per 4 KiB tile, the records of every E8/E9 below size - 4 (position and the
+// four bytes behind it, read after the previous tile's conversions), then the
+// reference's decisions over them (bcj_hit) writing the conversions.
+uint64_t emu_bcj_x86_tiled(uint8_t* data, uint64_t size, uint32_t ip, uint32_t* state,
+                           int encoding) {
+  if (size < 5) return 0;
+  const uint64_t limit = size - 4;
+  BcjRun run;
+  run.resume = 0;
+  run.prev_pos = ~uint64_t(0);
+  run.mask = *state & 7u;
+  std::vector<uint64_t> pos;
+  std::vector<uint32_t> op;
+  for (uint64_t tb = 0; tb < limit; tb += 4096) {
+    uint8_t tile[4096 + 4];
+    for (uint64_t k = 0; k < 4096 + 4; ++k) tile[k] = tb + k < size ? data[tb + k] : 0;
+    pos.clear();
+    op.clear();
+    for (uint64_t k = 0; k < 4096 && tb + k < limit; ++k)
+      if ((tile[k] & 0xFEu) == 0xE8u) {
+        pos.push_back(tb + k);
+        op.push_back(uint32_t(tile[k + 1]) | (uint32_t(tile[k + 2]) << 8) |
+                     (uint32_t(tile[k + 3]) << 16) | (uint32_t(tile[k + 4]) << 24));
+      }
+    for (size_t i = 0; i < pos.size(); ++i) {
+      if (pos[i] < run.resume) continue;
+      uint32_t v;
+      if (bcj_hit(run, pos[i], op[i], ip + 5, encoding, &v)) memcpy(data + pos[i] + 1, &v, 4);
+    }
+  }
+  return bcj_finish(run, limit, state);
+}
+
 // lzgpu_bcj2_kernel's lane (bcj2_decode) on host buffers; probabilities in a
 // lane-private array as the kernel's LDS slice.
 int emu_bcj2(const uint8_t* b0, uint64_t s0, const uint8_t* b1, uint64_t s1, const uint8_t* b2,

@@ -53,6 +53,9 @@ def L():
 def emu():
     subprocess.run(["make", "-s", "-f", "tests/emu/Makefile"], cwd=native.ROOT, check=True)
     lib = ctypes.CDLL(EMU_SO)
+    lib.emu_bcj_x86_tiled.restype = ctypes.c_uint64
+    lib.emu_bcj_x86_tiled.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_uint32,
+                                      ctypes.POINTER(ctypes.c_uint32), ctypes.c_int]
     lib.emu_bcj_x86.restype = ctypes.c_uint64
     lib.emu_bcj_x86.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_uint32,
                                 ctypes.POINTER(ctypes.c_uint32), ctypes.c_int]
@@ -119,6 +122,44 @@ def test_bcj_emu_matches_reference(emu):
         done = emu.emu_bcj_x86(buf, n, c["ip"], ctypes.byref(st), c["encoding"])
         assert (done, st.value) == (c["done"], c["state_out"]), c
         assert hashlib.sha256(buf.raw[:n]).hexdigest() == c["sha256"], c
+
+
+def test_bcj_tiled_emu_matches_reference(emu):
+    """The tiled x86 BCJ kernel's phases (hit records per 4 KiB tile, then the
+    reference's decisions over them) on every reference fixture, and against
+    the lane-serial statement on branch-dense buffers spanning many tiles
+    (conversions across tile edges, E8/E9 runs, every start state)."""
+    d = fixtures()
+    for c in d["bcj"]:
+        n = c["len"]
+        buf = ctypes.create_string_buffer(d["blob"][c["off"]:c["off"] + n] + b"\0" * 32, n + 32)
+        st = ctypes.c_uint32(c["state_in"])
+        done = emu.emu_bcj_x86_tiled(buf, n, c["ip"], ctypes.byref(st), c["encoding"])
+        assert (done, st.value) == (c["done"], c["state_out"]), c
+        assert hashlib.sha256(buf.raw[:n]).hexdigest() == c["sha256"], c
+    import random
+    rng = random.Random(17)
+    for it in range(40):
+        n = rng.choice([5, 4099, 4100, 4101, 8192 + 3, 20000, 50001])
+        b = bytearray(rng.getrandbits(8) for _ in range(n))
+        dens = rng.choice([0.02, 0.1, 0.3, 0.6])
+        for i in range(n):
+            if rng.random() < dens:
+                b[i] = rng.choice([0xE8, 0xE9])
+                if i + 4 < n and rng.random() < 0.7:
+                    b[i + 4] = rng.choice([0x00, 0xFF])
+        # force hits right at the tile edges
+        for e in range(4096, n, 4096):
+            for k in (-4, -3, -2, -1, 0, 1):
+                if 0 <= e + k < n and rng.random() < 0.5:
+                    b[e + k] = 0xE8
+        ip, s0, enc = rng.getrandbits(32), rng.randrange(8), rng.randrange(2)
+        b1 = ctypes.create_string_buffer(bytes(b) + b"\0" * 32, n + 32)
+        b2 = ctypes.create_string_buffer(bytes(b) + b"\0" * 32, n + 32)
+        s1, s2 = ctypes.c_uint32(s0), ctypes.c_uint32(s0)
+        d1 = emu.emu_bcj_x86(b1, n, ip, ctypes.byref(s1), enc)
+        d2 = emu.emu_bcj_x86_tiled(b2, n, ip, ctypes.byref(s2), enc)
+        assert (d1, s1.value) == (d2, s2.value) and b1.raw == b2.raw, (it, n, dens)
 
 
 def test_crc64_emu_matches_reference(emu):
@@ -193,3 +234,50 @@ def test_gpu_xz_many_blocks_round_trip(L):
     bad_file[b.check_off] ^= 1
     r, out, badb = L.XzDecode(bytes(bad_file), total)
     assert (r, badb) == (3, 300)
+
+
+@pytest.mark.gpu
+def test_gpu_bcj_x86_tiled_large_batch(L, emu):
+    """BcjGpu_X86Batch (the tiled kernel: 4 KiB tiles, hit records, one lane's
+    decisions) over 256 ranges x 40 KiB of branch-dense bytes at odd offsets,
+    every start state, both directions -- against the lane-serial statement
+    (itself pinned to the reference fixtures)."""
+    import numpy as np
+    import torch
+    rng = np.random.default_rng(23)
+    n, size = 256, 40000
+    raw = rng.integers(0, 256, n * (size + 3) + 64, dtype=np.uint8)
+    offs = np.array([i * (size + 3) + (i % 7) for i in range(n)], np.uint64)
+    for i in range(n):
+        o = int(offs[i])
+        seg = raw[o:o + size]
+        pick = rng.random(size) < (0.02 if i % 3 else 0.25)
+        seg[pick] = rng.choice([0xE8, 0xE9], int(pick.sum()))
+        ms = np.nonzero(pick)[0] + 4
+        ms = ms[ms < size]
+        seg[ms[rng.random(len(ms)) < 0.7]] = 0
+    ips = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
+    st0 = (np.arange(n) % 8).astype(np.uint32)
+    for enc in (0, 1):
+        want = raw.copy()
+        wst, wdone = [], []
+        for i in range(n):
+            o = int(offs[i])
+            b = ctypes.create_string_buffer(want[o:o + size].tobytes() + b"\0" * 32, size + 32)
+            s = ctypes.c_uint32(int(st0[i]))
+            wdone.append(emu.emu_bcj_x86(b, size, int(ips[i]), ctypes.byref(s), enc))
+            wst.append(s.value)
+            want[o:o + size] = np.frombuffer(b.raw[:size], np.uint8)
+        data = torch.from_numpy(raw.copy()).cuda()
+        d_off = torch.from_numpy(offs.view(np.int64).copy()).cuda()
+        d_len = torch.full((n,), size, dtype=torch.int64, device="cuda")
+        d_ip = torch.from_numpy(ips.view(np.int32).copy()).cuda()
+        d_st = torch.from_numpy(st0.view(np.int32).copy()).cuda()
+        d_done = torch.zeros(n, dtype=torch.int64, device="cuda")
+        assert L.bcj_x86_batch_device(data.data_ptr(), d_off.data_ptr(), d_len.data_ptr(),
+                                      d_ip.data_ptr(), d_st.data_ptr(), d_done.data_ptr(), n,
+                                      enc) == 0
+        torch.cuda.synchronize()
+        assert d_done.cpu().tolist() == wdone
+        assert (d_st.cpu().numpy().astype(np.uint32) == np.array(wst, np.uint32)).all()
+        assert np.array_equal(data.cpu().numpy(), want)
