@@ -926,6 +926,32 @@ SRes LzmaGpu_PlanBatchOpt(LzmaGpuStreamDesc* descs, size_t n, uint32_t* order, L
   return plan_batch_nothrow(descs, n, order, plan, opt ? *opt : env_options());
 }
 
+// Internal streams for concurrent class launches, one set per host thread and
+// device (created on first use, kept for the process: like the scratch
+// buffers, they are per-call resources the caller never sees).
+struct ClassStreams {
+  hipStream_t s[LZMA_GPU_MAX_CLASSES];
+  hipEvent_t fork, join[LZMA_GPU_MAX_CLASSES];
+};
+static ClassStreams* class_streams() {
+  static thread_local ClassStreams* per_dev[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  if (!per_dev[dev]) {
+    ClassStreams* c = new ClassStreams();
+    bool ok = hipEventCreateWithFlags(&c->fork, hipEventDisableTiming) == hipSuccess;
+    for (int k = 0; k < LZMA_GPU_MAX_CLASSES && ok; ++k)
+      ok = hipStreamCreateWithFlags(&c->s[k], hipStreamNonBlocking) == hipSuccess &&
+           hipEventCreateWithFlags(&c->join[k], hipEventDisableTiming) == hipSuccess;
+    if (!ok) {
+      set_error("class streams: creation failed");
+      return nullptr;  // (a failed set is not cached: the next call retries)
+    }
+    per_dev[dev] = c;
+  }
+  return per_dev[dev];
+}
+
 SRes LzmaGpu_DecodeBatchEx(const LzmaGpuPlan* plan, const LzmaGpuStreamDesc* d_descs,
                            const uint32_t* d_order, const Byte* d_src, Byte* d_dst,
                            void* d_workspace, LzmaGpuResult* d_results, void* stream) {
@@ -935,29 +961,42 @@ SRes LzmaGpu_DecodeBatchEx(const LzmaGpuPlan* plan, const LzmaGpuStreamDesc* d_d
     return SZ_ERROR_PARAM;
   hipStream_t st = static_cast<hipStream_t>(stream);
   uint16_t* ws = static_cast<uint16_t*>(d_workspace);
-  static int cus = 0;
-  if (cus == 0) {
-    int dev = 0, v = 0;
-    (void)hipGetDevice(&dev);
-    cus = (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess)
-              ? v
-              : 256;
-  }
+  const uint32_t cus = device_cus();
+  // Several width classes (mixed lc/lp/pb batches, config 5): each class is a
+  // persistent launch whose workgroups leave only when its queue is drained,
+  // so on one stream every class ends in a tail of a few long streams while
+  // the rest of the chip idles.  On their own streams (forked from and joined
+  // back into the caller's) the next class's workgroups fill the CUs the
+  // previous one frees.  LZGPU_CLASS_STREAMS=0: one stream (A/B).
+  uint32_t live = 0;
+  for (uint32_t k = 0; k < plan->n_classes; ++k) live += plan->classes[k].n ? 1u : 0u;
+  const bool fork = live > 1 && env_int("LZGPU_CLASS_STREAMS", 1) != 0;
+  ClassStreams* cs = fork ? class_streams() : nullptr;
+  if (fork && !cs) return SZ_ERROR_FAIL;
+  if (cs && !hip_ok(hipEventRecord(cs->fork, st), "class fork")) return SZ_ERROR_FAIL;
   uint64_t first = 0;
   for (uint32_t k = 0; k < plan->n_classes; ++k) {
     const LzmaGpuLdsClass& c = plan->classes[k];
     if (c.n == 0) continue;
     if (first + c.n > plan->n_lds) return SZ_ERROR_PARAM;
-    const uint32_t max_groups = plan->persistent ? uint32_t(cus) * c.groups_per_cu : 0u;
+    const uint32_t max_groups = plan->persistent ? cus * c.groups_per_cu : 0u;
     uint32_t* queue = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(d_workspace) +
                                                   plan->queue_offset + 64 * k);
+    hipStream_t sk = st;
+    if (cs) {
+      sk = cs->s[k];
+      if (!hip_ok(hipStreamWaitEvent(sk, cs->fork, 0), "class fork")) return SZ_ERROR_FAIL;
+    }
     if (lzgpu_launch_decode_lds(d_descs, d_order + first, uint32_t(c.n), d_src, d_dst, ws,
                                 d_results, c.lanes_per_group, c.lds_cells_per_lane,
                                 c.waves_per_simd, c.groups_per_cu, max_groups, queue, c.lds_mask,
-                                c.flags, st) != 0) {
+                                c.flags, sk) != 0) {
       set_error("LDS decode kernel launch failed");
       return SZ_ERROR_FAIL;
     }
+    if (cs && (!hip_ok(hipEventRecord(cs->join[k], sk), "class join") ||
+               !hip_ok(hipStreamWaitEvent(st, cs->join[k], 0), "class join")))
+      return SZ_ERROR_FAIL;
     first += c.n;
   }
   const uint32_t n_lds = uint32_t(plan->n_lds), n_glob = uint32_t(plan->n - plan->n_lds);

@@ -1040,9 +1040,11 @@ static SRes sz_open(const Byte* archive, size_t size, LzmaGpu7zFolder* folders, 
     o.first_file = x.folder_start_file[i];
     o.num_files = f.num_unpack_streams;
     o.num_coders = uint32_t(f.coders.size());
-    const std::vector<Byte>& p = f.coders.empty() ? std::vector<Byte>() : f.coders[0].props;
-    o.props_size = uint32_t(p.size());
-    memcpy(o.props, p.data(), std::min<size_t>(p.size(), sizeof o.props));
+    if (!f.coders.empty()) {
+      const std::vector<Byte>& p = f.coders[0].props;
+      o.props_size = uint32_t(p.size());
+      if (!p.empty()) memcpy(o.props, p.data(), std::min<size_t>(p.size(), sizeof o.props));
+    }
   }
   for (size_t i = 0; i < x.files.size() && files && i < file_cap; ++i) {
     const FileItem& f = x.files[i];
