@@ -690,11 +690,31 @@ def cfg4_cpu_baseline(parts, threads):
             "errors": int(len(oks) - sum(oks))}
 
 
-def cpu_baseline(comp, lens, offs, n, props, threads, sample_streams):
-    """The oracle restatement (CPU port of LzmaDec) on a bounded sample."""
+def cpu_baseline(comp, lens, offs, n, props, threads, sample_streams, impl="port"):
+    """A CPU LzmaDecode over a bounded sample: impl "reference" = the reference's
+    own LzmaDec.c (oracle/_ref/libref.so, compiled in place with gcc -O2),
+    "port" = the oracle restatement (oracle/liboracle.so)."""
     import native
-    orc = native.oracle()
     m = min(sample_streams, len(lens))
+    if impl == "reference":
+        ref = native.ref()
+        src_off = np.ascontiguousarray(offs[:m], dtype=np.uint64)
+        src_len = np.ascontiguousarray(lens[:m], dtype=np.uint64)
+        dst_off = np.arange(m, dtype=np.uint64) * n
+        dst_cap = np.full(m, n, dtype=np.uint64)
+        p5 = np.tile(np.frombuffer(props, dtype=np.uint8), m)
+        dst = np.zeros(m * n, dtype=np.uint8)
+        res = np.zeros(m, dtype=np.int32)
+        dl = np.zeros(m, dtype=np.uint64)
+        t0 = time.perf_counter()
+        errs = ref.ref_lzma_decode_batch(comp.ctypes.data, src_off.ctypes.data, src_len.ctypes.data,
+                                         p5.ctypes.data, dst.ctypes.data, dst_off.ctypes.data,
+                                         dst_cap.ctypes.data, 1, res.ctypes.data, dl.ctypes.data,
+                                         m, threads)
+        dt = time.perf_counter() - t0
+        errs += int((dl != n).sum())
+        return m * n / dt / 1e6, dt, m, errs
+    orc = native.oracle()
     src_off = np.ascontiguousarray(offs[:m], dtype=np.uint64)
     src_len = np.ascontiguousarray(lens[:m], dtype=np.uint64)
     dst_off = np.arange(m, dtype=np.uint64) * n
@@ -1219,16 +1239,24 @@ def main():
 
     cpu_base = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        import native
         thr = cpu["usable"]
-        v, dt, m, errs = cpu_baseline(comp, lens, offs, n, props, thr, sample_streams=count)
-        v1, dt1, m1, _ = cpu_baseline(comp, lens, offs, n, props, 1,
-                                      sample_streams=max(64, count // 32))
-        cpu_base = {"value": round(v, 2), "unit": "MB/s", "cores": thr, "kind": "port",
-                    "impl": "oracle/lzma_oracle.c: this build's C restatement of LzmaDec.c "
-                            "(pinned to the reference's outputs), not the reference binary",
+        kind = "reference" if native.have_ref() else "port"
+        v, dt, m, errs = cpu_baseline(comp, lens, offs, n, props, thr, count, kind)
+        v1, dt1, m1, _ = cpu_baseline(comp, lens, offs, n, props, 1, max(64, count // 32), kind)
+        impl = ("oracle/_ref/libref.so: the reference's own LzmaDec.c (LzmaDecode, "
+                "LzmaDec.c:972) compiled in place with gcc -O2 by oracle/Makefile.ref"
+                if kind == "reference" else
+                "oracle/lzma_oracle.c: this build's C restatement of LzmaDec.c "
+                "(pinned to the reference's outputs), not the reference binary")
+        cpu_base = {"value": round(v, 2), "unit": "MB/s", "cores": thr, "kind": kind,
+                    "impl": impl,
                     "sample": f"{m} streams ({m * n} B decompressed) of the same batch, "
                               f"{thr} threads, {dt:.2f}s; 1-core: {v1:.2f} MB/s over {m1} streams",
                     "one_core_MBps": round(v1, 2), "cpu": cpu, "errors": int(errs)}
+        if kind == "reference":
+            vp, dtp, mp_, _ = cpu_baseline(comp, lens, offs, n, props, thr, count, "port")
+            cpu_base["port_MBps"] = round(vp, 2)
 
     traffic = None
     tpath = os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")

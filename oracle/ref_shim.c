@@ -3,10 +3,12 @@
  *
  * Thin ctypes-friendly wrapper around the *reference* LZMA SDK 9.20 sources,
  * compiled in place from /root/reference by oracle/Makefile.ref into
- * oracle/_ref/libref.so (never copied into this repository).  Used only by
- * tests/golden/make_golden.py to (a) encode fixture streams with the
+ * oracle/_ref/libref.so (never copied into this repository).  Used by
+ * tests/golden/make_golden*.py to (a) encode fixture streams with the
  * reference encoder and (b) record the reference decoder's exact
- * {res, status, destLen, srcLen} and output for every golden case.
+ * {res, status, destLen, srcLen} and output for every golden case, and by
+ * bench.py's cpu_baseline leg (ref_lzma_decode_batch: the reference's own
+ * LzmaDecode over a batch on host threads, "kind": "reference").
  *
  * Nothing in the product (lzma-sdk-zliblike_amd/) links or loads this.
  *
@@ -23,6 +25,8 @@
  * pointing fd 1 at /dev/null around each decoder call.
  */
 #include <fcntl.h>
+#include <pthread.h>
+#include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -368,4 +372,89 @@ int ref_7z_extract(const unsigned char *arc, size_t size, unsigned char *out, si
   quiet_end(saved);
   *out_len = pos;
   return res;
+}
+
+/*
+ * CPU baseline: the reference LzmaDecode (LzmaDec.c:972) over n streams on
+ * `threads` host threads, 16 streams per work grab.  Streams i: src + src_off[i]
+ * (src_len[i] bytes), props5 + 5 i, output dst + dst_off[i] (dst_cap[i] bytes).
+ * The fork prints a line from LzmaDec_AllocateProbs (LzmaDec.c:945) on every
+ * call: fd 1 points at /dev/null for the whole batch (the printf cost stays in
+ * the timing -- it is the reference's own).  Returns the number of streams
+ * whose result was not SZ_OK; res_out / dest_len_out may be NULL.
+ */
+typedef struct {
+  const unsigned char *src, *props5;
+  const uint64_t *src_off, *src_len, *dst_off, *dst_cap;
+  unsigned char *dst;
+  int fin;
+  int32_t *res_out;
+  uint64_t *dest_len_out;
+  size_t n, next;
+  pthread_mutex_t mu;
+  int errors;
+} ref_batch;
+
+static void *ref_batch_worker(void *arg) {
+  ref_batch *b = (ref_batch *)arg;
+  int errs = 0;
+  for (;;) {
+    size_t i, end, k;
+    pthread_mutex_lock(&b->mu);
+    i = b->next;
+    end = i + 16 < b->n ? i + 16 : b->n;
+    b->next = end;
+    pthread_mutex_unlock(&b->mu);
+    if (i >= b->n) break;
+    for (k = i; k < end; k++) {
+      SizeT dl = (SizeT)b->dst_cap[k], sl = (SizeT)b->src_len[k];
+      ELzmaStatus st;
+      SRes r = LzmaDecode(b->dst + b->dst_off[k], &dl, b->src + b->src_off[k], &sl,
+                          b->props5 + 5 * k, LZMA_PROPS_SIZE, (ELzmaFinishMode)b->fin, &st,
+                          &g_shim_alloc);
+      if (b->res_out) b->res_out[k] = r;
+      if (b->dest_len_out) b->dest_len_out[k] = dl;
+      if (r != SZ_OK) errs++;
+    }
+  }
+  pthread_mutex_lock(&b->mu);
+  b->errors += errs;
+  pthread_mutex_unlock(&b->mu);
+  return NULL;
+}
+
+int ref_lzma_decode_batch(const unsigned char *src, const uint64_t *src_off,
+                          const uint64_t *src_len, const unsigned char *props5,
+                          unsigned char *dst, const uint64_t *dst_off, const uint64_t *dst_cap,
+                          int finish_mode, int32_t *res_out, uint64_t *dest_len_out, size_t n,
+                          int threads) {
+  ref_batch b;
+  pthread_t tid[256];
+  int t, saved;
+  if (threads < 1) threads = 1;
+  if (threads > 256) threads = 256;
+  b.src = src;
+  b.src_off = src_off;
+  b.src_len = src_len;
+  b.props5 = props5;
+  b.dst = dst;
+  b.dst_off = dst_off;
+  b.dst_cap = dst_cap;
+  b.fin = finish_mode;
+  b.res_out = res_out;
+  b.dest_len_out = dest_len_out;
+  b.n = n;
+  b.next = 0;
+  b.errors = 0;
+  pthread_mutex_init(&b.mu, NULL);
+  saved = quiet_begin();
+  if (threads == 1) {
+    ref_batch_worker(&b);
+  } else {
+    for (t = 0; t < threads; t++) pthread_create(&tid[t], NULL, ref_batch_worker, &b);
+    for (t = 0; t < threads; t++) pthread_join(tid[t], NULL);
+  }
+  quiet_end(saved);
+  pthread_mutex_destroy(&b.mu);
+  return b.errors;
 }

@@ -70,8 +70,18 @@ def ref():
         f.argtypes = [ctypes.c_char_p, size_t_p, ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int,
                       ctypes.c_uint, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_size_t,
                       ctypes.POINTER(ctypes.c_ubyte)]
+        f = lib.ref_lzma_decode_batch
+        f.restype = ctypes.c_int
+        f.argtypes = [ctypes.c_void_p] * 7 + [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                              ctypes.c_size_t, ctypes.c_int]
         lib._declared = True
     return lib
+
+
+def have_ref():
+    """True when the reference library (oracle/_ref, built from /root/reference
+    in the build container) is present -- it travels to the GPU box with the tree."""
+    return os.path.exists(REF_SO)
 
 
 def crc_funcs(lib, update, calc):
