@@ -264,8 +264,9 @@ SRes LzmaGpu_PlanBatchEx(LzmaGpuStreamDesc *descs, size_t n, uint32_t *order, Lz
  *               per wave -- the config-3 kernel, whatever the batch size;
  *   LATENCY     placement 0x1BF, one stream per wave (lanes_per_group may
  *               widen it);
- *   COOP        placement 0x1BF, one stream per 32-lane wave, literal trees
- *               decided cooperatively (wave-speculation kernel);
+ *   COOP        one stream per 32-lane wave, literal trees decided
+ *               cooperatively (wave-speculation kernel); placement 0x7FF (all
+ *               sections in LDS) where the whole table fits, else 0x1BF;
  *   GLOBAL      every stream on the generic kernel (tables in global memory).
  * A class whose latency-placement table exceeds the LDS limit keeps the
  * throughput placement.  cus: CUs to size the plan for (0 = the device's). */
@@ -291,6 +292,11 @@ typedef struct LzmaGpuPlanOptions {
 #define LZMA_GPU_PLAN_SLICE_ALIGN8 1u
 /* every class on the kernel build with the LZMA2 chunk walker (A/B only) */
 #define LZMA_GPU_PLAN_KERNEL_LZMA2 2u
+/* cooperative classes keep the latency placement 0x1BF (SpecPos, matched-
+ * literal trees and LenHigh in global memory).  Default: every section in LDS
+ * (placement 0x7FF) when the whole table fits the class's streams per CU --
+ * config 4 2.85 -> 3.00 GB/s, the xz leg 2.52 -> 2.63 (profiles/r02_ab/). */
+#define LZMA_GPU_PLAN_COOP_LAT 4u
 
 /* LzmaGpu_PlanBatchEx with explicit options (opt == NULL: as PlanBatchEx,
  * whose defaults take the LZGPU_* experiment variables of the environment,

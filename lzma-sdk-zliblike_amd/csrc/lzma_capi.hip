@@ -703,7 +703,8 @@ static uint32_t device_cus() {
 // Planner defaults with the experiment overrides of the environment, read at
 // call time (LZGPU_KERNEL=global|throughput|latency|coop, LZGPU_MASK=1|2,
 // LZGPU_COOP=0|1, LZGPU_CUS, LZGPU_LANES, LZGPU_GROUPS, LZGPU_OCC,
-// LZGPU_PERSIST=0, LZGPU_CLASSES=1).  Only LzmaGpu_PlanBatchEx reads them;
+// LZGPU_PERSIST=0, LZGPU_CLASSES=1, LZGPU_SLICE_ALIGN8=1, LZGPU_KERNEL_LZMA2=1,
+// LZGPU_COOP_LAT=1).  Only LzmaGpu_PlanBatchEx reads them;
 // LzmaGpu_PlanBatchOpt takes its options from the caller alone.
 static LzmaGpuPlanOptions env_options() {
   LzmaGpuPlanOptions o;
@@ -730,7 +731,8 @@ static LzmaGpuPlanOptions env_options() {
   o.persistent = env_int("LZGPU_PERSIST", 1) ? 0u : 2u;
   o.one_class = env_int("LZGPU_CLASSES", 0) == 1 ? 1u : 0u;
   o.flags = (env_int("LZGPU_SLICE_ALIGN8", 0) ? LZMA_GPU_PLAN_SLICE_ALIGN8 : 0u) |
-            (env_int("LZGPU_KERNEL_LZMA2", 0) ? LZMA_GPU_PLAN_KERNEL_LZMA2 : 0u);
+            (env_int("LZGPU_KERNEL_LZMA2", 0) ? LZMA_GPU_PLAN_KERNEL_LZMA2 : 0u) |
+            (env_int("LZGPU_COOP_LAT", 0) ? LZMA_GPU_PLAN_COOP_LAT : 0u);
   return o;
 }
 
@@ -815,6 +817,14 @@ static int lds_bucket(uint32_t cells) {
   return 3;
 }
 
+// cells of an item's whole table (every section in LDS); 0 = bad props
+static uint32_t all_cells(const LzmaGpuStreamDesc& d) {
+  if (d.kind == LZMA_GPU_KIND_LZMA2) return d.props[0] <= 40 ? lzgpu::table_cells(4, 0, 4) : 0u;
+  uint32_t lc, lp, pb, dict;
+  if (lzgpu::lz_props_parse(d.props, d.props_size, lc, lp, pb, dict) != SZ_OK) return 0;
+  return lzgpu::table_cells(lc, lp, pb);
+}
+
 static SRes plan_batch(LzmaGpuStreamDesc* descs, size_t n, uint32_t* order, LzmaGpuPlan* plan,
                        const LzmaGpuPlanOptions& o) {
   if (!order || !plan) return SZ_ERROR_PARAM;
@@ -877,7 +887,22 @@ static SRes plan_batch(LzmaGpuStreamDesc* descs, size_t n, uint32_t* order, Lzma
         const bool coop = o.kernel == LZMA_GPU_KERNEL_COOP ||
                           (o.kernel == LZMA_GPU_KERNEL_AUTO &&
                            (o.coop == 1 || (o.coop == 0 && per_cu_batch <= 8)));
-        if (c.lanes_per_group == 1 && coop) c.lds_mask = LZGPU_LDS_MASK_LAT | lzgpu::kCoopBit;
+        if (c.lanes_per_group == 1 && coop) {
+          c.lds_mask = LZGPU_LDS_MASK_LAT | lzgpu::kCoopBit;
+          if (!(o.flags & LZMA_GPU_PLAN_COOP_LAT)) {
+            // the whole table in LDS if it still fits the streams per CU the
+            // latency plan gives this class: no global round trip left in the
+            // match path (SpecPos, LenHigh) or the matched literal
+            uint32_t stride_all = 0;
+            for (uint32_t i : bucket_idx[b]) stride_all = std::max(stride_all, all_cells(descs[i]));
+            if (stride_all != 0 && stride_all <= kMaxLdsCells) {
+              LzmaGpuLdsClass ca = plan_lds_class(stride_all, bucket_idx[b].size(),
+                                                  LZGPU_LDS_MASK_ALL | lzgpu::kCoopBit, cus, 2, o);
+              const uint64_t want = std::min<uint64_t>(per_cu_batch, c.groups_per_cu);
+              if (ca.lanes_per_group == 1 && ca.groups_per_cu >= want) c = ca;
+            }
+          }
+        }
       }
     }
     if (o.flags & LZMA_GPU_PLAN_KERNEL_LZMA2) c.flags |= LZMA_GPU_CLASS_HAS_LZMA2;

@@ -615,6 +615,14 @@ template <>
 struct BulkReaderFor<LZGPU_LDS_MASK_LAT | kCoopBit> {
   typedef GlobalReaderQ type;
 };
+// every section in LDS (cooperative classes with few streams per CU)
+#ifndef LZGPU_LDS_MASK_ALL
+#define LZGPU_LDS_MASK_ALL 0x7FFu
+#endif
+template <>
+struct BulkReaderFor<LZGPU_LDS_MASK_ALL | kCoopBit> {
+  typedef GlobalReaderQ type;
+};
 
 // checkpoint hooks for readers without them: every NORMALIZE checks
 template <class Rd>

@@ -194,6 +194,15 @@ static int launch_class(const LzmaGpuStreamDesc* d_descs, const uint32_t* d_orde
     return launch_coop<4, MC, K2>(d_descs, d_order, n, d_src, d_dst, d_ws, d_results, stride,
                                   groups_per_cu, max_groups, d_queue, stream);
   }
+  if (lds_mask == (LZGPU_LDS_MASK_ALL | kCoopBit)) {
+    constexpr uint32_t MC = LZGPU_LDS_MASK_ALL | kCoopBit;
+    const uint32_t w = (groups_per_cu + 3) / 4;
+    if (w <= 2)
+      return launch_coop<2, MC, K2>(d_descs, d_order, n, d_src, d_dst, d_ws, d_results, stride,
+                                    groups_per_cu, max_groups, d_queue, stream);
+    return launch_coop<4, MC, K2>(d_descs, d_order, n, d_src, d_dst, d_ws, d_results, stride,
+                                  groups_per_cu, max_groups, d_queue, stream);
+  }
   if (lds_mask == LZGPU_LDS_MASK_LAT)
     return launch_lds_w<LZGPU_LDS_MASK_LAT, K2>(d_descs, d_order, n, d_src, d_dst, d_ws,
                                                 d_results, lanes, stride, waves_per_simd,

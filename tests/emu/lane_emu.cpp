@@ -32,7 +32,12 @@ void emu_decode_batch_lds(const LzmaGpuStreamDesc* descs, size_t n, const uint8_
   uint16_t* slab = (uint16_t*)malloc(size_t(stride) * 2 + 16);
   for (size_t i = 0; i < n; ++i) {
     memset(slab, 0xA5, size_t(stride) * 2);  // LDS is not zeroed between workgroups
-#if defined(EMU_COOP)
+#if defined(EMU_COOP_ALL)
+    // the wave-cooperative kernel with every section in LDS (its default
+    // placement where the whole table fits)
+    results[i] = lane_decode_lds<LZGPU_LDS_MASK_ALL | kCoopBit>(descs[i], src, dst, ws, slab,
+                                                                stride);
+#elif defined(EMU_COOP)
     // the wave-cooperative kernel's instantiation (speculative tree stages run
     // their paths one after another here)
     results[i] = lane_decode_lds<LZGPU_LDS_MASK_LAT | kCoopBit>(descs[i], src, dst, ws, slab,

@@ -130,8 +130,10 @@ def test_plan_batch_workspace_and_order():
     plan, order2 = L.plan_ex(descs)
     assert plan.n == 3 and plan.n_lds == 2 and list(order2) == [1, 0, 2]
     # one LDS launch per table-width class, in the lane order.  A one-stream class
-    # is in the latency regime: placement 0x1BF (all but SpecPos, matched-literal
-    # and LenHigh trees in LDS) = 56 * 2^pb + 324 + 0x100 << (lc+lp) cells
+    # is in the latency regime on the cooperative kernel with the whole table in
+    # LDS (placement 0x7FF: 56 * 2^pb + 950 + 0x300 << (lc+lp) cells); with
+    # LZMA_GPU_PLAN_COOP_LAT the latency placement 0x1BF (all but SpecPos,
+    # matched-literal and LenHigh trees) = 56 * 2^pb + 324 + 0x100 << (lc+lp)
     assert plan.n_classes == 2
     c0, c1 = plan.classes[0], plan.classes[1]
     COOP = 0x80000000  # one stream per workgroup: the wave-cooperative kernel
@@ -139,10 +141,15 @@ def test_plan_batch_workspace_and_order():
     def odd_dwords(cells):  # per-lane slices: an odd number of dwords (LDS banks)
         return ((cells + 1) & ~1) | 2
 
-    assert (c0.n, c0.lds_cells_per_lane, c0.lds_mask) == (1, odd_dwords(56 + 324 + 256), 0x1BF | COOP)
-    assert (c1.n, c1.lds_cells_per_lane, c1.lds_mask) == (1, odd_dwords(56 * 4 + 324 + (256 << 3)),
-                                                          0x1BF | COOP)
+    assert (c0.n, c0.lds_cells_per_lane, c0.lds_mask) == (1, odd_dwords(56 + 950 + 768), 0x7FF | COOP)
+    assert (c1.n, c1.lds_cells_per_lane, c1.lds_mask) == (1, odd_dwords(56 * 4 + 950 + (768 << 3)),
+                                                          0x7FF | COOP)
     assert (c0.lanes_per_group, c0.groups_per_cu) == (1, 16)
+    pl, _ = L.plan_ex(descs, L.plan_options("auto", flags=4))
+    assert (pl.classes[0].lds_cells_per_lane, pl.classes[0].lds_mask) == \
+        (odd_dwords(56 + 324 + 256), 0x1BF | COOP)
+    assert (pl.classes[1].lds_cells_per_lane, pl.classes[1].lds_mask) == \
+        (odd_dwords(56 * 4 + 324 + (256 << 3)), 0x1BF | COOP)
     # a full-size batch is in the throughput regime: placement 0x105 (IsMatch,
     # IsRep/G0/G1/G2, plain literal tree) = 12 * 2^pb + 48 + 0x100 << (lc+lp) cells
     big = L.make_descs([dict(src_off=0, src_len=1000, dst_off=4096 * i, dst_cap=4096,
@@ -179,7 +186,7 @@ def test_plan_options_force_each_instantiation():
         elif k == "latency":
             assert set(masks[k]) == {0x1BF} and set(lanes) == {1}
         elif k == "coop":
-            assert set(masks[k]) == {0x1BF | COOP}
+            assert set(masks[k]) <= {0x1BF | COOP, 0x7FF | COOP} and 0x7FF | COOP in masks[k]
         elif k == "global":
             assert p.n_lds == 0 and p.n_classes == 0
     # 200 narrow streams over 4 CUs = 50 per CU: latency regime by the planner

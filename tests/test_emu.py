@@ -47,6 +47,7 @@ EMU_VARIANTS = {
     "match_fat_global_len": "-DLZGPU_LDS_MASK_LAT=0x105 -DLZGPU_LDS_MASK=0x107 -DEMU_LAT_MASK",
     "latency_instantiation": "-DEMU_LAT_MASK",
     "coop_instantiation": "-DEMU_COOP",
+    "coop_all_lds_instantiation": "-DEMU_COOP_ALL",
     "copy_bytes": "-DLZGPU_COPY_WIDE=0",
     "lit_store_each": "-DLZGPU_LIT_WC=0",
     "lit_threshold": "-DLZGPU_LIT_THR=60 -DLZGPU_LIT_BATCH=32",

@@ -32,9 +32,12 @@ import workloads as W
 pytestmark = pytest.mark.gpu
 
 COOP = 0x80000000
-M_THR, M_LAT = 0x105, 0x1BF
+M_THR, M_LAT, M_ALL = 0x105, 0x1BF, 0x7FF
 RES_DT = np.dtype([("res", "<i4"), ("status", "<i4"), ("dest_len", "<u8"), ("src_len", "<u8")])
-KERNELS = ("throughput", "latency", "coop", "global")
+# coop: the cooperative kernel, every table section in LDS where the table fits
+# (placement 0x7FF); coop_lat: the same kernel on the latency placement 0x1BF
+# (LZMA_GPU_PLAN_COOP_LAT)
+KERNELS = ("throughput", "latency", "coop", "coop_lat", "global")
 
 
 @pytest.fixture(scope="module")
@@ -64,8 +67,15 @@ def _check_plan(plan, kernel):
             assert c.lds_mask == M_THR, hex(c.lds_mask)
         elif kernel == "latency":
             assert c.lds_mask == M_LAT and c.lanes_per_group == 1, hex(c.lds_mask)
+        elif kernel == "coop":
+            # all sections in LDS where the whole table fits the class's
+            # streams per CU, else the latency placement
+            assert c.lds_mask in (M_ALL | COOP, M_LAT | COOP) and c.lanes_per_group == 1, \
+                hex(c.lds_mask)
         else:
             assert c.lds_mask == M_LAT | COOP, hex(c.lds_mask)
+    if kernel == "coop":
+        assert any(c.lds_mask == M_ALL | COOP for c in cls)
     if kernel == "throughput":
         # wave width follows table width: 32 streams per wave for lc+lp = 0
         # (config 3), 8 for lc+lp = 1, 2 for LZMA2 ranges (lc+lp <= 4 slices)
@@ -75,6 +85,8 @@ def _check_plan(plan, kernel):
 def _opts(L, kernel):
     # plan as if the batch were spread over a few CUs, so that the throughput
     # shape (>= 64 streams per CU) is what a real 64K batch gets
+    if kernel == "coop_lat":
+        return L.plan_options("coop", cus=8, flags=4)
     return L.plan_options(kernel, cus=8)
 
 
@@ -334,7 +346,7 @@ def test_cfg4_1024_lzma2_blocks_coop_kernel(L, torch):
              for k, (o, ln, u) in enumerate(blocks)]
     descs = L.make_descs(items)
     plan, res, d_dst = _device_decode(L, torch, descs, np.frombuffer(blob, np.uint8), nb << 20)
-    assert plan.n_classes == 1 and plan.classes[0].lds_mask == M_LAT | COOP
+    assert plan.n_classes == 1 and plan.classes[0].lds_mask == M_ALL | COOP
     assert (res["res"] == 0).all() and (res["status"] == 2).all()
     assert (res["dest_len"] == 1 << 20).all()
     assert (res["src_len"] == np.array([ln for _, ln, _ in blocks])).all()
