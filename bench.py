@@ -1083,7 +1083,8 @@ def issue_roofline(cfg, kernel_ms):
     summary for this config (profiles/pmc_<cfg>.json, written by
     scripts/pmc_summary.py from separate --pmc passes of this bench):
     VALU issue rate against the chip's one VALU wave-instruction per SIMD per
-    clock, lanes active per VALU instruction, share of wave cycles waiting."""
+    4-cycle issue window, lanes active per VALU instruction, share of wave cycles
+    waiting."""
     path = os.path.join(ROOT, "profiles", f"pmc_{cfg}.json")
     if not os.path.exists(path):
         return None
@@ -1095,8 +1096,11 @@ def issue_roofline(cfg, kernel_ms):
     out = {"source": os.path.relpath(path, ROOT), "binary": p.get("binary")}
     clk = p.get("effective_clock_GHz") or 2.4
     if "SQ_INSTS_VALU" in c:
-        # SQ_INSTS_* count per SE/XCD instance summed; wave-instructions per launch
-        peak = 256 * 4 * clk * 1e9  # VALU wave-instructions per second, whole chip
+        # SQ_INSTS_* count per SE/XCD instance summed; wave-instructions per launch.
+        # The sequencer visits a SIMD once per 4-cycle window and issues at most one
+        # VALU instruction there (SQ_ACTIVE_INST_VALU = SQ_INSTS_VALU: one quad-cycle
+        # each), so the chip's VALU issue peak is 256 CUs x 4 SIMDs x clk / 4.
+        peak = 256 * 4 * clk * 1e9 / 4  # VALU wave-instructions per second, whole chip
         rate = c["SQ_INSTS_VALU"] / (kernel_ms * 1e-3)
         out.update({"valu_insts_per_launch": c["SQ_INSTS_VALU"],
                     "salu_insts_per_launch": c.get("SQ_INSTS_SALU"),

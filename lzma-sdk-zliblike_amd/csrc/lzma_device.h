@@ -165,6 +165,10 @@ typedef __attribute__((address_space(1))) uint32_t gu32;
 #ifndef LZGPU_NORM_BRANCHLESS
 #define LZGPU_NORM_BRANCHLESS 0
 #endif
+// branch-free NORMALIZE after a checkpoint (GlobalReaderQ) -- A/B flag
+#ifndef LZGPU_NORMU_BRANCHLESS
+#define LZGPU_NORMU_BRANCHLESS 0
+#endif
 #ifndef LZGPU_BIT_MASK
 #define LZGPU_BIT_MASK 2
 #endif
@@ -690,6 +694,19 @@ struct Rc {
   }
   // NORMALIZE after a reader checkpoint: the byte is known to be in the window
   __device__ __forceinline__ void norm_u() {
+#if LZGPU_NORMU_BRANCHLESS
+    if constexpr (__is_same(Rd, GlobalReaderQ)) {
+      // selects instead of a branch: no exec-mask save/restore and no
+      // s_cbranch per decision (a wave issues one instruction per cycle
+      // window whatever its type)
+      const bool n = range < kTop;
+      code = n ? ((code << 8) | (uint32_t(rd->win) & 0xFFu)) : code;
+      range = n ? (range << 8) : range;
+      rd->win = n ? (rd->win >> 8) : rd->win;
+      rd->nb -= n ? 1u : 0u;
+      return;
+    }
+#endif
     if (range < kTop) {
       range <<= 8;
       code = (code << 8) | rd_take_u(*rd);
