@@ -1078,6 +1078,54 @@ def measure_e2e(L, torch, plan, d_desc, d_order, d_src, d_dst, d_ws, d_res, comp
             "note": "pinned host buffers, copies and decode serialised on one stream"}
 
 
+def measure_e2e_pipelined(L, torch, plan, d_desc, d_order, d_ws, d_res, comp, plain, count, n,
+                          dev, batches):
+    """Serving shape: a stream of batches from pinned host memory, each batch
+    H2D -> decode -> D2H, with batch k+1's H2D and batch k-1's D2H on their own
+    streams (copy engines) while batch k decodes; two device buffer sets.  The
+    steady-state rate is what a service feeding the GPU continuously sees."""
+    nb = int(comp.size)
+    h_src = torch.from_numpy(np.ascontiguousarray(comp)).pin_memory()
+    h_dst = [torch.empty(count * n, dtype=torch.uint8).pin_memory() for _ in range(2)]
+    d_src = [torch.empty(nb + 64, dtype=torch.uint8, device=dev) for _ in range(2)]
+    d_dst = [torch.empty(count * n + 64, dtype=torch.uint8, device=dev) for _ in range(2)]
+    s_h2d, s_dec, s_d2h = (torch.cuda.Stream(dev) for _ in range(3))
+    h2d_done = [torch.cuda.Event() for _ in range(2)]
+    dec_done = [torch.cuda.Event() for _ in range(2)]
+    d2h_done = [torch.cuda.Event() for _ in range(2)]
+    for e in dec_done + d2h_done:
+        e.record(torch.cuda.current_stream(dev))
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for b in range(batches):
+        k = b % 2
+        s_h2d.wait_event(dec_done[k])          # d_src[k] free (batch b-2 decoded)
+        with torch.cuda.stream(s_h2d):
+            d_src[k][:nb].copy_(h_src, non_blocking=True)
+        h2d_done[k].record(s_h2d)
+        s_dec.wait_event(h2d_done[k])
+        s_dec.wait_event(d2h_done[k])          # d_dst[k] free (batch b-2 copied out)
+        if L.decode_batch_device_ex(plan, d_desc.data_ptr(), d_order.data_ptr(),
+                                    d_src[k].data_ptr(), d_dst[k].data_ptr(), d_ws.data_ptr(),
+                                    d_res.data_ptr(), s_dec.cuda_stream):
+            raise RuntimeError(L.last_error())
+        dec_done[k].record(s_dec)
+        s_d2h.wait_event(dec_done[k])
+        with torch.cuda.stream(s_d2h):
+            h_dst[k].copy_(d_dst[k][:count * n], non_blocking=True)
+        d2h_done[k].record(s_d2h)
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    ok = bool(np.array_equal(h_dst[(batches - 1) % 2].numpy(), plain))
+    return {"value": round(batches * count * n / wall / 1e6, 2), "unit": "MB/s",
+            "batches": batches, "ms_per_batch": round(wall / batches * 1e3, 4),
+            "verified": ok,
+            "note": "H2D / decode / D2H of consecutive batches on three streams, two device "
+                    "buffer sets; an H2D overlapping a running decode is starved (12-16 ms "
+                    "instead of 2, profiles/r02_e2e/overlap_timeline.log), so this is no "
+                    "faster than the serial path"}
+
+
 def issue_roofline(cfg, kernel_ms):
     """Issue-side figures of the decode kernel from the committed rocprofv3 PMC
     summary for this config (profiles/pmc_<cfg>.json, written by
@@ -1228,6 +1276,9 @@ def main():
     if not args.no_e2e:
         e2e = measure_e2e(L, torch, plan, d_desc, d_order, d_src, d_dst, d_ws, d_res, comp, count,
                           n, stream, min(args.steps, 5))
+        e2e["pipelined"] = measure_e2e_pipelined(L, torch, plan, d_desc, d_order, d_ws, d_res,
+                                                 comp, plain, count, n, dev, 8)
+        ok = D.all_true(ok and e2e["pipelined"]["verified"], dev)
 
     total_streams = int(D.reduce_sum(float(count), dev))
     total_bytes = total_streams * n * args.steps
