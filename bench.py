@@ -427,6 +427,35 @@ def run_cfg4(args):
     dec_ms = float(np.mean([b.elapsed_time(c) for _, b, c in ev]))
     scat_ms = D.reduce_max(scat_ms, dev)
 
+    # optional last exchange: every rank's decoded blocks
+    # gathered on rank 0 by grouped point-to-point receives; timed on its own
+    gather = None
+    if world > 1 and not args.no_gather:
+        sizes = [int(sum(u for _, _, u in table[r])) for r in range(world)]
+        whole = torch.empty(sum(sizes), dtype=torch.uint8, device=dev) if rank == 0 else None
+        D.barrier()
+        g0, g1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        g0.record(stream)
+        D.gather_ranges(d_dst, sizes, whole, rank, world)
+        g1.record(stream)
+        torch.cuda.synchronize()
+        g_ms = D.reduce_max(float(g0.elapsed_time(g1)), dev)
+        g_ok = True
+        if rank == 0:  # each rank's first and last block, by their CRC-32, where they belong
+            import zlib
+            off = 0
+            for r in range(world):
+                us = [u for _, _, u in table[r]]
+                for j in (0, len(us) - 1):
+                    a = off + sum(us[:j])
+                    blk = whole[a:a + us[j]].cpu().numpy().tobytes()
+                    g_ok = g_ok and zlib.crc32(blk) == crc_seq[r * B + j]
+                off += sizes[r]
+        gather = {"gather_ms": round(g_ms, 4), "bytes_to_rank0": int(sum(sizes[1:])),
+                  "GBps_into_rank0": round(sum(sizes[1:]) / (g_ms * 1e-3) / 1e9, 2),
+                  "verified": D.all_true(g_ok, dev)}
+        del whole
+
     # verify: per-block results and the CRC of every decoded block (on the GPU)
     res = np.frombuffer(d_res.cpu().numpy().tobytes(), dtype=np.dtype(
         [("res", "<i4"), ("status", "<i4"), ("dest_len", "<u8"), ("src_len", "<u8")]))
@@ -471,7 +500,8 @@ def run_cfg4(args):
                        "exchange": {"collective": "grouped P2P isend/irecv from rank 0"
                                     if world > 1 else "none (1 GPU)",
                                     "scatter_ms": round(scat_ms, 4),
-                                    "bytes_per_peer": comp_bytes}},
+                                    "bytes_per_peer": comp_bytes,
+                                    "gather": gather}},
             "roofline": {"bound": "issue", "priced_against": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
                          "traffic": None, "kernel": "lzgpu_decode_lds_kernel",
@@ -1180,6 +1210,8 @@ def main():
     ap.add_argument("--config", default="cfg3", choices=sorted(CONFIGS) + ["cfg4", "cfg5", "xz", "7z"])
     ap.add_argument("--streams", type=int, default=0, help="cfg5: streams per GPU (32768)")
     ap.add_argument("--blocks", type=int, default=1024, help="cfg4: LZMA2 blocks per GPU")
+    ap.add_argument("--no-gather", action="store_true",
+                    help="cfg4: skip the optional gather of decoded blocks on rank 0")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-crc", action="store_true", help="skip the CRC-32 (8(f) row 1) leg")
     ap.add_argument("--no-e2e", action="store_true", help="skip the H2D + decode + D2H leg")

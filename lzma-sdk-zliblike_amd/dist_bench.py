@@ -9,7 +9,8 @@ tensors) on the GPU box and "gloo" (CPU tensors) in the CPU test-suite.
 Config 4 (LZMA2 dict-reset blocks) has the one real exchange:
 the compressed file sits on rank 0 and each peer receives the byte range of its
 blocks (and its block table) by point-to-point sends -- RCCL over xGMI on the
-box, one link per peer, all sends posted as one group.
+box, one link per peer, all sends posted as one group.  The optional last step
+(8(e) step 5) gathers every rank's decoded blocks back to rank 0 the same way.
 """
 import os
 
@@ -106,6 +107,31 @@ def scatter_ranges(src, ranges, out, rank, world):
                 ops.append(dist.P2POp(dist.isend, src[a:b], r))
     elif hi > lo:
         ops.append(dist.P2POp(dist.irecv, out, 0))
+    if ops:
+        for req in dist.batch_isend_irecv(ops):
+            req.wait()
+
+
+def gather_ranges(mine, sizes, out, rank, world):
+    """Every rank r sends its `mine` (sizes[r] elements) to rank 0, which lands
+    it at out[sum(sizes[:r]) : + sizes[r]] (its own part by a local copy); out
+    is only written on rank 0 (None elsewhere).  One grouped point-to-point
+    batch, like scatter_ranges."""
+    import torch.distributed as dist
+    offs = [0]
+    for n in sizes:
+        offs.append(offs[-1] + n)
+    if rank == 0:
+        out[offs[0]:offs[1]].copy_(mine[:sizes[0]])
+    if world == 1:
+        return
+    ops = []
+    if rank == 0:
+        for r in range(1, world):
+            if sizes[r]:
+                ops.append(dist.P2POp(dist.irecv, out[offs[r]:offs[r + 1]], r))
+    elif sizes[rank]:
+        ops.append(dist.P2POp(dist.isend, mine[:sizes[rank]], 0))
     if ops:
         for req in dist.batch_isend_irecv(ops):
             req.wait()

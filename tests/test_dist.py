@@ -105,18 +105,27 @@ def _scatter_worker(rank, world, port, q):
         D.scatter_ranges(src, ranges, out, rank, world)
         mine = out.numpy().tobytes()
         orc = native.oracle()
-        ok = True
+        ok, decoded = True, []
         for k in range(per_rank):
             b = rank * per_rank + k
             blk = mine[offs[b] - lo:offs[b + 1] - lo]
             res, st, dl, sl, data = native.lzma2_decode(orc, "orc", blk, 16, len(plain[b]), 0)
             ok = ok and (res, st, dl, sl) == (0, 2, len(plain[b]), len(blk)) and data == plain[b]
+            decoded.append(data)
+        # the optional last step: every rank's decoded blocks gathered on rank 0
+        dec = b"".join(decoded)
+        sizes = [sum(len(plain[r * per_rank + k]) for k in range(per_rank)) for r in range(world)]
+        whole = torch.empty(sum(sizes), dtype=torch.uint8) if rank == 0 else None
+        D.gather_ranges(torch.frombuffer(bytearray(dec), dtype=torch.uint8), sizes, whole, rank,
+                        world)
+        if rank == 0:
+            ok = ok and whole.numpy().tobytes() == b"".join(plain)
         q.put((rank, len(mine), ok))
     finally:
         dist.destroy_process_group()
 
 
-def test_two_rank_gloo_lzma2_block_scatter():
+def test_two_rank_gloo_lzma2_block_scatter_and_gather():
     world = 2
     port = _free_port()
     ctx = mp.get_context("spawn")
