@@ -1156,6 +1156,36 @@ def measure_e2e_pipelined(L, torch, plan, d_desc, d_order, d_ws, d_res, comp, pl
                     "faster than the serial path"}
 
 
+def run_secondary(cfgs, steps=5, warmup=1, timeout=420):
+    """The other BASELINE configs, each a short run of this script in a child
+    process (started, not exec'd: this process has touched the GPU), so the
+    default bench line also carries them.  Not `value`."""
+    out = {}
+    for c in cfgs:
+        cmd = [sys.executable, os.path.abspath(__file__), "--config", c, "--steps", str(steps),
+               "--warmup", str(warmup), "--no-cpu-baseline", "--no-e2e", "--no-crc",
+               "--no-secondary"]
+        t0 = time.perf_counter()
+        try:
+            r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                               timeout=timeout, env=os.environ.copy())
+            lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+            d = json.loads(lines[-1]) if lines else {}
+        except (subprocess.TimeoutExpired, ValueError) as e:
+            d, r = {"error": type(e).__name__}, None
+        roof = d.get("roofline") or {}
+        cfg_d = d.get("config") or {}
+        out[c] = {"value": d.get("value"), "unit": d.get("unit"),
+                  "ms_per_step": d.get("ms_per_step"),
+                  "kernel_avg_ms": roof.get("kernel_avg_ms") or
+                  (cfg_d.get("kernel_ms") or {}).get("lzma2_batch"),
+                  "workload": cfg_d.get("workload"), "kernel_plan": cfg_d.get("kernel_plan"),
+                  "verified": bool(d.get("verified")) and (r is not None and r.returncode == 0),
+                  "wall_s": round(time.perf_counter() - t0, 1)}
+        log(f"[secondary] {c}: {out[c]['value']} MB/s verified={out[c]['verified']}")
+    return out
+
+
 def issue_roofline(cfg, kernel_ms):
     """Issue-side figures of the decode kernel from the committed rocprofv3 PMC
     summary for this config (profiles/pmc_<cfg>.json, written by
@@ -1217,6 +1247,9 @@ def main():
     ap.add_argument("--no-e2e", action="store_true", help="skip the H2D + decode + D2H leg")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher, sharding and reductions on CPU (gloo), no decode")
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="config 3 at N = 1: skip the short runs of configs 2, 4 and 5 "
+                         "reported under 'secondary'")
     args = ap.parse_args()
     if "RANK" not in os.environ and args.gpus > 1:
         return launch_ranks(args.gpus)  # spawns the ranks; touches no GPU here
@@ -1353,6 +1386,10 @@ def main():
         except Exception:
             traffic = None
     issue = issue_roofline(args.config, avg_kern_ms)
+    secondary = None
+    if rank == 0 and world == 1 and args.config == "cfg3" and not args.no_secondary:
+        # reported with their own `verified`; the headline's stands on config 3 alone
+        secondary = run_secondary(("cfg2", "cfg4", "cfg5"))
 
     if rank == 0:
         line = {
@@ -1391,6 +1428,7 @@ def main():
             "e2e": e2e,
             "cpu_baseline": cpu_base,
             "crc32": crc,
+            "secondary": secondary,
             "verified": ok,
         }
         print(json.dumps(line), flush=True)
