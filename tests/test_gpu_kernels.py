@@ -19,6 +19,7 @@ Bit-exact throughout: output bytes and {res, status, destLen, srcLen}.
 """
 import ctypes
 import lzma
+import os
 import random
 from concurrent.futures import ThreadPoolExecutor
 
@@ -150,10 +151,12 @@ def _fuzz_set():
     (the CPU restatement, pinned to the reference's vectors)."""
     if "v" in _FUZZ:
         return _FUZZ["v"]
-    rng = random.Random(7331)
+    # a bigger campaign: LZGPU_FUZZ_CASES / LZGPU_FUZZ_SEED (profiles/r02_tests/)
+    cases = int(os.environ.get("LZGPU_FUZZ_CASES", "1500"))
+    rng = random.Random(int(os.environ.get("LZGPU_FUZZ_SEED", "7331")))
     orc = native.oracle()
     items, srcs, exp, off, doff = [], [], [], 0, 0
-    for it in range(1500):
+    for it in range(cases):
         lc, lp, pb = rng.randrange(5), rng.randrange(3), rng.randrange(5)
         if lc + lp > 4:
             lp = 0
