@@ -204,6 +204,76 @@ def test_fuzz_vs_oracle_each_kernel(L, kernel):
     assert not bad, (kernel, len(bad), bad[:8])
 
 
+# ---------------------------------------------------------------- LZMA2 fuzz, every kernel
+
+_FUZZ2 = {}
+
+
+def _fuzz2_set():
+    """Seeded LZMA2 items (600 by default; LZGPU_FUZZ2_CASES / LZGPU_FUZZ2_SEED):
+    random lc/lp/pb and dictionary props, 0-300 KB of text / random / runs (so
+    several chunks, stored chunks for random data), with or without the end
+    byte, bit flips, truncations, capacities, both finish modes and a few bad
+    dictionary props; expectations from the oracle's Lzma2Dec_DecodeToDic
+    restatement (the 7zDec.c:181-202 pattern the golden LZMA2 vectors pin)."""
+    if "v" in _FUZZ2:
+        return _FUZZ2["v"]
+    cases = int(os.environ.get("LZGPU_FUZZ2_CASES", "600"))
+    rng = random.Random(int(os.environ.get("LZGPU_FUZZ2_SEED", "2718")))
+    orc = native.oracle()
+    items, srcs, exp, off, doff = [], [], [], 0, 0
+    for it in range(cases):
+        lc = rng.randrange(5)
+        lp = rng.randrange(5 - lc)
+        pb = rng.randrange(5)
+        prop = rng.choice([0, 8, 16, 18])        # dict 4 KiB, 64 KiB, 1 MiB, 2 MiB
+        dsz = (2 | (prop & 1)) << (prop // 2 + 11)
+        n = rng.choice([0, 1, 100, 5000, 70000, 140000, 300000])
+        kind = rng.choice(["text", "text", "random", "runs"])
+        data = native.gen(kind, 97_000 + it, n)
+        filt = [{"id": lzma.FILTER_LZMA2, "dict_size": dsz, "lc": lc, "lp": lp, "pb": pb,
+                 "preset": rng.choice([0, 6])}]
+        comp = bytearray(lzma.compress(data, format=lzma.FORMAT_RAW, filters=filt))
+        mode = rng.randrange(6)
+        if mode == 1 and len(comp) > 8:
+            for _ in range(rng.randrange(1, 4)):
+                comp[rng.randrange(len(comp))] ^= 1 << rng.randrange(8)
+        elif mode == 2:
+            comp = comp[:rng.randrange(len(comp) + 1)]
+        elif mode == 3 and comp:
+            comp = comp[:-1]                      # no end byte
+        if rng.random() < 0.02:
+            prop = rng.choice([41, 60, 255])      # bad dictionary prop
+        cap = max(0, n + rng.choice([0, 0, 0, 1, -1, 100, -100, -20000]))
+        fin = rng.randrange(2)
+        comp = bytes(comp)
+        items.append(dict(src_off=off, src_len=len(comp), dst_off=doff, dst_cap=cap,
+                          props=bytes([prop]), finish=fin, kind=1))
+        srcs.append(comp)
+        exp.append(native.lzma2_decode(orc, "orc", comp, prop, cap, fin))
+        off += len(comp)
+        doff += cap
+    _FUZZ2["v"] = (items, b"".join(srcs), doff, exp)
+    return _FUZZ2["v"]
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_lzma2_fuzz_vs_oracle_each_kernel(L, kernel):
+    items, src, dst_bytes, exp = _fuzz2_set()
+    descs = L.make_descs(items)
+    plan = L.Plan()
+    r, res, dst = L.decode_batch_host(descs, src, dst_bytes, _opts(L, kernel), plan)
+    assert r == 0, L.last_error()
+    bad = []
+    for k in range(len(items)):
+        got = (res[k].res, res[k].status, res[k].dest_len, res[k].src_len)
+        out = dst[items[k]["dst_off"]:items[k]["dst_off"] + res[k].dest_len]
+        want = exp[k][:4]
+        if got != want or out != exp[k][4]:
+            bad.append((k, got, exp[k][:4]))
+    assert not bad, (kernel, len(bad), bad[:8])
+
+
 # ---------------------------------------------------------------- full-size configs
 
 def _device_decode(L, torch, descs, comp, dst_bytes, opts=None):
