@@ -458,3 +458,95 @@ int ref_lzma_decode_batch(const unsigned char *src, const uint64_t *src_off,
   pthread_mutex_destroy(&b.mu);
   return b.errors;
 }
+
+/*
+ * CPU baseline for LZMA2 blocks (config 4): the 7zDec.c:181-202 pattern --
+ * Lzma2Dec_AllocateProbs + Lzma2Dec_Init + Lzma2Dec_DecodeToDic over a flat
+ * dictionary -- per block on `threads` host threads; fd 1 at /dev/null for the
+ * whole batch (the per-call redirect of ref_lzma2_decode is not thread-safe).
+ */
+typedef struct {
+  const unsigned char *src;
+  const uint64_t *src_off, *src_len, *dst_off, *dst_cap;
+  unsigned char *dst;
+  unsigned char prop;
+  int fin;
+  int32_t *res_out;
+  uint64_t *dest_len_out;
+  size_t n, next;
+  pthread_mutex_t mu;
+  int errors;
+} ref2_batch;
+
+static void *ref2_batch_worker(void *arg) {
+  ref2_batch *b = (ref2_batch *)arg;
+  int errs = 0;
+  /* one decoder per thread, its probabilities allocated once (the same prop
+     for every block), re-initialised per block as 7zDec.c does per folder */
+  CLzma2Dec dec;
+  SRes ar;
+  Lzma2Dec_Construct(&dec);
+  ar = Lzma2Dec_AllocateProbs(&dec, b->prop, &g_shim_alloc);
+  for (;;) {
+    size_t k;
+    pthread_mutex_lock(&b->mu);
+    k = b->next++;
+    pthread_mutex_unlock(&b->mu);
+    if (k >= b->n) break;
+    {
+      ELzmaStatus st;
+      SizeT sl = (SizeT)b->src_len[k];
+      SRes r = ar;
+      if (r == SZ_OK) {
+        dec.decoder.dic = b->dst + b->dst_off[k];
+        dec.decoder.dicBufSize = (SizeT)b->dst_cap[k];
+        Lzma2Dec_Init(&dec);
+        r = Lzma2Dec_DecodeToDic(&dec, (SizeT)b->dst_cap[k], b->src + b->src_off[k], &sl,
+                                 (ELzmaFinishMode)b->fin, &st);
+        if (b->dest_len_out) b->dest_len_out[k] = dec.decoder.dicPos;
+      }
+      if (b->res_out) b->res_out[k] = r;
+      if (r != SZ_OK) errs++;
+    }
+  }
+  Lzma2Dec_FreeProbs(&dec, &g_shim_alloc);
+  pthread_mutex_lock(&b->mu);
+  b->errors += errs;
+  pthread_mutex_unlock(&b->mu);
+  return NULL;
+}
+
+int ref_lzma2_decode_batch(const unsigned char *src, const uint64_t *src_off,
+                           const uint64_t *src_len, unsigned char prop, unsigned char *dst,
+                           const uint64_t *dst_off, const uint64_t *dst_cap, int finish_mode,
+                           int32_t *res_out, uint64_t *dest_len_out, size_t n, int threads) {
+  ref2_batch b;
+  pthread_t tid[256];
+  int t, saved;
+  if (threads < 1) threads = 1;
+  if (threads > 256) threads = 256;
+  b.src = src;
+  b.src_off = src_off;
+  b.src_len = src_len;
+  b.prop = prop;
+  b.dst = dst;
+  b.dst_off = dst_off;
+  b.dst_cap = dst_cap;
+  b.fin = finish_mode;
+  b.res_out = res_out;
+  b.dest_len_out = dest_len_out;
+  b.n = n;
+  b.next = 0;
+  b.errors = 0;
+  pthread_mutex_init(&b.mu, NULL);
+  saved = quiet_begin();
+  if (threads == 1) {
+    ref2_batch_worker(&b);
+  } else {
+    for (t = 0; t < threads; t++) pthread_create(&tid[t], NULL, ref2_batch_worker, &b);
+    for (t = 0; t < threads; t++) pthread_join(tid[t], NULL);
+  }
+  quiet_end(saved);
+  pthread_mutex_destroy(&b.mu);
+  return b.errors;
+}

@@ -74,6 +74,10 @@ def ref():
         f.restype = ctypes.c_int
         f.argtypes = [ctypes.c_void_p] * 7 + [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                                               ctypes.c_size_t, ctypes.c_int]
+        f = lib.ref_lzma2_decode_batch
+        f.restype = ctypes.c_int
+        f.argtypes = [ctypes.c_void_p] * 3 + [ctypes.c_ubyte] + [ctypes.c_void_p] * 3 + [
+            ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
         lib._declared = True
     return lib
 
