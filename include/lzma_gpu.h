@@ -221,7 +221,10 @@ size_t LzmaGpu_PlanBatch(LzmaGpuStreamDesc *descs, size_t n, uint32_t *order);
  * environment on every call: LZGPU_KERNEL=global|throughput|latency|coop,
  * LZGPU_LANES=<streams per workgroup>, LZGPU_GROUPS=<workgroups per CU>,
  * LZGPU_OCC=<1|2|4 waves per SIMD>, LZGPU_CUS, LZGPU_COOP=0|1,
- * LZGPU_PERSIST=0 (one stream per lane), LZGPU_CLASSES=1 (one LDS launch).
+ * LZGPU_PERSIST=0 (one stream per lane), LZGPU_CLASSES=1 (one LDS launch),
+ * LZGPU_SLICE_ALIGN8=1, LZGPU_KERNEL_LZMA2=1, LZGPU_COOP_LAT=1 (the
+ * LZMA_GPU_PLAN_* flags below); DecodeBatchEx reads LZGPU_CLASS_STREAMS=0
+ * (classes launched one after another on the caller's stream).
  * workspace_bytes includes the LDS launches' work counters at queue_offset
  * (zeroed by every DecodeBatchEx launch on its stream). */
 #define LZMA_GPU_MAX_CLASSES 4
