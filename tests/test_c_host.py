@@ -1,0 +1,97 @@
+"""The drop-in from C: tests/c_host/lzma_c_host.c is written against the LZMA
+SDK's own decode API (LzmaUncompress, LzmaDecode, LzmaDec_Allocate + Init +
+DecodeToBuf, CrcCalc) the way a user of the reference calls it, compiled with
+include/lzma_gpu.h in place of LzmaDec.h / LzmaLib.h / 7zCrc.h and linked to
+liblzmagpu.so (no Python, no torch in the process).
+
+CPU: it builds warning-free and, with no device, every call fails loudly with
+SZ_ERROR_FAIL (no CPU fallback).  GPU: its results -- res, status, destLen,
+srcLen, the CRC-32 of the output, the streaming loop's call count -- equal the
+oracle's LzmaDecode / DecodeToBuf loop on the same inputs (the restatement
+pinned to the reference's vectors)."""
+import os
+import subprocess
+import zlib
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SRC = os.path.join(ROOT, "tests", "c_host", "lzma_c_host.c")
+BIN = os.path.join(ROOT, "tests", "c_host", "build", "lzma_c_host")
+
+
+def build_c_host():
+    """gcc -Wall -Wextra -Werror against include/, rpath to the in-tree library."""
+    os.makedirs(os.path.dirname(BIN), exist_ok=True)
+    subprocess.run(["gcc", "-O2", "-std=c99", "-Wall", "-Wextra", "-Werror", "-D_POSIX_C_SOURCE=200809L",
+                    "-I", os.path.join(ROOT, "include"), "-o", BIN, SRC,
+                    "-L", os.path.join(ROOT, "lzma-sdk-zliblike_amd", "lib"), "-llzmagpu",
+                    "-Wl,-rpath,$ORIGIN/../../../lzma-sdk-zliblike_amd/lib"], check=True)
+    return BIN
+
+
+def _run(tmp, props, src, out_size, in_chunk, out_chunk):
+    p, s = os.path.join(tmp, "props.bin"), os.path.join(tmp, "stream.bin")
+    open(p, "wb").write(props)
+    open(s, "wb").write(src)
+    r = subprocess.run([BIN, p, s, str(out_size), str(in_chunk), str(out_chunk)],
+                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    return {ln.split()[0]: ln.split()[1:] for ln in r.stdout.splitlines()}
+
+
+def test_c_host_builds_and_fails_loudly_without_gpu(tmp_path):
+    import lzma
+    build_c_host()
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("a device is visible: the GPU test covers this host")
+    data = b"drop-in from C " * 500
+    comp = lzma.compress(data, format=lzma.FORMAT_RAW, filters=[
+        {"id": lzma.FILTER_LZMA1, "dict_size": 1 << 16, "lc": 3, "lp": 0, "pb": 2}])
+    out = _run(str(tmp_path), bytes([0x5D]) + (1 << 16).to_bytes(4, "little"), comp,
+               len(data), 1000, 4096)
+    for name in ("LzmaUncompress", "LzmaDecode", "LzmaDec_DecodeToBuf"):
+        assert out[name][0] == "11", (name, out[name])  # SZ_ERROR_FAIL, nothing decoded
+        assert out[name][2] == "0"
+
+
+@pytest.mark.gpu
+def test_gpu_c_host_matches_oracle(tmp_path):
+    import lzma
+    import native
+    import workloads as W
+    if not os.path.exists(BIN):
+        build_c_host()
+    orc = native.oracle()
+    cases = []
+    for k, (lc, lp, pb, dsz, n, mark, cut, in_chunk, out_chunk) in enumerate([
+            (3, 0, 2, 1 << 16, 200_000, False, 0, 1000, 4096),
+            (3, 0, 2, 1 << 16, 200_000, True, 0, 7, 65536),
+            (0, 2, 0, 4096, 50_000, True, 0, 1 << 20, 1),
+            (4, 0, 4, 1 << 20, 300_000, False, 100, 4096, 100_000),
+            (1, 1, 1, 1 << 14, 30_000, True, 7, 333, 777)]):
+        data = native.gen("text", 555_000 + k, n)
+        filt = {"id": lzma.FILTER_LZMA1, "dict_size": dsz, "lc": lc, "lp": lp, "pb": pb}
+        if mark:
+            comp = lzma.compress(data, format=lzma.FORMAT_ALONE, filters=[filt])[13:]
+        else:
+            comp = lzma.compress(data, format=lzma.FORMAT_RAW, filters=[filt])
+        if cut:
+            comp = comp[:-cut]
+        cases.append((W.props_bytes(lc, lp, pb, dsz), comp, n, in_chunk, out_chunk))
+    for props, comp, n, in_chunk, out_chunk in cases:
+        out = _run(str(tmp_path), props, comp, n, in_chunk, out_chunk)
+        res, st, dl, sl, dec = native.decode(orc, "orc", comp, props, n, 0)
+        assert out["LzmaUncompress"] == [str(res), "-", str(dl), str(sl),
+                                         "%08x" % zlib.crc32(dec)]
+        res, st, dl, sl, dec = native.decode(orc, "orc", comp, props, n, 1)
+        got = out["LzmaDecode"]
+        assert [got[0], got[2], got[3], got[4]] == [str(res), str(dl), str(sl),
+                                                    "%08x" % zlib.crc32(dec)]
+        if res == 0:
+            assert got[1] == str(st)
+        calls, trace, dec, used = native.stream_decode(orc, "orc", comp, props, n, in_chunk,
+                                                       out_chunk, 0)
+        assert out["LzmaDec_DecodeToBuf"] == [str(trace[-1][0]), str(trace[-1][1]), str(len(dec)),
+                                              str(used), "%08x" % zlib.crc32(dec), str(calls)]
