@@ -30,6 +30,25 @@ def build_c_host():
     return BIN
 
 
+BATCH_SRC = os.path.join(ROOT, "tests", "c_host", "lzma_c_batch.c")
+BATCH_BIN = os.path.join(ROOT, "tests", "c_host", "build", "lzma_c_batch")
+
+
+def build_c_batch():
+    """The batch program also calls the HIP runtime's C API (hipMalloc, ...):
+    gcc with ROCm's headers (__HIP_PLATFORM_AMD__ is what hipcc would define
+    for them) and libamdhip64."""
+    os.makedirs(os.path.dirname(BATCH_BIN), exist_ok=True)
+    subprocess.run(["gcc", "-O2", "-std=c99", "-Wall", "-Wextra", "-Werror",
+                    "-D__HIP_PLATFORM_AMD__", "-I", os.path.join(ROOT, "include"),
+                    "-I", "/opt/rocm/include", "-o", BATCH_BIN, BATCH_SRC,
+                    "-L", os.path.join(ROOT, "lzma-sdk-zliblike_amd", "lib"), "-llzmagpu",
+                    "-L", "/opt/rocm/lib", "-lamdhip64",
+                    "-Wl,-rpath,$ORIGIN/../../../lzma-sdk-zliblike_amd/lib",
+                    "-Wl,-rpath,/opt/rocm/lib"], check=True)
+    return BATCH_BIN
+
+
 def _run(tmp, props, src, out_size, in_chunk, out_chunk):
     p, s = os.path.join(tmp, "props.bin"), os.path.join(tmp, "stream.bin")
     open(p, "wb").write(props)
@@ -43,6 +62,7 @@ def _run(tmp, props, src, out_size, in_chunk, out_chunk):
 def test_c_host_builds_and_fails_loudly_without_gpu(tmp_path):
     import lzma
     build_c_host()
+    build_c_batch()
     import torch
     if torch.cuda.is_available():
         pytest.skip("a device is visible: the GPU test covers this host")
@@ -95,3 +115,53 @@ def test_gpu_c_host_matches_oracle(tmp_path):
                                                        out_chunk, 0)
         assert out["LzmaDec_DecodeToBuf"] == [str(trace[-1][0]), str(trace[-1][1]), str(len(dec)),
                                               str(used), "%08x" % zlib.crc32(dec), str(calls)]
+
+
+@pytest.mark.gpu
+def test_gpu_c_batch_host_and_device_match_oracle(tmp_path):
+    """300 streams (mixed lc/lp/pb and dictionaries, corrupt and truncated ones)
+    through LzmaGpu_DecodeBatchHost and through PlanBatchEx + DecodeBatchEx on
+    the C program's own hipMalloc'd buffers: per-stream results and output CRCs
+    equal the oracle's LzmaDecode."""
+    import lzma
+    import random
+    import struct
+    import native
+    import workloads as W
+    if not os.path.exists(BATCH_BIN):
+        build_c_batch()
+    rng = random.Random(99)
+    orc = native.oracle()
+    cap = 20000
+    srcs, lens, props_all, want = [], [], [], []
+    for i in range(300):
+        lc = rng.randrange(5)
+        lp = rng.randrange(5 - lc)
+        pb = rng.randrange(5)
+        dsz = rng.choice([4096, 1 << 16])
+        n = rng.choice([0, 10, 4096, 15000, 20000])
+        data = native.gen(rng.choice(["text", "random"]), 777_000 + i, n)
+        comp = bytearray(lzma.compress(data, format=lzma.FORMAT_RAW, filters=[
+            {"id": lzma.FILTER_LZMA1, "dict_size": dsz, "lc": lc, "lp": lp, "pb": pb}]))
+        if i % 7 == 3 and len(comp) > 8:
+            comp[rng.randrange(5, len(comp))] ^= 0x10
+        if i % 11 == 5:
+            comp = comp[:rng.randrange(len(comp) + 1)]
+        props = W.props_bytes(lc, lp, pb, dsz)
+        res, st, dl, sl, dec = native.decode(orc, "orc", bytes(comp), props, cap, 0)
+        srcs.append(bytes(comp))
+        lens.append(len(comp))
+        props_all.append(props)
+        want.append("%d %d %d %d %08x" % (res, st, dl, sl, zlib.crc32(dec)))
+    files = {k: os.path.join(str(tmp_path), k) for k in ("src", "lens", "props")}
+    open(files["src"], "wb").write(b"".join(srcs))
+    open(files["lens"], "wb").write(b"".join(struct.pack("<Q", x) for x in lens))
+    open(files["props"], "wb").write(b"".join(props_all))
+    for mode in ("host", "device"):
+        r = subprocess.run([BATCH_BIN, mode, files["src"], files["lens"], files["props"],
+                            str(cap), "0"], stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                           text=True, timeout=120)
+        assert r.returncode == 0, (mode, r.stderr)
+        got = r.stdout.splitlines()
+        bad = [(k, got[k], want[k]) for k in range(len(want)) if got[k] != want[k]]
+        assert len(got) == len(want) and not bad, (mode, bad[:5])
