@@ -222,7 +222,7 @@ size_t LzmaGpu_PlanBatch(LzmaGpuStreamDesc *descs, size_t n, uint32_t *order);
  * LZGPU_LANES=<streams per workgroup>, LZGPU_GROUPS=<workgroups per CU>,
  * LZGPU_OCC=<1|2|4 waves per SIMD>, LZGPU_CUS, LZGPU_COOP=0|1,
  * LZGPU_PERSIST=0 (one stream per lane), LZGPU_CLASSES=1 (one LDS launch),
- * LZGPU_SLICE_ALIGN8=1, LZGPU_KERNEL_LZMA2=1, LZGPU_COOP_LAT=1 (the
+ * LZGPU_SLICE_ALIGN8=1, LZGPU_KERNEL_LZMA2=1, LZGPU_COOP_LAT=1, LZGPU_MERGE_LAT=0 (the
  * LZMA_GPU_PLAN_* flags below); DecodeBatchEx reads LZGPU_CLASS_STREAMS=0
  * (classes launched one after another on the caller's stream).
  * workspace_bytes includes the LDS launches' work counters at queue_offset
@@ -300,6 +300,9 @@ typedef struct LzmaGpuPlanOptions {
  * (placement 0x7FF) when the whole table fits the class's streams per CU --
  * config 4 2.85 -> 3.00 GB/s, the xz leg 2.52 -> 2.63 (profiles/r02_ab/). */
 #define LZMA_GPU_PLAN_COOP_LAT 4u
+/* one class per table-width bucket even when several land in the one-lane
+ * latency regime (default: those are merged into one class, one launch) */
+#define LZMA_GPU_PLAN_NO_MERGE_LAT 8u
 
 /* LzmaGpu_PlanBatchEx with explicit options (opt == NULL: as PlanBatchEx,
  * whose defaults take the LZGPU_* experiment variables of the environment,

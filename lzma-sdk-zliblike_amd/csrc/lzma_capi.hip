@@ -704,7 +704,7 @@ static uint32_t device_cus() {
 // call time (LZGPU_KERNEL=global|throughput|latency|coop, LZGPU_MASK=1|2,
 // LZGPU_COOP=0|1, LZGPU_CUS, LZGPU_LANES, LZGPU_GROUPS, LZGPU_OCC,
 // LZGPU_PERSIST=0, LZGPU_CLASSES=1, LZGPU_SLICE_ALIGN8=1, LZGPU_KERNEL_LZMA2=1,
-// LZGPU_COOP_LAT=1).  Only LzmaGpu_PlanBatchEx reads them;
+// LZGPU_COOP_LAT=1, LZGPU_MERGE_LAT=0).  Only LzmaGpu_PlanBatchEx reads them;
 // LzmaGpu_PlanBatchOpt takes its options from the caller alone.
 static LzmaGpuPlanOptions env_options() {
   LzmaGpuPlanOptions o;
@@ -732,7 +732,8 @@ static LzmaGpuPlanOptions env_options() {
   o.one_class = env_int("LZGPU_CLASSES", 0) == 1 ? 1u : 0u;
   o.flags = (env_int("LZGPU_SLICE_ALIGN8", 0) ? LZMA_GPU_PLAN_SLICE_ALIGN8 : 0u) |
             (env_int("LZGPU_KERNEL_LZMA2", 0) ? LZMA_GPU_PLAN_KERNEL_LZMA2 : 0u) |
-            (env_int("LZGPU_COOP_LAT", 0) ? LZMA_GPU_PLAN_COOP_LAT : 0u);
+            (env_int("LZGPU_COOP_LAT", 0) ? LZMA_GPU_PLAN_COOP_LAT : 0u) |
+            (env_int("LZGPU_MERGE_LAT", 1) ? 0u : LZMA_GPU_PLAN_NO_MERGE_LAT);
   return o;
 }
 
@@ -742,7 +743,7 @@ static LzmaGpuPlanOptions env_options() {
 // 2 = latency shape (one stream per wave) forced.
 static LzmaGpuLdsClass plan_lds_class(uint32_t stride, uint64_t count, uint32_t mask,
                                       uint32_t cus, int regime, const LzmaGpuPlanOptions& o,
-                                      bool* latency = nullptr) {
+                                      bool* latency = nullptr, bool any_groups = false) {
   LzmaGpuLdsClass c;
   memset(&c, 0, sizeof c);
   c.lds_mask = mask;
@@ -787,7 +788,11 @@ static LzmaGpuLdsClass plan_lds_class(uint32_t stride, uint64_t count, uint32_t 
     lanes = std::max<uint32_t>(1, std::min<uint32_t>(32, pow2floor(std::max<uint32_t>(1, per_cu / 8))));
     groups = pow2floor(std::max<uint32_t>(1, std::min<uint32_t>(per_cu / lanes, 16)));
   } else {
-    groups = pow2floor(std::min<uint32_t>(per_cu, 16));
+    // one lane per wave: as many waves as LDS allows, up to the 16 the
+    // register budget keeps resident; a power of two unless the caller
+    // (a merged class, persistent lanes drawing from one queue) takes any
+    groups = std::min<uint32_t>(per_cu, 16);
+    if (!any_groups) groups = pow2floor(groups);
   }
   const uint32_t over = o.lanes_per_group;
   if (over > 0 && over <= 64 && over * stride * 2 <= lds_per_cu) {
@@ -859,52 +864,82 @@ static SRes plan_batch(LzmaGpuStreamDesc* descs, size_t n, uint32_t* order, Lzma
     if (wa != wb) return wa > wb;
     return w[a] > w[b];
   };
+  // One class per width bucket: the throughput placement first; a class that
+  // lands in the latency regime is re-planned with the latency placement (more
+  // tables in LDS, few streams per CU); few streams per CU go cooperative.
+  auto plan_bucket = [&](const std::vector<uint32_t>& idx, uint32_t stride_lo,
+                         bool any_groups) -> LzmaGpuLdsClass {
+    bool lat = false;
+    const int regime = o.kernel == LZMA_GPU_KERNEL_THROUGHPUT ? 1 : 0;
+    LzmaGpuLdsClass c = plan_lds_class(stride_lo, idx.size(), LZGPU_LDS_MASK, cus, regime, o,
+                                       &lat);
+    const bool want_lat = o.kernel == LZMA_GPU_KERNEL_LATENCY || o.kernel == LZMA_GPU_KERNEL_COOP ||
+                          (o.kernel == LZMA_GPU_KERNEL_AUTO && lat);
+    if (!want_lat) return c;
+    uint32_t stride_lat = 0;
+    for (uint32_t i : idx) stride_lat = std::max(stride_lat, w_lat[i]);
+    if (stride_lat > kMaxLdsCells) return c;
+    c = plan_lds_class(stride_lat, idx.size(), LZGPU_LDS_MASK_LAT, cus,
+                       o.kernel == LZMA_GPU_KERNEL_AUTO ? 0 : 2, o, nullptr, any_groups);
+    // few streams per CU: the wave-cooperative kernel (all 32 lanes on one
+    // stream, literal trees decided by lane speculation) -- config 4
+    // 1.71 -> 2.85 GB/s and the xz leg 1.45 -> 2.36 at 4 streams per CU;
+    // at 16 per CU (config 2) the single-lane waves are faster (5.9 vs 5.2)
+    const uint64_t per_cu_batch = (idx.size() + cus - 1) / cus;
+    const bool coop = o.kernel == LZMA_GPU_KERNEL_COOP ||
+                      (o.kernel == LZMA_GPU_KERNEL_AUTO &&
+                       (o.coop == 1 || (o.coop == 0 && per_cu_batch <= 8)));
+    if (c.lanes_per_group == 1 && coop) {
+      c.lds_mask = LZGPU_LDS_MASK_LAT | lzgpu::kCoopBit;
+      if (!(o.flags & LZMA_GPU_PLAN_COOP_LAT)) {
+        // the whole table in LDS if it still fits the streams per CU the
+        // latency plan gives this class: no global round trip left in the
+        // match path (SpecPos, LenHigh) or the matched literal
+        uint32_t stride_all = 0;
+        for (uint32_t i : idx) stride_all = std::max(stride_all, all_cells(descs[i]));
+        if (stride_all != 0 && stride_all <= kMaxLdsCells) {
+          LzmaGpuLdsClass ca = plan_lds_class(stride_all, idx.size(),
+                                              LZGPU_LDS_MASK_ALL | lzgpu::kCoopBit, cus, 2, o);
+          const uint64_t want = std::min<uint64_t>(per_cu_batch, c.groups_per_cu);
+          if (ca.lanes_per_group == 1 && ca.groups_per_cu >= want) c = ca;
+        }
+      }
+    }
+    return c;
+  };
+  // Several buckets in the one-lane latency regime (mixed-props batches,
+  // config 5) become one class: its lanes draw from one queue in one launch,
+  // so the batch has one tail instead of one per class, and its workgroup
+  // count per CU is what the widest slice allows (up to 16, any number: the
+  // queue balances the SIMDs) -- config 5 4.6-4.8 -> 4.9 GB/s, and steadier
+  // (profiles/r02_ab/cfg5_merge_lat_ab.log).  LZMA_GPU_PLAN_NO_MERGE_LAT keeps
+  // one class per bucket.
+  int merged = -1;  // the bucket holding the merged latency class
+  if (!one_class && !(o.flags & LZMA_GPU_PLAN_NO_MERGE_LAT)) {
+    int lat_b[LZMA_GPU_MAX_CLASSES], n_lat = 0;
+    for (int b = 0; b < LZMA_GPU_MAX_CLASSES; ++b) {
+      if (bucket_idx[b].empty()) continue;
+      const LzmaGpuLdsClass c = plan_bucket(bucket_idx[b], bucket_stride[b], false);
+      if (c.lds_mask == LZGPU_LDS_MASK_LAT && c.lanes_per_group == 1) lat_b[n_lat++] = b;
+    }
+    if (n_lat >= 2) {
+      const int t = lat_b[0];
+      for (int j = 1; j < n_lat; ++j) {
+        const int b = lat_b[j];
+        bucket_idx[t].insert(bucket_idx[t].end(), bucket_idx[b].begin(), bucket_idx[b].end());
+        bucket_stride[t] = std::max(bucket_stride[t], bucket_stride[b]);
+        bucket_idx[b].clear();
+      }
+      merged = t;
+    }
+  }
   size_t k = 0;
   uint64_t best = 0;
   for (int b = 0; b < LZMA_GPU_MAX_CLASSES; ++b) {
     if (bucket_idx[b].empty()) continue;
     std::stable_sort(bucket_idx[b].begin(), bucket_idx[b].end(), by_len);
     for (uint32_t i : bucket_idx[b]) order[k++] = i;
-    // throughput placement first; a class that lands in the latency regime is
-    // re-planned with the latency placement (more tables in LDS, few streams)
-    bool lat = false;
-    const int regime = o.kernel == LZMA_GPU_KERNEL_THROUGHPUT ? 1 : 0;
-    LzmaGpuLdsClass c = plan_lds_class(bucket_stride[b], bucket_idx[b].size(), LZGPU_LDS_MASK,
-                                       cus, regime, o, &lat);
-    const bool want_lat = o.kernel == LZMA_GPU_KERNEL_LATENCY || o.kernel == LZMA_GPU_KERNEL_COOP ||
-                          (o.kernel == LZMA_GPU_KERNEL_AUTO && lat);
-    if (want_lat) {
-      uint32_t stride_lat = 0;
-      for (uint32_t i : bucket_idx[b]) stride_lat = std::max(stride_lat, w_lat[i]);
-      if (stride_lat <= kMaxLdsCells) {
-        c = plan_lds_class(stride_lat, bucket_idx[b].size(), LZGPU_LDS_MASK_LAT, cus,
-                           o.kernel == LZMA_GPU_KERNEL_AUTO ? 0 : 2, o);
-        // few streams per CU: the wave-cooperative kernel (all 32 lanes on one
-        // stream, literal trees decided by lane speculation) -- config 4
-        // 1.71 -> 2.85 GB/s and the xz leg 1.45 -> 2.36 at 4 streams per CU;
-        // at 16 per CU (config 2) the single-lane waves are faster (5.9 vs 5.2)
-        const uint64_t per_cu_batch = (bucket_idx[b].size() + cus - 1) / cus;
-        const bool coop = o.kernel == LZMA_GPU_KERNEL_COOP ||
-                          (o.kernel == LZMA_GPU_KERNEL_AUTO &&
-                           (o.coop == 1 || (o.coop == 0 && per_cu_batch <= 8)));
-        if (c.lanes_per_group == 1 && coop) {
-          c.lds_mask = LZGPU_LDS_MASK_LAT | lzgpu::kCoopBit;
-          if (!(o.flags & LZMA_GPU_PLAN_COOP_LAT)) {
-            // the whole table in LDS if it still fits the streams per CU the
-            // latency plan gives this class: no global round trip left in the
-            // match path (SpecPos, LenHigh) or the matched literal
-            uint32_t stride_all = 0;
-            for (uint32_t i : bucket_idx[b]) stride_all = std::max(stride_all, all_cells(descs[i]));
-            if (stride_all != 0 && stride_all <= kMaxLdsCells) {
-              LzmaGpuLdsClass ca = plan_lds_class(stride_all, bucket_idx[b].size(),
-                                                  LZGPU_LDS_MASK_ALL | lzgpu::kCoopBit, cus, 2, o);
-              const uint64_t want = std::min<uint64_t>(per_cu_batch, c.groups_per_cu);
-              if (ca.lanes_per_group == 1 && ca.groups_per_cu >= want) c = ca;
-            }
-          }
-        }
-      }
-    }
+    LzmaGpuLdsClass c = plan_bucket(bucket_idx[b], bucket_stride[b], b == merged);
     if (o.flags & LZMA_GPU_PLAN_KERNEL_LZMA2) c.flags |= LZMA_GPU_CLASS_HAS_LZMA2;
     for (uint32_t i : bucket_idx[b])
       if (descs[i].kind == LZMA_GPU_KIND_LZMA2) {

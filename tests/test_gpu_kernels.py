@@ -387,20 +387,27 @@ def test_cfg5_full_count_mixed_props(L, torch):
                                dst_cap=int(nout[i]), props=parts[i][2], finish=int(fin[i]))
                           for i in range(count)])
     comp = np.frombuffer(b"".join(p[1] for p in parts), dtype=np.uint8)
-    plan, res, d_dst = _device_decode(L, torch, descs, comp, int(nout.sum()))
-    # four width classes, all in the latency regime (<= 8K streams per class)
-    masks = sorted(plan.classes[k].lds_mask for k in range(plan.n_classes))
-    assert plan.n_classes == 4 and plan.n_lds == count and set(masks) == {M_LAT}, masks
-    # FINISH_END reads the end mark (FINISHED_WITH_MARK); FINISH_ANY stops at
-    # destLen in front of it (NOT_FINISHED)
-    want_status = np.where(fin == 1, 1, 2)
-    assert (res["res"] == 0).all() and (res["status"] == want_status).all()
-    assert (res["dest_len"] == nout).all()
-    assert (res["src_len"][fin == 1] == lens[fin == 1]).all()
-    assert (res["src_len"][fin == 0] < lens[fin == 0]).all()
-    out = d_dst[:int(nout.sum())].cpu().numpy().tobytes()
     plain = b"".join(p[0] for p in parts)
-    assert out == plain
+    # the planner's default: the four width buckets all land in the one-lane
+    # latency regime and are merged into one class (one launch, 15 workgroups
+    # per CU for the widest slice); LZMA_GPU_PLAN_NO_MERGE_LAT: four classes
+    # launched concurrently on forked streams
+    for opts, n_classes in ((None, 1), (L.plan_options("auto", flags=8), 4)):
+        plan, res, d_dst = _device_decode(L, torch, descs, comp, int(nout.sum()), opts)
+        masks = sorted(plan.classes[k].lds_mask for k in range(plan.n_classes))
+        assert plan.n_classes == n_classes and plan.n_lds == count and set(masks) == {M_LAT}, \
+            masks
+        if n_classes == 1:
+            assert plan.classes[0].groups_per_cu == 15 and plan.classes[0].lanes_per_group == 1
+        # FINISH_END reads the end mark (FINISHED_WITH_MARK); FINISH_ANY stops
+        # at destLen in front of it (NOT_FINISHED)
+        want_status = np.where(fin == 1, 1, 2)
+        assert (res["res"] == 0).all() and (res["status"] == want_status).all()
+        assert (res["dest_len"] == nout).all()
+        assert (res["src_len"][fin == 1] == lens[fin == 1]).all()
+        assert (res["src_len"][fin == 0] < lens[fin == 0]).all()
+        out = d_dst[:int(nout.sum())].cpu().numpy().tobytes()
+        assert out == plain
 
 
 def test_cfg4_1024_lzma2_blocks_coop_kernel(L, torch):
