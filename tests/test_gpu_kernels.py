@@ -38,7 +38,9 @@ RES_DT = np.dtype([("res", "<i4"), ("status", "<i4"), ("dest_len", "<u8"), ("src
 # coop: the cooperative kernel, every table section in LDS where the table fits
 # (placement 0x7FF); coop_lat: the same kernel on the latency placement 0x1BF
 # (LZMA_GPU_PLAN_COOP_LAT)
-KERNELS = ("throughput", "latency", "coop", "coop_lat", "global")
+# throughput_np: the throughput kernel without persistent lanes (one stream
+# per lane, the grid covers the batch)
+KERNELS = ("throughput", "throughput_np", "latency", "coop", "coop_lat", "global")
 
 
 @pytest.fixture(scope="module")
@@ -64,7 +66,7 @@ def _check_plan(plan, kernel):
         return
     assert plan.n_lds > 0 and cls
     for c in cls:
-        if kernel == "throughput":
+        if kernel in ("throughput", "throughput_np"):
             assert c.lds_mask == M_THR, hex(c.lds_mask)
         elif kernel == "latency":
             assert c.lds_mask == M_LAT and c.lanes_per_group == 1, hex(c.lds_mask)
@@ -77,10 +79,11 @@ def _check_plan(plan, kernel):
             assert c.lds_mask == M_LAT | COOP, hex(c.lds_mask)
     if kernel == "coop":
         assert any(c.lds_mask == M_ALL | COOP for c in cls)
-    if kernel == "throughput":
+    if kernel in ("throughput", "throughput_np"):
         # wave width follows table width: 32 streams per wave for lc+lp = 0
         # (config 3), 8 for lc+lp = 1, 2 for LZMA2 ranges (lc+lp <= 4 slices)
         assert all(c.lanes_per_group >= 2 for c in cls)
+        assert plan.persistent == (0 if kernel == "throughput_np" else 1)
 
 
 def _opts(L, kernel):
@@ -88,6 +91,8 @@ def _opts(L, kernel):
     # shape (>= 64 streams per CU) is what a real 64K batch gets
     if kernel == "coop_lat":
         return L.plan_options("coop", cus=8, flags=4)
+    if kernel == "throughput_np":
+        return L.plan_options("throughput", cus=8, persistent=2)
     return L.plan_options(kernel, cus=8)
 
 
