@@ -32,7 +32,13 @@
 namespace lzgpu {
 
 constexpr uint32_t kCrcPoly = 0xEDB88320u;
-constexpr uint32_t kCrcChunk = 2048;  // bytes per chunk lane (multiple of 16)
+#ifndef LZGPU_CRC_CHUNK
+#define LZGPU_CRC_CHUNK 2048
+#endif
+#ifndef LZGPU_CRC_UNROLL
+#define LZGPU_CRC_UNROLL 8
+#endif
+constexpr uint32_t kCrcChunk = LZGPU_CRC_CHUNK;  // bytes per chunk lane (multiple of 16)
 
 struct CrcTables {
   uint32_t slice[16][256];  // slice[k][v]: register after byte v then k zero bytes
@@ -136,13 +142,15 @@ __device__ __forceinline__ uint32_t crc_span(uint32_t crc, uintptr_t p, uintptr_
     crc = crc_block_bytes(crc, load16(a), uint32_t(p - a), k1, t);
     a += 16;
   }
-  while (a + 64 <= e) {
-    const u32x4 v0 = load16(a), v1 = load16(a + 16), v2 = load16(a + 32), v3 = load16(a + 48);
-    crc = crc_block16(crc, v0, t);
-    crc = crc_block16(crc, v1, t);
-    crc = crc_block16(crc, v2, t);
-    crc = crc_block16(crc, v3, t);
-    a += 64;
+  // LZGPU_CRC_UNROLL aligned 16-byte loads in flight per lane
+  constexpr uint32_t U = LZGPU_CRC_UNROLL;
+  while (a + 16 * U <= e) {
+    u32x4 v[U];
+#pragma unroll
+    for (uint32_t k = 0; k < U; ++k) v[k] = load16(a + 16 * k);
+#pragma unroll
+    for (uint32_t k = 0; k < U; ++k) crc = crc_block16(crc, v[k], t);
+    a += 16 * U;
   }
   while (a + 16 <= e) {
     crc = crc_block16(crc, load16(a), t);

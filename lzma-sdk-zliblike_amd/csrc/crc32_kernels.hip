@@ -3,7 +3,7 @@
 // Two launches per batch (formulation in crc32_device.h):
 //   lzgpu_crc_chunk_kernel: one lane per kChunk-byte chunk slot, grid-stride;
 //     raw CRC register of the chunk with slice-by-16 tables in LDS.  The loop
-//     reads aligned 16-byte blocks, four in flight per lane; partial blocks at
+//     reads aligned 16-byte blocks, eight in flight per lane; partial blocks at
 //     either end of a chunk are loaded whole (an aligned block holding a valid
 //     byte never crosses a page) and consumed byte-wise from registers.
 //   lzgpu_crc_fold_kernel: one lane per range; folds the chunk registers with

@@ -22,6 +22,9 @@ namespace lzgpu {
 
 constexpr uint64_t kCrc64Poly = 0xC96C5795D7870F42ull;
 constexpr uint32_t kCrc64Chunk = 2048;  // bytes per chunk lane (multiple of 16)
+#ifndef LZGPU_CRC64_UNROLL
+#define LZGPU_CRC64_UNROLL 8
+#endif
 
 struct Crc64Tables {
   uint64_t slice[8][256];  // slice[k][v]: register after byte v then k zero bytes
@@ -115,13 +118,15 @@ __device__ __forceinline__ uint64_t crc64_span(uint64_t crc, uintptr_t p, uintpt
     crc = crc64_block_bytes(crc, load16(a), uint32_t(p - a), k1, t);
     a += 16;
   }
-  while (a + 64 <= e) {
-    const u32x4 v0 = load16(a), v1 = load16(a + 16), v2 = load16(a + 32), v3 = load16(a + 48);
-    crc = crc64_block16(crc, v0, t);
-    crc = crc64_block16(crc, v1, t);
-    crc = crc64_block16(crc, v2, t);
-    crc = crc64_block16(crc, v3, t);
-    a += 64;
+  // LZGPU_CRC64_UNROLL aligned 16-byte loads in flight per lane
+  constexpr uint32_t U = LZGPU_CRC64_UNROLL;
+  while (a + 16 * U <= e) {
+    u32x4 v[U];
+#pragma unroll
+    for (uint32_t k = 0; k < U; ++k) v[k] = load16(a + 16 * k);
+#pragma unroll
+    for (uint32_t k = 0; k < U; ++k) crc = crc64_block16(crc, v[k], t);
+    a += 16 * U;
   }
   while (a + 16 <= e) {
     crc = crc64_block16(crc, load16(a), t);
