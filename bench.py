@@ -1140,49 +1140,67 @@ def measure_e2e(L, torch, plan, d_desc, d_order, d_src, d_dst, d_ws, d_res, comp
 def measure_e2e_pipelined(L, torch, plan, d_desc, d_order, d_ws, d_res, comp, plain, count, n,
                           dev, batches):
     """Serving shape: a stream of batches from pinned host memory, each batch
-    H2D -> decode -> D2H, with batch k+1's H2D and batch k-1's D2H on their own
-    streams (copy engines) while batch k decodes; two device buffer sets.  The
-    steady-state rate is what a service feeding the GPU continuously sees."""
+    H2D -> decode -> D2H, two device buffer sets, the copies on one copy stream
+    and the decode on another.  Enqueue order per step is H2D(b+1), decode(b),
+    D2H(b): the next batch's upload is queued ahead of this batch's download,
+    so it runs while batch b decodes instead of waiting behind a download that
+    waits for that decode (the order H2D(b), decode(b), D2H(b) held every upload
+    behind the previous download: 18-19 ms per batch,
+    profiles/r02_e2e/overlap_timeline.log; look-ahead order
+    profiles/r02_e2e/overlap_ahead.log).  `value` = batches x bytes / wall time
+    including the pipeline's fill and drain; `steady_ms_per_batch` = decode
+    starts of the last and the second batch apart, over the batches between."""
     nb = int(comp.size)
-    h_src = torch.from_numpy(np.ascontiguousarray(comp)).pin_memory()
+    h_src = torch.from_numpy(np.array(comp)).pin_memory()
     h_dst = [torch.empty(count * n, dtype=torch.uint8).pin_memory() for _ in range(2)]
     d_src = [torch.empty(nb + 64, dtype=torch.uint8, device=dev) for _ in range(2)]
     d_dst = [torch.empty(count * n + 64, dtype=torch.uint8, device=dev) for _ in range(2)]
-    s_h2d, s_dec, s_d2h = (torch.cuda.Stream(dev) for _ in range(3))
+    s_copy, s_dec = torch.cuda.Stream(dev), torch.cuda.Stream(dev)
     h2d_done = [torch.cuda.Event() for _ in range(2)]
     dec_done = [torch.cuda.Event() for _ in range(2)]
     d2h_done = [torch.cuda.Event() for _ in range(2)]
+    dec_start = [torch.cuda.Event(enable_timing=True) for _ in range(batches)]
     for e in dec_done + d2h_done:
         e.record(torch.cuda.current_stream(dev))
     torch.cuda.synchronize()
+
+    def upload(b):
+        k = b % 2
+        s_copy.wait_event(dec_done[k])         # d_src[k] free (batch b-2 decoded)
+        with torch.cuda.stream(s_copy):
+            d_src[k][:nb].copy_(h_src, non_blocking=True)
+        h2d_done[k].record(s_copy)
+
     t0 = time.perf_counter()
+    upload(0)
     for b in range(batches):
         k = b % 2
-        s_h2d.wait_event(dec_done[k])          # d_src[k] free (batch b-2 decoded)
-        with torch.cuda.stream(s_h2d):
-            d_src[k][:nb].copy_(h_src, non_blocking=True)
-        h2d_done[k].record(s_h2d)
+        if b + 1 < batches:
+            upload(b + 1)
         s_dec.wait_event(h2d_done[k])
         s_dec.wait_event(d2h_done[k])          # d_dst[k] free (batch b-2 copied out)
+        dec_start[b].record(s_dec)
         if L.decode_batch_device_ex(plan, d_desc.data_ptr(), d_order.data_ptr(),
                                     d_src[k].data_ptr(), d_dst[k].data_ptr(), d_ws.data_ptr(),
                                     d_res.data_ptr(), s_dec.cuda_stream):
             raise RuntimeError(L.last_error())
         dec_done[k].record(s_dec)
-        s_d2h.wait_event(dec_done[k])
-        with torch.cuda.stream(s_d2h):
+        s_copy.wait_event(dec_done[k])
+        with torch.cuda.stream(s_copy):
             h_dst[k].copy_(d_dst[k][:count * n], non_blocking=True)
-        d2h_done[k].record(s_d2h)
+        d2h_done[k].record(s_copy)
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
-    ok = bool(np.array_equal(h_dst[(batches - 1) % 2].numpy(), plain))
+    ok = all(bool(np.array_equal(h.numpy(), plain)) for h in h_dst)
+    steady = dec_start[1].elapsed_time(dec_start[batches - 1]) / (batches - 2)
     return {"value": round(batches * count * n / wall / 1e6, 2), "unit": "MB/s",
             "batches": batches, "ms_per_batch": round(wall / batches * 1e3, 4),
+            "steady_ms_per_batch": round(steady, 4),
+            "steady_MBps": round(count * n / (steady * 1e-3) / 1e6, 2),
             "verified": ok,
-            "note": "H2D / decode / D2H of consecutive batches on three streams, two device "
-                    "buffer sets; an H2D overlapping a running decode is starved (12-16 ms "
-                    "instead of 2, profiles/r02_e2e/overlap_timeline.log), so this is no "
-                    "faster than the serial path"}
+            "note": "H2D(b+1) / decode(b) / D2H(b) from pinned host memory: one copy stream, "
+                    "one decode stream, two device buffer sets; the copies of one batch "
+                    "(H2D + D2H) hide under the next batch's decode"}
 
 
 def run_secondary(cfgs, steps=5, warmup=1, timeout=420):
@@ -1371,7 +1389,7 @@ def main():
         e2e = measure_e2e(L, torch, plan, d_desc, d_order, d_src, d_dst, d_ws, d_res, comp, count,
                           n, stream, min(args.steps, 5))
         e2e["pipelined"] = measure_e2e_pipelined(L, torch, plan, d_desc, d_order, d_ws, d_res,
-                                                 comp, plain, count, n, dev, 8)
+                                                 comp, plain, count, n, dev, 12)
         ok = D.all_true(ok and e2e["pipelined"]["verified"], dev)
 
     total_streams = int(D.reduce_sum(float(count), dev))
