@@ -222,7 +222,7 @@ size_t LzmaGpu_PlanBatch(LzmaGpuStreamDesc *descs, size_t n, uint32_t *order);
  * LZGPU_LANES=<streams per workgroup>, LZGPU_GROUPS=<workgroups per CU>,
  * LZGPU_OCC=<1|2|4 waves per SIMD>, LZGPU_CUS, LZGPU_COOP=0|1,
  * LZGPU_PERSIST=0 (one stream per lane), LZGPU_CLASSES=1 (one LDS launch),
- * LZGPU_SLICE_ALIGN8=1, LZGPU_KERNEL_LZMA2=1, LZGPU_COOP_LAT=1, LZGPU_MERGE_LAT=0 (the
+ * LZGPU_SLICE_ALIGN8=1, LZGPU_KERNEL_LZMA2=1, LZGPU_COOP_LAT=1, LZGPU_MERGE_LAT=0, LZGPU_ILV=0 (the
  * LZMA_GPU_PLAN_* flags below); DecodeBatchEx reads LZGPU_CLASS_STREAMS=0
  * (classes launched one after another on the caller's stream).
  * workspace_bytes includes the LDS launches' work counters at queue_offset
@@ -239,6 +239,14 @@ typedef struct LzmaGpuLdsClass {
   uint32_t waves_per_simd;
   uint32_t lds_mask;      /* which probability sections live in LDS */
   uint32_t flags;         /* LZMA_GPU_CLASS_*: set by the planner */
+  /* lane-interleaved global sections (lds_mask bit 30; the throughput
+   * placement's default, LZMA_GPU_PLAN_NO_ILV turns it off): the class's slot
+   * area in the workspace, in 16-bit cells -- slot_groups workgroups, each lane
+   * group of 32 owning slot_cells rows of 32 cells; its streams get no
+   * per-stream slice (probs_off 0) */
+  uint64_t slot_off;
+  uint32_t slot_cells;
+  uint32_t slot_groups;
 } LzmaGpuLdsClass;
 /* the class holds LZMA2 items: launched on the kernel build with the LZMA2 chunk
  * walker (without it the LZMA-only build runs, fewer registers) */
@@ -303,6 +311,11 @@ typedef struct LzmaGpuPlanOptions {
 /* one class per table-width bucket even when several land in the one-lane
  * latency regime (default: those are merged into one class, one launch) */
 #define LZMA_GPU_PLAN_NO_MERGE_LAT 8u
+/* throughput classes keep the probability sections that are not in LDS in
+ * per-stream slices (the round-2 layout) instead of lane-interleaved -- cell i
+ * of the 32 lanes of a lane group side by side -- in a slot area per class
+ * (LZGPU_ILV=0) */
+#define LZMA_GPU_PLAN_NO_ILV 16u
 
 /* LzmaGpu_PlanBatchEx with explicit options (opt == NULL: as PlanBatchEx,
  * whose defaults take the LZGPU_* experiment variables of the environment,

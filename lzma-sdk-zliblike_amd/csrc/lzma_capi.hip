@@ -640,13 +640,20 @@ SRes Lzma2Decode(Byte* dest, SizeT* destLen, const Byte* src, SizeT* srcLen, Byt
 // Workspace: each item gets a 16-byte aligned slice of table_cells() cells
 // (LZMA2 ranges: the lc+lp=4, pb=4 maximum).  Returns per-item lo-table
 // widths (0 = not LDS-eligible) through lo_w when given.
+// `skip` (optional): items whose global sections live in a class slot area
+// (lane-interleaved throughput classes) get no slice (probs_off 0, unused).
 static uint64_t plan_workspace(LzmaGpuStreamDesc* descs, size_t n, std::vector<uint32_t>* lo_w,
-                               std::vector<uint32_t>* lat_w = nullptr) {
+                               std::vector<uint32_t>* lat_w = nullptr,
+                               const std::vector<uint8_t>* skip = nullptr) {
   uint64_t off = 0;
   if (lo_w) lo_w->assign(n, 0);
   if (lat_w) lat_w->assign(n, 0);
   for (size_t i = 0; i < n; ++i) {
     LzmaGpuStreamDesc& d = descs[i];
+    if (skip && (*skip)[i]) {
+      d.probs_off = 0;
+      continue;
+    }
     uint32_t np = 0;
     if (d.kind == LZMA_GPU_KIND_LZMA2) {
       np = lzgpu::table_cells(4, 0, 4);
@@ -704,7 +711,7 @@ static uint32_t device_cus() {
 // call time (LZGPU_KERNEL=global|throughput|latency|coop, LZGPU_MASK=1|2,
 // LZGPU_COOP=0|1, LZGPU_CUS, LZGPU_LANES, LZGPU_GROUPS, LZGPU_OCC,
 // LZGPU_PERSIST=0, LZGPU_CLASSES=1, LZGPU_SLICE_ALIGN8=1, LZGPU_KERNEL_LZMA2=1,
-// LZGPU_COOP_LAT=1, LZGPU_MERGE_LAT=0).  Only LzmaGpu_PlanBatchEx reads them;
+// LZGPU_COOP_LAT=1, LZGPU_MERGE_LAT=0, LZGPU_ILV=0).  Only LzmaGpu_PlanBatchEx reads them;
 // LzmaGpu_PlanBatchOpt takes its options from the caller alone.
 static LzmaGpuPlanOptions env_options() {
   LzmaGpuPlanOptions o;
@@ -733,7 +740,8 @@ static LzmaGpuPlanOptions env_options() {
   o.flags = (env_int("LZGPU_SLICE_ALIGN8", 0) ? LZMA_GPU_PLAN_SLICE_ALIGN8 : 0u) |
             (env_int("LZGPU_KERNEL_LZMA2", 0) ? LZMA_GPU_PLAN_KERNEL_LZMA2 : 0u) |
             (env_int("LZGPU_COOP_LAT", 0) ? LZMA_GPU_PLAN_COOP_LAT : 0u) |
-            (env_int("LZGPU_MERGE_LAT", 1) ? 0u : LZMA_GPU_PLAN_NO_MERGE_LAT);
+            (env_int("LZGPU_MERGE_LAT", 1) ? 0u : LZMA_GPU_PLAN_NO_MERGE_LAT) |
+            (env_int("LZGPU_ILV", 1) ? 0u : LZMA_GPU_PLAN_NO_ILV);
   return o;
 }
 
@@ -935,6 +943,8 @@ static SRes plan_batch(LzmaGpuStreamDesc* descs, size_t n, uint32_t* order, Lzma
   }
   size_t k = 0;
   uint64_t best = 0;
+  std::vector<uint8_t> in_slots;  // items of lane-interleaved classes
+  uint64_t slot_total[LZMA_GPU_MAX_CLASSES] = {0, 0, 0, 0};
   for (int b = 0; b < LZMA_GPU_MAX_CLASSES; ++b) {
     if (bucket_idx[b].empty()) continue;
     std::stable_sort(bucket_idx[b].begin(), bucket_idx[b].end(), by_len);
@@ -946,6 +956,31 @@ static SRes plan_batch(LzmaGpuStreamDesc* descs, size_t n, uint32_t* order, Lzma
         c.flags |= LZMA_GPU_CLASS_HAS_LZMA2;
         break;
       }
+    if (!(o.flags & LZMA_GPU_PLAN_NO_ILV) && c.lds_mask == LZGPU_LDS_MASK &&
+        c.lanes_per_group <= 64) {
+      // lane-interleaved global sections: one column per resident lane (the
+      // lanes keep it across the streams they take from the queue); config 3
+      // 28.1 -> 29.9 GB/s (profiles/r02_ilv/ilv_ab.log)
+      uint32_t rows = 0;
+      for (uint32_t i : bucket_idx[b]) {
+        const LzmaGpuStreamDesc& d = descs[i];
+        uint32_t lc = 4, lp = 0, pb = 4, dict;
+        if (d.kind != LZMA_GPU_KIND_LZMA2 &&
+            lzgpu::lz_props_parse(d.props, d.props_size, lc, lp, pb, dict) != SZ_OK)
+          continue;
+        rows = std::max(rows, lzgpu::make_layout(lc, lp, pb, LZGPU_LDS_MASK).glb_cells);
+      }
+      const uint64_t grid = (c.n + c.lanes_per_group - 1) / c.lanes_per_group;
+      const uint64_t groups =
+          o.persistent == 2 ? grid : std::min<uint64_t>(grid, uint64_t(cus) * c.groups_per_cu);
+      const uint64_t lane_groups = (c.lanes_per_group + lzgpu::kIlv - 1) / lzgpu::kIlv;
+      c.slot_cells = std::max<uint32_t>(rows, 1);
+      c.slot_groups = uint32_t(groups);
+      slot_total[plan->n_classes] = groups * lane_groups * lzgpu::kIlv * c.slot_cells;
+      c.lds_mask |= lzgpu::kIlvBit;
+      if (in_slots.empty()) in_slots.assign(n, 0);
+      for (uint32_t i : bucket_idx[b]) in_slots[i] = 1;
+    }
     plan->classes[plan->n_classes++] = c;
     plan->n_lds += c.n;
     if (c.n > best) {
@@ -959,7 +994,17 @@ static SRes plan_batch(LzmaGpuStreamDesc* descs, size_t n, uint32_t* order, Lzma
   std::stable_sort(glob_idx.begin(), glob_idx.end(), by_len);
   for (uint32_t i : glob_idx) order[k++] = i;
   plan->persistent = o.persistent == 2 ? 0u : 1u;
-  // the LDS launches' work counters, after the probability slices
+  // per-stream slices only for items outside the slot areas, then the slot
+  // areas (128-byte aligned), then the LDS launches' work counters
+  uint64_t ws_cells = plan->workspace_bytes / 2;
+  if (!in_slots.empty()) ws_cells = plan_workspace(descs, n, nullptr, nullptr, &in_slots) / 2;
+  for (uint32_t c = 0; c < plan->n_classes; ++c) {
+    if (!slot_total[c]) continue;
+    ws_cells = (ws_cells + 63) & ~uint64_t(63);
+    plan->classes[c].slot_off = ws_cells;
+    ws_cells += slot_total[c];
+  }
+  plan->workspace_bytes = ws_cells * 2;
   plan->queue_offset = (plan->workspace_bytes + 63) & ~uint64_t(63);
   plan->workspace_bytes = plan->queue_offset + 64 * LZMA_GPU_MAX_CLASSES;
   return SZ_OK;
@@ -1050,7 +1095,8 @@ SRes LzmaGpu_DecodeBatchEx(const LzmaGpuPlan* plan, const LzmaGpuStreamDesc* d_d
     if (lzgpu_launch_decode_lds(d_descs, d_order + first, uint32_t(c.n), d_src, d_dst, ws,
                                 d_results, c.lanes_per_group, c.lds_cells_per_lane,
                                 c.waves_per_simd, c.groups_per_cu, max_groups, queue, c.lds_mask,
-                                c.flags, sk) != 0) {
+                                c.flags, LzgpuSlots{c.slot_off, c.slot_cells, c.slot_groups},
+                                sk) != 0) {
       set_error("LDS decode kernel launch failed");
       return SZ_ERROR_FAIL;
     }
@@ -1209,7 +1255,7 @@ size_t Lzma2Gpu_SplitBlocks(const Byte* src, size_t src_len, uint64_t* src_off,
 // ------------------------------------------------------------------ streaming sessions
 
 static_assert(sizeof(LzmaGpuSession) == 192, "LzmaGpuSession layout");
-static_assert(sizeof(LzmaGpuPlan) == 184, "LzmaGpuPlan layout");
+static_assert(sizeof(LzmaGpuPlan) == 248, "LzmaGpuPlan layout");
 
 size_t LzmaGpu_SessionProbsBytes(const Byte* props, unsigned propsSize) {
   CLzmaProps pr;

@@ -158,6 +158,22 @@ typedef __attribute__((address_space(1))) uint16_t gu16;
 typedef __attribute__((address_space(1))) uint32_t gu32;
 #endif
 
+// Lane-interleaved global tables (placement bit kIlvBit, throughput kernel):
+// the global sections of the 32 lanes of a lane group are stored cell-major --
+// cell i of lane l at column l of row i (row = kIlv cells) -- so that lanes
+// reading the same cell (choice bits, tree tops, IsRep0Long of one state) hit
+// one 64-byte span instead of one line each, and a wave's frequently used
+// cells share a few lines that stay cached.  GS is the lane's view: a pointer
+// to its column with cell arithmetic scaled by the row length.
+constexpr uint32_t kIlvBit = 0x40000000u;
+constexpr uint32_t kIlv = 32u;
+struct GS {
+  gu16* p;
+  __device__ __forceinline__ GS operator+(uint32_t k) const { return GS{p + kIlv * k}; }
+  __device__ __forceinline__ gu16& operator[](uint32_t k) const { return p[kIlv * k]; }
+  __device__ __forceinline__ gu16& operator*() const { return *p; }
+};
+
 // Build-time code-shape switches (A/B'd on MI355X):
 //   LZGPU_NORM_BRANCHLESS  NORMALIZE as selects instead of a skip-able branch
 //   LZGPU_BIT_MASK         decision/update: 0 if/else, 1 mask arithmetic, 2 selects
@@ -325,12 +341,19 @@ struct Tab {
   Layout L;
   __device__ __forceinline__ Tab(const LzStateT<Lo>& s)
       : lo(s.lo), gl(s.gl), L(make_layout(s.lc, s.lp, s.pb, M)) {}
+  // cell `off` of the global table (lane-interleaved under kIlvBit)
+  __device__ __forceinline__ auto g(uint32_t off) const {
+    if constexpr ((M & kIlvBit) != 0u)
+      return GS{gl + kIlv * off};
+    else
+      return gl + off;
+  }
   template <uint32_t S>
   __device__ __forceinline__ auto at(uint32_t i) const {
     if constexpr (((M >> S) & 1u) != 0u)
       return lo + (L.o[S] + i);
     else
-      return gl + (L.o[S] + i);
+      return g(L.o[S] + i);
   }
 };
 
@@ -612,6 +635,10 @@ struct BulkReaderFor {
 #if LZGPU_READER_Q
 template <>
 struct BulkReaderFor<LZGPU_LDS_MASK> {
+  typedef GlobalReaderQ type;
+};
+template <>
+struct BulkReaderFor<LZGPU_LDS_MASK | kIlvBit> {
   typedef GlobalReaderQ type;
 };
 #endif
@@ -1307,7 +1334,7 @@ __device__ __forceinline__ uint32_t lit_bit(Rc<Rd>& rc, const Tab<M, Lo>& T, uin
     if constexpr (p_lds)
       return rc.bit(T.lo + (rel + sym));
     else
-      return rc.bit(T.gl + (rel + sym));
+      return rc.bit(T.g(rel + sym));
   } else {
     if (offs_mbit) return rc.bit(T.template at<S_LITM>((ctx << 9) + offs_mbit - 0x100u + sym));
     return rc.bit(T.template at<S_LITP>((ctx << 8) + sym));
@@ -1722,12 +1749,12 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
       static_assert(((M >> S_LEN) & 1u) == ((M >> S_REPLEN) & 1u), "Len/RepLen placement");
       constexpr bool len_lds = ((M >> S_LEN) & 1u) != 0u;
       auto lbase = [&]() {
-        if constexpr (len_lds) return T.lo + lsec_o; else return T.gl + lsec_o;
+        if constexpr (len_lds) return T.lo + lsec_o; else return T.g(lsec_o);
       }();
       if constexpr (!len_lds && LZGPU_TREE_GPF) {
         // global length coder: the choice bits and the low tree load together,
         // the mid tree only behind choice = 1
-        if constexpr (LZGPU_MATCH_FAT && M != LZGPU_LDS_MASK) {
+        if constexpr (LZGPU_MATCH_FAT && (M & ~kIlvBit) != LZGPU_LDS_MASK) {
         // choice, choice2 and both 3-level trees of this posState in ONE load
         // batch; only lengths >= 18 go back to memory (LenHigh, 3 batches)
         auto lo_t = lbase + 2 + (ps << 3);
@@ -1802,7 +1829,7 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
               mask = 8;
               nbits -= 3;
             }
-            if constexpr (LZGPU_MATCH_FAT && M != LZGPU_LDS_MASK) if (nbits == 2) {
+            if constexpr (LZGPU_MATCH_FAT && (M & ~kIlvBit) != LZGPU_LDS_MASK) if (nbits == 2) {
               // the last two bits in one batch as well
               const uint32_t n2 = rc.sub2(T.template at<S_SPEC>(sp), node);
               dist |= (((n2 >> 1) & 1u) ? mask : 0u) | ((n2 & 1u) ? (mask << 1) : 0u);
@@ -1822,7 +1849,7 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
           dist <<= 4;
           uint32_t node = 1;
           if constexpr (((M >> S_ALIGN) & 1u) == 0u && LZGPU_TREE_GPF) {
-            if constexpr (LZGPU_MATCH_FAT && M != LZGPU_LDS_MASK) {
+            if constexpr (LZGPU_MATCH_FAT && (M & ~kIlvBit) != LZGPU_LDS_MASK) {
               // all four reverse bits from one batch of the 15 cells
               node = rc.sub4(T.template at<S_ALIGN>(0), 1);
               dist |= ((node >> 3) & 1u) | (((node >> 2) & 1u) << 1) |
@@ -2044,7 +2071,7 @@ __device__ int lz_probe(const LzStateT<Lo>& s, BP in, uint64_t n) {
     }
     const uint32_t lo_off = is_rep ? T.L.o[S_REPLEN] : T.L.o[S_LEN];
     auto lbase = [&]() {
-      if constexpr (((M >> S_LEN) & 1u) != 0u) return T.lo + lo_off; else return T.gl + lo_off;
+      if constexpr (((M >> S_LEN) & 1u) != 0u) return T.lo + lo_off; else return T.g(lo_off);
     }();
     LZ_PB(lbase);
     if (b == 0) {
@@ -2134,7 +2161,13 @@ __device__ __forceinline__ void lz_init_state_real(LzStateT<Lo>& s) {
 #endif
   {
     if constexpr ((M & ~kCoopBit) != 0u) fill_prob_init(s.lo, L.lds_cells);
-    fill_prob_init(s.gl, L.glb_cells);
+    if constexpr ((M & kIlvBit) != 0u) {
+      // the lane's column: one cell per row (the lanes of a group that start
+      // together store whole 64-byte rows)
+      for (uint32_t i = 0; i < L.glb_cells; ++i) s.gl[kIlv * i] = uint16_t(kProbInit);
+    } else {
+      fill_prob_init(s.gl, L.glb_cells);
+    }
   }
   s.rep0 = s.rep1 = s.rep2 = s.rep3 = 1;
   s.st = 0;

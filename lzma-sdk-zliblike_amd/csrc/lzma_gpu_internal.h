@@ -11,13 +11,22 @@ extern "C" int lzgpu_launch_decode_batch(const LzmaGpuStreamDesc* d_descs, const
                                          uint16_t* d_ws, LzmaGpuResult* d_results,
                                          hipStream_t stream);
 extern "C" int lzgpu_launch_session(LzgpuSession* d_sess, uint32_t n, hipStream_t stream);
+// Slot area of a lane-interleaved class (LZMA_GPU_PLAN_ILV): `off` cells into
+// the workspace, `cells` rows of kIlv cells per lane group, room for `groups`
+// workgroups.
+struct LzgpuSlots {
+  uint64_t off;
+  uint32_t cells;
+  uint32_t groups;
+};
 extern "C" int lzgpu_launch_decode_lds(const LzmaGpuStreamDesc* d_descs, const uint32_t* d_order,
                                        uint32_t n, const uint8_t* d_src, uint8_t* d_dst,
                                        uint16_t* d_ws, LzmaGpuResult* d_results, uint32_t lanes,
                                        uint32_t stride, uint32_t waves_per_simd,
                                        uint32_t groups_per_cu, uint32_t max_groups,
                                        uint32_t* d_queue, uint32_t lds_mask,
-                                       uint32_t class_flags, hipStream_t stream);
+                                       uint32_t class_flags, LzgpuSlots slots,
+                                       hipStream_t stream);
 extern "C" int lzgpu_launch_crc_arrays(const uint8_t* d_data, const uint64_t* d_off,
                                        const uint64_t* d_len, uint32_t n,
                                        const uint32_t* d_chunk_base,

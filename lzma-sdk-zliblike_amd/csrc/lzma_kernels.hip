@@ -42,19 +42,32 @@ __global__ void __launch_bounds__(64) lzgpu_decode_batch_kernel(
 // K2: the build carries the LZMA2 chunk walker (classes with LZMA2 items); the
 // LZMA-only build needs fewer registers (169 vs 202 VGPRs at W = 2, 21 vs 153
 // spilled at W = 4), so classes without LZMA2 items launch it.
+// Lane-interleaved placements (M & kIlvBit): the global sections live in the
+// class's slot area (`slot_off` cells into ws) instead of per-stream slices --
+// lane group g (32 lanes of one workgroup) owns rows of kIlv cells, `slot_cells`
+// rows, and lane l its column l; the lane keeps its column for every stream
+// it takes from the queue.
 template <int W, uint32_t M, bool K2>
 __global__ void __launch_bounds__(64, W) lzgpu_decode_lds_kernel(
     const LzmaGpuStreamDesc* __restrict__ descs, const uint32_t* __restrict__ order, uint32_t n,
     const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, uint16_t* __restrict__ ws,
-    LzmaGpuResult* __restrict__ results, uint32_t stride, uint32_t* __restrict__ queue) {
+    LzmaGpuResult* __restrict__ results, uint32_t stride, uint32_t* __restrict__ queue,
+    uint64_t slot_off, uint32_t slot_cells) {
   extern __shared__ uint32_t lz_smem[];
   lds_u16* lo = (lds_u16*)((uint16_t*)lz_smem) + threadIdx.x * stride;
   const uint32_t lanes_total = gridDim.x * blockDim.x;
   uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x;
+  gu16* gcol = nullptr;
+  if constexpr ((M & kIlvBit) != 0u) {
+    const uint32_t grp = blockIdx.x * ((blockDim.x + kIlv - 1) / kIlv) + threadIdx.x / kIlv;
+    gcol = (gu16*)(ws + slot_off) + uint64_t(grp) * slot_cells * kIlv + (threadIdx.x % kIlv);
+  }
+  (void)slot_off;
+  (void)slot_cells;
   while (idx < n) {
     const uint32_t id = order ? order[idx] : idx;
     const LzmaGpuStreamDesc d = descs[id];
-    results[id] = lane_decode_lds<M, K2>(d, src, dst, ws, lo, stride);
+    results[id] = lane_decode_lds<M, K2>(d, src, dst, ws, lo, stride, gcol);
     idx = lanes_total + atomicAdd(queue, 1u);
   }
 }
@@ -110,7 +123,7 @@ static int launch_lds(const LzmaGpuStreamDesc* d_descs, const uint32_t* d_order,
                       const uint8_t* d_src, uint8_t* d_dst, uint16_t* d_ws,
                       LzmaGpuResult* d_results, uint32_t lanes, uint32_t stride,
                       uint32_t groups_per_cu, uint32_t max_groups, uint32_t* d_queue,
-                      hipStream_t stream) {
+                      const LzgpuSlots& sl, hipStream_t stream) {
   static bool attr_set = false;
   if (!attr_set) {
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(lzgpu_decode_lds_kernel<W, M, K2>),
@@ -127,9 +140,18 @@ static int launch_lds(const LzmaGpuStreamDesc* d_descs, const uint32_t* d_order,
   }
   uint32_t grid = (n + lanes - 1) / lanes;
   if (max_groups && grid > max_groups) grid = max_groups;
+  if constexpr ((M & kIlvBit) != 0u) {
+    // the slot area holds sl.groups workgroups' columns; persistent lanes
+    // cover the rest of the batch from the queue
+    if (sl.groups == 0 || lanes > 64) return -1;
+    if (grid > sl.groups) {
+      if (!max_groups) return -1;
+      grid = sl.groups;
+    }
+  }
   auto kfn = lzgpu_decode_lds_kernel<W, M, K2>;
   hipLaunchKernelGGL(kfn, dim3(grid), dim3(lanes), lds, stream, d_descs,
-                     d_order, n, d_src, d_dst, d_ws, d_results, stride, d_queue);
+                     d_order, n, d_src, d_dst, d_ws, d_results, stride, d_queue, sl.off, sl.cells);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -163,15 +185,15 @@ static int launch_lds_w(const LzmaGpuStreamDesc* d_descs, const uint32_t* d_orde
                         const uint8_t* d_src, uint8_t* d_dst, uint16_t* d_ws,
                         LzmaGpuResult* d_results, uint32_t lanes, uint32_t stride,
                         uint32_t waves_per_simd, uint32_t groups_per_cu, uint32_t max_groups,
-                        uint32_t* d_queue, hipStream_t stream) {
+                        uint32_t* d_queue, const LzgpuSlots& sl, hipStream_t stream) {
   if (waves_per_simd <= 1)
     return launch_lds<1, M, K2>(d_descs, d_order, n, d_src, d_dst, d_ws, d_results, lanes, stride,
-                                groups_per_cu, max_groups, d_queue, stream);
+                                groups_per_cu, max_groups, d_queue, sl, stream);
   if (waves_per_simd == 2)
     return launch_lds<2, M, K2>(d_descs, d_order, n, d_src, d_dst, d_ws, d_results, lanes, stride,
-                                groups_per_cu, max_groups, d_queue, stream);
+                                groups_per_cu, max_groups, d_queue, sl, stream);
   return launch_lds<4, M, K2>(d_descs, d_order, n, d_src, d_dst, d_ws, d_results, lanes, stride,
-                              groups_per_cu, max_groups, d_queue, stream);
+                              groups_per_cu, max_groups, d_queue, sl, stream);
 }
 
 template <bool K2>
@@ -179,11 +201,17 @@ static int launch_class(const LzmaGpuStreamDesc* d_descs, const uint32_t* d_orde
                         const uint8_t* d_src, uint8_t* d_dst, uint16_t* d_ws,
                         LzmaGpuResult* d_results, uint32_t lanes, uint32_t stride,
                         uint32_t waves_per_simd, uint32_t groups_per_cu, uint32_t max_groups,
-                        uint32_t* d_queue, uint32_t lds_mask, hipStream_t stream) {
+                        uint32_t* d_queue, uint32_t lds_mask, const LzgpuSlots& sl,
+                        hipStream_t stream) {
   if (lds_mask == LZGPU_LDS_MASK)
     return launch_lds_w<LZGPU_LDS_MASK, K2>(d_descs, d_order, n, d_src, d_dst, d_ws, d_results,
                                             lanes, stride, waves_per_simd, groups_per_cu,
-                                            max_groups, d_queue, stream);
+                                            max_groups, d_queue, sl, stream);
+  if (lds_mask == (LZGPU_LDS_MASK | kIlvBit))
+    return launch_lds_w<LZGPU_LDS_MASK | kIlvBit, K2>(d_descs, d_order, n, d_src, d_dst, d_ws,
+                                                      d_results, lanes, stride, waves_per_simd,
+                                                      groups_per_cu, max_groups, d_queue, sl,
+                                                      stream);
   if (lds_mask == (LZGPU_LDS_MASK_LAT | kCoopBit)) {
     // one wave per workgroup: register budget by workgroups per SIMD
     constexpr uint32_t MC = LZGPU_LDS_MASK_LAT | kCoopBit;
@@ -206,7 +234,7 @@ static int launch_class(const LzmaGpuStreamDesc* d_descs, const uint32_t* d_orde
   if (lds_mask == LZGPU_LDS_MASK_LAT)
     return launch_lds_w<LZGPU_LDS_MASK_LAT, K2>(d_descs, d_order, n, d_src, d_dst, d_ws,
                                                 d_results, lanes, stride, waves_per_simd,
-                                                groups_per_cu, max_groups, d_queue, stream);
+                                                groups_per_cu, max_groups, d_queue, sl, stream);
   return -1;  // no kernel built for this placement
 }
 
@@ -216,14 +244,16 @@ extern "C" int lzgpu_launch_decode_lds(const LzmaGpuStreamDesc* d_descs, const u
                                        uint32_t stride, uint32_t waves_per_simd,
                                        uint32_t groups_per_cu, uint32_t max_groups,
                                        uint32_t* d_queue, uint32_t lds_mask,
-                                       uint32_t class_flags, hipStream_t stream) {
+                                       uint32_t class_flags, LzgpuSlots slots,
+                                       hipStream_t stream) {
   if (n == 0) return 0;
   if (class_flags & LZMA_GPU_CLASS_HAS_LZMA2)
     return launch_class<true>(d_descs, d_order, n, d_src, d_dst, d_ws, d_results, lanes, stride,
                               waves_per_simd, groups_per_cu, max_groups, d_queue, lds_mask,
-                              stream);
+                              slots, stream);
   return launch_class<false>(d_descs, d_order, n, d_src, d_dst, d_ws, d_results, lanes, stride,
-                             waves_per_simd, groups_per_cu, max_groups, d_queue, lds_mask, stream);
+                             waves_per_simd, groups_per_cu, max_groups, d_queue, lds_mask, slots,
+                             stream);
 }
 
 extern "C" int lzgpu_launch_session(LzgpuSession* d_sess, uint32_t n, hipStream_t stream) {

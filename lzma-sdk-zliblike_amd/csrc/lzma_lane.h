@@ -102,7 +102,15 @@ __device__ __forceinline__ LzmaGpuResult lane_decode_lds(const LzmaGpuStreamDesc
                                                          const uint8_t* __restrict__ src,
                                                          uint8_t* __restrict__ dst,
                                                          uint16_t* __restrict__ ws, lds_u16* lo,
-                                                         uint32_t lo_cap) {
+                                                         uint32_t lo_cap, gu16* gcol = nullptr) {
+  // global sections: the stream's own workspace slice, or under kIlvBit the
+  // lane's column of its group's interleaved slot rows
+  auto gtab = [&]() -> gu16* {
+    if constexpr ((M & kIlvBit) != 0u)
+      return gcol;
+    else
+      return (gu16*)(ws + d.probs_off);
+  };
   LzmaGpuResult r;
   r.status = -1;
   r.dest_len = 0;
@@ -119,7 +127,7 @@ __device__ __forceinline__ LzmaGpuResult lane_decode_lds(const LzmaGpuStreamDesc
       return r;
     }
     Lz2StateT<lds_u16*> p;
-    r.res = lz2_init(p, d.props[0], lo, (gu16*)(ws + d.probs_off), (gbyte*)(dst + d.dst_off),
+    r.res = lz2_init(p, d.props[0], lo, gtab(), (gbyte*)(dst + d.dst_off),
                      d.dst_cap);
     if (r.res != kOk) return r;
     uint64_t sl = d.src_len;
@@ -155,7 +163,7 @@ __device__ __forceinline__ LzmaGpuResult lane_decode_lds(const LzmaGpuStreamDesc
     return r;
   }
   s.lo = lo;
-  s.gl = (gu16*)(ws + d.probs_off);
+  s.gl = gtab();
   s.dic = (gbyte*)(dst + d.dst_off);
   s.cap = d.dst_cap;
   s.pos = 0;

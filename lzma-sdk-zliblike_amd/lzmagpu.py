@@ -76,7 +76,8 @@ class LdsClass(ctypes.Structure):
     _fields_ = [("n", ctypes.c_uint64), ("lanes_per_group", ctypes.c_uint32),
                 ("lds_cells_per_lane", ctypes.c_uint32), ("groups_per_cu", ctypes.c_uint32),
                 ("waves_per_simd", ctypes.c_uint32), ("lds_mask", ctypes.c_uint32),
-                ("flags", ctypes.c_uint32)]
+                ("flags", ctypes.c_uint32), ("slot_off", ctypes.c_uint64),
+                ("slot_cells", ctypes.c_uint32), ("slot_groups", ctypes.c_uint32)]
 
 
 class Plan(ctypes.Structure):
@@ -171,7 +172,7 @@ class SzFile(ctypes.Structure):
 assert ctypes.sizeof(XzBlock) == 104 and ctypes.sizeof(Bcj2Job) == 80
 assert ctypes.sizeof(SzFolder) == 80 and ctypes.sizeof(SzFile) == 48
 assert ctypes.sizeof(StreamDesc) == 48 and ctypes.sizeof(Result) == 24
-assert ctypes.sizeof(Session) == 192 and ctypes.sizeof(Plan) == 184
+assert ctypes.sizeof(Session) == 192 and ctypes.sizeof(Plan) == 248
 assert ctypes.sizeof(PlanOptions) == 40
 assert ctypes.sizeof(CLzmaDec) == 136
 

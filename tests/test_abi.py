@@ -15,6 +15,8 @@ import pytest
 
 import native
 
+ILV = 0x40000000  # placement bit: lane-interleaved global sections (throughput kernel)
+
 ROOT = native.ROOT
 HEADER = os.path.join(ROOT, "include", "lzma_gpu.h")
 LIB = os.path.join(ROOT, "lzma-sdk-zliblike_amd", "lib", "liblzmagpu.so")
@@ -156,7 +158,18 @@ def test_plan_batch_workspace_and_order():
                              props=b"\x00\x00\x10\x00\x00") for i in range(65536)])
     pb_, _ = L.plan_ex(big)
     cb = pb_.classes[0]
-    assert (pb_.n_classes, cb.n, cb.lds_cells_per_lane, cb.lds_mask) == (1, 65536, 318, 0x105)
+    assert (pb_.n_classes, cb.n, cb.lds_cells_per_lane, cb.lds_mask) == \
+        (1, 65536, 318, 0x105 | ILV)
+    # global sections lane-interleaved in the class's slot area: 8 groups x 256
+    # CUs of 32 lanes, one column each of the lc0/pb0 global rows (LitM 0x200,
+    # Len + RepLen 2 x 18, PosSlot 256, SpecPos 114, Align 16, LenHigh 512, IsRep0Long 12)
+    assert (cb.slot_groups, cb.slot_cells) == (2048, 512 + 36 + 256 + 114 + 16 + 512 + 12)
+    assert cb.slot_off % 64 == 0
+    assert pb_.workspace_bytes >= 2 * (cb.slot_off + 2048 * 32 * cb.slot_cells)
+    # every stream of the class draws on the slot area: no per-stream slices
+    assert cb.slot_off == 0
+    ps, _ = L.plan_ex(big, L.plan_options("auto", flags=16))  # LZMA_GPU_PLAN_NO_ILV
+    assert ps.classes[0].lds_mask == 0x105 and ps.classes[0].slot_cells == 0
     assert (cb.lanes_per_group, cb.groups_per_cu, cb.waves_per_simd) == (32, 8, 2)
     assert (cb.lds_cells_per_lane // 2) % 2 == 1  # 159 dwords: 32 lanes, 32 banks
     # LZMA_GPU_PLAN_SLICE_ALIGN8: the round-1 8-byte aligned slices (158 dwords)
@@ -182,7 +195,7 @@ def test_plan_options_force_each_instantiation():
         masks[k] = [p.classes[c].lds_mask for c in range(p.n_classes)]
         lanes = [p.classes[c].lanes_per_group for c in range(p.n_classes)]
         if k == "throughput":
-            assert set(masks[k]) == {0x105} and max(lanes) == 32
+            assert set(masks[k]) == {0x105 | ILV} and max(lanes) == 32
         elif k == "latency":
             assert set(masks[k]) == {0x1BF} and set(lanes) == {1}
         elif k == "coop":
@@ -190,7 +203,7 @@ def test_plan_options_force_each_instantiation():
         elif k == "global":
             assert p.n_lds == 0 and p.n_classes == 0
     # 200 narrow streams over 4 CUs = 50 per CU: latency regime by the planner
-    assert masks["auto"] and 0x105 not in masks["auto"]
+    assert masks["auto"] and 0x105 not in masks["auto"] and 0x105 | ILV not in masks["auto"]
     # more CUs: <= 8 streams per CU, the cooperative kernel
     p, _ = L.plan_ex(descs, L.plan_options("auto", cus=256))
     assert all(p.classes[c].lds_mask & COOP for c in range(p.n_classes))

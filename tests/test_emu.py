@@ -5,6 +5,7 @@ oracle.  Catches logic bugs before a GPU run; the GPU suite
 (test_gpu_parity.py) then checks the same vectors on the device."""
 import ctypes
 import os
+import shutil
 import random
 import subprocess
 import tempfile
@@ -46,6 +47,7 @@ EMU_VARIANTS = {
     "match_thin": "-DLZGPU_MATCH_FAT=0",
     "match_fat_global_len": "-DLZGPU_LDS_MASK_LAT=0x105 -DLZGPU_LDS_MASK=0x107 -DEMU_LAT_MASK",
     "latency_instantiation": "-DEMU_LAT_MASK",
+    "interleaved_global_instantiation": "-DEMU_ILV",
     "coop_instantiation": "-DEMU_COOP",
     "coop_all_lds_instantiation": "-DEMU_COOP_ALL",
     "copy_bytes": "-DLZGPU_COPY_WIDE=0",
@@ -61,10 +63,16 @@ def emu(request):
     # (the GPU suite's test_bra compares against it), the rest never ship
     vdir = os.path.join(tempfile.gettempdir(), "lzgpu_emu_variants")
     os.makedirs(vdir, exist_ok=True)
-    out = EMU_SO if request.param == "default" else os.path.join(
-        vdir, f"liblane_emu_{request.param}.so")
+    # one build per process (pytest-xdist workers would otherwise rebuild a
+    # variant another worker has loaded); the default one is then moved
+    # into the tree atomically
+    out = os.path.join(vdir, f"liblane_emu_{request.param}.{os.getpid()}.so")
     subprocess.run(["make", "-s", "-f", "tests/emu/Makefile", f"EMU_OUT={out}",
                     f"EMU_FLAGS={EMU_VARIANTS[request.param]}"], cwd=native.ROOT, check=True)
+    if request.param == "default":
+        tmp = f"{EMU_SO}.{os.getpid()}"
+        shutil.copyfile(out, tmp)
+        os.replace(tmp, EMU_SO)
     lib = ctypes.CDLL(out)
     lib.emu_decode_batch_lds.restype = None
     lib.emu_decode_batch_lds.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_char_p,

@@ -40,7 +40,13 @@ RES_DT = np.dtype([("res", "<i4"), ("status", "<i4"), ("dest_len", "<u8"), ("src
 # (LZMA_GPU_PLAN_COOP_LAT)
 # throughput_np: the throughput kernel without persistent lanes (one stream
 # per lane, the grid covers the batch)
-KERNELS = ("throughput", "throughput_np", "latency", "coop", "coop_lat", "global")
+# throughput / throughput_np: the throughput kernel (global sections
+# lane-interleaved in a slot area, the default) with and without persistent
+# lanes; throughput_slices / throughput_slices_np: the same with per-stream
+# global slices (LZMA_GPU_PLAN_NO_ILV, the round-2 layout)
+ILV, PLAN_NO_ILV = 0x40000000, 16
+THR = ("throughput", "throughput_np", "throughput_slices", "throughput_slices_np")
+KERNELS = THR + ("latency", "coop", "coop_lat", "global")
 
 
 @pytest.fixture(scope="module")
@@ -66,8 +72,11 @@ def _check_plan(plan, kernel):
         return
     assert plan.n_lds > 0 and cls
     for c in cls:
-        if kernel in ("throughput", "throughput_np"):
-            assert c.lds_mask == M_THR, hex(c.lds_mask)
+        if kernel in THR:
+            want = M_THR | (0 if "slices" in kernel else ILV)
+            assert c.lds_mask == want, hex(c.lds_mask)
+            if "slices" not in kernel:
+                assert c.slot_cells > 0 and c.slot_groups > 0 and c.slot_off % 64 == 0
         elif kernel == "latency":
             assert c.lds_mask == M_LAT and c.lanes_per_group == 1, hex(c.lds_mask)
         elif kernel == "coop":
@@ -79,11 +88,11 @@ def _check_plan(plan, kernel):
             assert c.lds_mask == M_LAT | COOP, hex(c.lds_mask)
     if kernel == "coop":
         assert any(c.lds_mask == M_ALL | COOP for c in cls)
-    if kernel in ("throughput", "throughput_np"):
+    if kernel in THR:
         # wave width follows table width: 32 streams per wave for lc+lp = 0
         # (config 3), 8 for lc+lp = 1, 2 for LZMA2 ranges (lc+lp <= 4 slices)
         assert all(c.lanes_per_group >= 2 for c in cls)
-        assert plan.persistent == (0 if kernel == "throughput_np" else 1)
+        assert plan.persistent == (0 if kernel.endswith("_np") else 1)
 
 
 def _opts(L, kernel):
@@ -93,6 +102,10 @@ def _opts(L, kernel):
         return L.plan_options("coop", cus=8, flags=4)
     if kernel == "throughput_np":
         return L.plan_options("throughput", cus=8, persistent=2)
+    if kernel == "throughput_slices":
+        return L.plan_options("throughput", cus=8, flags=PLAN_NO_ILV)
+    if kernel == "throughput_slices_np":
+        return L.plan_options("throughput", cus=8, persistent=2, flags=PLAN_NO_ILV)
     return L.plan_options(kernel, cus=8)
 
 
@@ -133,7 +146,7 @@ def test_goldens_through_each_kernel(L, kernel):
     r, res, dst = L.decode_batch_host(descs, src, dst_bytes, _opts(L, kernel), plan)
     assert r == 0, L.last_error()
     _check_plan(plan, kernel)
-    if kernel == "throughput":
+    if kernel in ("throughput", "throughput_slices"):
         # the lc0/lp0 goldens run the config-3 launch shape: 32 streams per wave
         assert max(plan.classes[k].lanes_per_group for k in range(plan.n_classes)) == 32
     bad = []
@@ -320,7 +333,8 @@ def test_cfg3_full_64k_streams_throughput_kernel(L, torch):
     plan, res, d_dst = _device_decode(L, torch, descs, comp, count * n)
     assert plan.n_classes == 1 and plan.n_lds == count
     c = plan.classes[0]
-    assert (c.lds_mask, c.lanes_per_group, c.groups_per_cu, c.waves_per_simd) == (M_THR, 32, 8, 2)
+    assert (c.lds_mask, c.lanes_per_group, c.groups_per_cu, c.waves_per_simd) == \
+        (M_THR | ILV, 32, 8, 2)
     assert (res["res"] == 0).all() and (res["status"] == 1).all()
     assert (res["dest_len"] == n).all() and (res["src_len"] == lens).all()
     assert np.array_equal(d_dst[:count * n].cpu().numpy(), plain)
@@ -338,7 +352,7 @@ def test_cfg3_full_finish_any_and_short_caps(L, torch):
     descs = L.make_descs([dict(src_off=int(offs[i]), src_len=int(lens[i]), dst_off=i * n,
                                dst_cap=caps[i], props=props, finish=0) for i in range(count)])
     plan, res, d_dst = _device_decode(L, torch, descs, comp, count * n)
-    assert plan.classes[0].lds_mask == M_THR and plan.classes[0].lanes_per_group == 32
+    assert plan.classes[0].lds_mask == M_THR | ILV and plan.classes[0].lanes_per_group == 32
     out = d_dst[:count * n].cpu().numpy().reshape(count, n)
     rows = plain.reshape(count, n)
     caps = np.array(caps)
@@ -440,7 +454,7 @@ def test_cfg4_1024_lzma2_blocks_coop_kernel(L, torch):
         assert out[k].tobytes() == ub[k % uniq][0], k
 
 
-@pytest.mark.parametrize("kernel", ("throughput", "latency"))
+@pytest.mark.parametrize("kernel", ("throughput", "throughput_slices", "latency"))
 def test_cfg4_blocks_on_lane_kernels(L, torch, kernel):
     """The same LZMA2 dict-reset blocks (256 KiB here) on the per-lane kernels,
     forced: LZMA2 chunk walking on 0x105 (32 lanes per wave) and 0x1BF."""

@@ -19,7 +19,7 @@ def test_session_layout_and_init():
     import lzmagpu as L
     assert ctypes.sizeof(L.Session) == 192
     assert L.Session.out.offset == 176 and L.Session.temp_buf.offset == 148
-    assert ctypes.sizeof(L.Plan) == 184
+    assert ctypes.sizeof(L.Plan) == 248
     assert L.session_probs_bytes(b"\x5d\x00\x00\x01\x00") == 2 * (56 * 4 + 950 + (768 << 3))
     assert L.session_probs_bytes(b"\xe1\x00\x00\x01\x00") == 0  # props byte 225
     r, s = L.session_init(b"\x5d\x00\x00\x01\x00", 0x1000, 0x2000, 65536)
