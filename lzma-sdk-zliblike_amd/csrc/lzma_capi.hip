@@ -974,7 +974,7 @@ static SRes plan_batch(LzmaGpuStreamDesc* descs, size_t n, uint32_t* order, Lzma
       const uint64_t groups =
           o.persistent == 2 ? grid : std::min<uint64_t>(grid, uint64_t(cus) * c.groups_per_cu);
       const uint64_t lane_groups = (c.lanes_per_group + lzgpu::kIlv - 1) / lzgpu::kIlv;
-      c.slot_cells = std::max<uint32_t>(rows, 1);
+      c.slot_cells = std::max<uint32_t>((rows + 1) & ~1u, 2);  // even: pairs of cells
       c.slot_groups = uint32_t(groups);
       slot_total[plan->n_classes] = groups * lane_groups * lzgpu::kIlv * c.slot_cells;
       c.lds_mask |= lzgpu::kIlvBit;

@@ -167,12 +167,33 @@ typedef __attribute__((address_space(1))) uint32_t gu32;
 // to its column with cell arithmetic scaled by the row length.
 constexpr uint32_t kIlvBit = 0x40000000u;
 constexpr uint32_t kIlv = 32u;
+// LZGPU_ILV_PAIR (A/B flag): cells interleaved two at a time instead -- cells
+// 2k, 2k+1 of a lane side by side in row k (128 bytes for 32 lanes), so the two
+// children of a tree node come in one 32-bit read
+#ifndef LZGPU_ILV_PAIR
+#define LZGPU_ILV_PAIR 0
+#endif
+#if LZGPU_ILV_PAIR
+__host__ __device__ __forceinline__ uint32_t ilv_cell(uint32_t i) {
+  return ((i & ~1u) << 5) + (i & 1u);  // row i / 2 of 2 * kIlv cells, slot i % 2
+}
+struct GS {
+  gu16* p;     // the lane's column (two cells wide)
+  uint32_t i;  // logical cell
+  __device__ __forceinline__ GS operator+(uint32_t k) const { return GS{p, i + k}; }
+  __device__ __forceinline__ gu16& operator[](uint32_t k) const { return p[ilv_cell(i + k)]; }
+  __device__ __forceinline__ gu16& operator*() const { return p[ilv_cell(i)]; }
+};
+constexpr uint32_t kIlvLaneCells = 2u;
+#else
 struct GS {
   gu16* p;
   __device__ __forceinline__ GS operator+(uint32_t k) const { return GS{p + kIlv * k}; }
   __device__ __forceinline__ gu16& operator[](uint32_t k) const { return p[kIlv * k]; }
   __device__ __forceinline__ gu16& operator*() const { return *p; }
 };
+constexpr uint32_t kIlvLaneCells = 1u;
+#endif
 
 // Build-time code-shape switches (A/B'd on MI355X):
 //   LZGPU_NORM_BRANCHLESS  NORMALIZE as selects instead of a skip-able branch
@@ -344,7 +365,11 @@ struct Tab {
   // cell `off` of the global table (lane-interleaved under kIlvBit)
   __device__ __forceinline__ auto g(uint32_t off) const {
     if constexpr ((M & kIlvBit) != 0u)
+#if LZGPU_ILV_PAIR
+      return GS{gl, off};
+#else
       return GS{gl + kIlv * off};
+#endif
     else
       return gl + off;
   }
@@ -2164,7 +2189,12 @@ __device__ __forceinline__ void lz_init_state_real(LzStateT<Lo>& s) {
     if constexpr ((M & kIlvBit) != 0u) {
       // the lane's column: one cell per row (the lanes of a group that start
       // together store whole 64-byte rows)
+#if LZGPU_ILV_PAIR
+      for (uint32_t i = 0; i < L.glb_cells; i += 2)
+        *(gu32*)(s.gl + ilv_cell(i)) = kProbInit | (kProbInit << 16);
+#else
       for (uint32_t i = 0; i < L.glb_cells; ++i) s.gl[kIlv * i] = uint16_t(kProbInit);
+#endif
     } else {
       fill_prob_init(s.gl, L.glb_cells);
     }

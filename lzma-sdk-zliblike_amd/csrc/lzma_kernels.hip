@@ -60,7 +60,8 @@ __global__ void __launch_bounds__(64, W) lzgpu_decode_lds_kernel(
   gu16* gcol = nullptr;
   if constexpr ((M & kIlvBit) != 0u) {
     const uint32_t grp = blockIdx.x * ((blockDim.x + kIlv - 1) / kIlv) + threadIdx.x / kIlv;
-    gcol = (gu16*)(ws + slot_off) + uint64_t(grp) * slot_cells * kIlv + (threadIdx.x % kIlv);
+    gcol = (gu16*)(ws + slot_off) + uint64_t(grp) * slot_cells * kIlv +
+           (threadIdx.x % kIlv) * kIlvLaneCells;
   }
   (void)slot_off;
   (void)slot_cells;

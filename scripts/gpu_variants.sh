@@ -8,7 +8,7 @@ TAG=${1:-var}
 for round in 1 2; do
 for so in lzma-sdk-zliblike_amd/lib/variants/*.so; do
   v=$(basename $so .so)
-  LZGPU_LIB=$PWD/$so timeout -k 10 300 python bench.py --steps 5 --warmup 1 --no-cpu-baseline > gpurun_out/${TAG}_${v}_$round.json 2>> gpurun_out/${TAG}.err
+  LZGPU_LIB=$PWD/$so timeout -k 10 300 python bench.py --steps 5 --warmup 1 --no-cpu-baseline --no-secondary --no-e2e --no-crc > gpurun_out/${TAG}_${v}_$round.json 2>> gpurun_out/${TAG}.err
   s=$?; echo "$v r$round exit $s: $(python -c "import json;d=json.load(open('gpurun_out/${TAG}_${v}_$round.json'));print(d['value'], d['ms_per_step'], d['verified'])")"
   [ $s -eq 0 ] || exit $s
 done

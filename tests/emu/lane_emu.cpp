@@ -34,14 +34,14 @@ void emu_decode_batch_lds(const LzmaGpuStreamDesc* descs, size_t n, const uint8_
   // lane-interleaved global sections: 32 lane columns of the widest LZMA2
   // layout's global rows; stream i runs in column i % 32, its neighbours'
   // cells left as garbage (columns are reused stream after stream)
-  const size_t rows = make_layout(4, 0, 4, LZGPU_LDS_MASK).glb_cells;
+  const size_t rows = (make_layout(4, 0, 4, LZGPU_LDS_MASK).glb_cells + 1) & ~size_t(1);
   std::vector<uint16_t> slots(rows * kIlv, 0x5A5A);
 #endif
   for (size_t i = 0; i < n; ++i) {
     memset(slab, 0xA5, size_t(stride) * 2);  // LDS is not zeroed between workgroups
 #if defined(EMU_ILV)
     results[i] = lane_decode_lds<LZGPU_LDS_MASK | kIlvBit>(descs[i], src, dst, ws, slab, stride,
-                                                          slots.data() + (i % kIlv));
+                                                          slots.data() + (i % kIlv) * kIlvLaneCells);
 #elif defined(EMU_COOP_ALL)
     // the wave-cooperative kernel with every section in LDS (its default
     // placement where the whole table fits)

@@ -48,6 +48,7 @@ EMU_VARIANTS = {
     "match_fat_global_len": "-DLZGPU_LDS_MASK_LAT=0x105 -DLZGPU_LDS_MASK=0x107 -DEMU_LAT_MASK",
     "latency_instantiation": "-DEMU_LAT_MASK",
     "interleaved_global_instantiation": "-DEMU_ILV",
+    "interleaved_pairs_instantiation": "-DEMU_ILV -DLZGPU_ILV_PAIR=1",
     "coop_instantiation": "-DEMU_COOP",
     "coop_all_lds_instantiation": "-DEMU_COOP_ALL",
     "copy_bytes": "-DLZGPU_COPY_WIDE=0",
