@@ -315,6 +315,15 @@ constexpr uint32_t kIlvLaneCells = 1u;
 #endif
 //   LZGPU_UNIFORM_EXIT the literal batch loop exits only when every lane of
 //                      the wave is done (lanes drop out by a flag)
+//   LZGPU_IN_NT / LZGPU_OUT_NT  compressed input read / literal bytes written with
+//                      the nontemporal hint (A/B flags: input is read once, output
+//                      lines are written a byte at a time over a long time)
+#ifndef LZGPU_IN_NT
+#define LZGPU_IN_NT 0
+#endif
+#ifndef LZGPU_OUT_NT
+#define LZGPU_OUT_NT 0
+#endif
 #ifndef LZGPU_UNIFORM_EXIT
 #define LZGPU_UNIFORM_EXIT 1
 #endif
@@ -384,6 +393,15 @@ struct Tab {
 
 __device__ __forceinline__ uint64_t ring_back(uint64_t pos, uint32_t dist, uint64_t cap) {
   return pos - dist + (pos < dist ? cap : 0);
+}
+
+// one decoded literal byte to the window
+__device__ __forceinline__ void lz_put(gbyte* p, uint32_t v) {
+#if LZGPU_OUT_NT && !defined(LZGPU_HOST_EMU)
+  __builtin_nontemporal_store(uint8_t(v), p);
+#else
+  *p = uint8_t(v);
+#endif
 }
 
 // ------------------------------------------------------------------ input readers
@@ -575,6 +593,8 @@ struct GlobalReaderQ {
     const gu32* a = left ? wp : (const gu32*)g_lz_zero_word;
 #ifdef LZGPU_HOST_EMU
     nx = u32x4{a[0], a[1], a[2], a[3]};
+#elif LZGPU_IN_NT
+    nx = __builtin_nontemporal_load((const __attribute__((address_space(1))) u32x4*)a);
 #else
     nx = *(const __attribute__((address_space(1))) u32x4*)a;
 #endif
@@ -1454,7 +1474,7 @@ __device__ __forceinline__ void lz_literal(Rc<Rd>& rc, const Tab<M, Lo>& T, uint
     }
   }
   prev = sym & 0xFFu;
-  if constexpr (St) dic[pos] = uint8_t(prev);
+  if constexpr (St) lz_put(dic + pos, prev);
   pos++;
   total++;
 }
@@ -1737,7 +1757,7 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
       if (!rc.bit(T.template at<S_REP>(12 + st))) {
         if (!rc.bit(T.template at<S_REP0L>((st << pb) + ps))) {
           prev = dic[ring_back(pos, r0, cap)];
-          dic[pos++] = uint8_t(prev);
+          lz_put(dic + pos++, prev);
           total++;
           st = (st < 7) ? 9 : 11;
 #if LZGPU_MB_PF
