@@ -957,10 +957,11 @@ static SRes plan_batch(LzmaGpuStreamDesc* descs, size_t n, uint32_t* order, Lzma
         break;
       }
     if (!(o.flags & LZMA_GPU_PLAN_NO_ILV) && c.lds_mask == LZGPU_LDS_MASK &&
-        c.lanes_per_group <= 64) {
+        (c.lanes_per_group == 32 || c.lanes_per_group == 64)) {
       // lane-interleaved global sections: one column per resident lane (the
       // lanes keep it across the streams they take from the queue); config 3
-      // 28.1 -> 29.9 GB/s (profiles/r02_ilv/ilv_ab.log)
+      // 28.1 -> 29.9 GB/s (profiles/r02_ilv/ilv_ab.log).  Only for whole lane
+      // groups: a narrower workgroup would leave most of every row unused.
       uint32_t rows = 0;
       for (uint32_t i : bucket_idx[b]) {
         const LzmaGpuStreamDesc& d = descs[i];

@@ -73,9 +73,10 @@ def _check_plan(plan, kernel):
     assert plan.n_lds > 0 and cls
     for c in cls:
         if kernel in THR:
-            want = M_THR | (0 if "slices" in kernel else ILV)
-            assert c.lds_mask == want, hex(c.lds_mask)
-            if "slices" not in kernel:
+            # interleaved rows for whole 32-lane groups, slices for narrower waves
+            ilv = "slices" not in kernel and c.lanes_per_group in (32, 64)
+            assert c.lds_mask == M_THR | (ILV if ilv else 0), (hex(c.lds_mask), c.lanes_per_group)
+            if ilv:
                 assert c.slot_cells > 0 and c.slot_groups > 0 and c.slot_off % 64 == 0
         elif kernel == "latency":
             assert c.lds_mask == M_LAT and c.lanes_per_group == 1, hex(c.lds_mask)
@@ -92,6 +93,9 @@ def _check_plan(plan, kernel):
         # wave width follows table width: 32 streams per wave for lc+lp = 0
         # (config 3), 8 for lc+lp = 1, 2 for LZMA2 ranges (lc+lp <= 4 slices)
         assert all(c.lanes_per_group >= 2 for c in cls)
+        if kernel == "throughput_np":
+            # 32 lanes forced wherever the slices fit: interleaved rows for those
+            assert any(c.lds_mask & ILV for c in cls)
         assert plan.persistent == (0 if kernel.endswith("_np") else 1)
 
 
@@ -101,7 +105,9 @@ def _opts(L, kernel):
     if kernel == "coop_lat":
         return L.plan_options("coop", cus=8, flags=4)
     if kernel == "throughput_np":
-        return L.plan_options("throughput", cus=8, persistent=2)
+        # 32 streams per wave wherever the slices fit: the interleaved rows
+        # without persistent lanes on every batch, not only lc+lp = 0 classes
+        return L.plan_options("throughput", cus=8, persistent=2, lanes_per_group=32)
     if kernel == "throughput_slices":
         return L.plan_options("throughput", cus=8, flags=PLAN_NO_ILV)
     if kernel == "throughput_slices_np":
