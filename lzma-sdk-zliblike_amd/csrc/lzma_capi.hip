@@ -956,8 +956,9 @@ static SRes plan_batch(LzmaGpuStreamDesc* descs, size_t n, uint32_t* order, Lzma
         c.flags |= LZMA_GPU_CLASS_HAS_LZMA2;
         break;
       }
+    static const bool ilv_any = env_int("LZGPU_ILV_ANY", 0) != 0;  // A/B: any lane count
     if (!(o.flags & LZMA_GPU_PLAN_NO_ILV) && c.lds_mask == LZGPU_LDS_MASK &&
-        (c.lanes_per_group == 32 || c.lanes_per_group == 64)) {
+        (c.lanes_per_group == 32 || c.lanes_per_group == 64 || (ilv_any && c.lanes_per_group <= 64))) {
       // lane-interleaved global sections: one column per resident lane (the
       // lanes keep it across the streams they take from the queue); config 3
       // 28.1 -> 29.9 GB/s (profiles/r02_ilv/ilv_ab.log).  Only for whole lane
