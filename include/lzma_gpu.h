@@ -222,7 +222,8 @@ size_t LzmaGpu_PlanBatch(LzmaGpuStreamDesc *descs, size_t n, uint32_t *order);
  * LZGPU_LANES=<streams per workgroup>, LZGPU_GROUPS=<workgroups per CU>,
  * LZGPU_OCC=<1|2|4 waves per SIMD>, LZGPU_CUS, LZGPU_COOP=0|1,
  * LZGPU_PERSIST=0 (one stream per lane), LZGPU_CLASSES=1 (one LDS launch),
- * LZGPU_SLICE_ALIGN8=1, LZGPU_KERNEL_LZMA2=1, LZGPU_COOP_LAT=1, LZGPU_MERGE_LAT=0, LZGPU_ILV=0 (the
+ * LZGPU_SLICE_ALIGN8=1, LZGPU_KERNEL_LZMA2=1, LZGPU_COOP_LAT=1, LZGPU_MERGE_LAT=0, LZGPU_ILV=0,
+ * LZGPU_ILV_ANY=1 (the
  * LZMA_GPU_PLAN_* flags below); DecodeBatchEx reads LZGPU_CLASS_STREAMS=0
  * (classes launched one after another on the caller's stream).
  * workspace_bytes includes the LDS launches' work counters at queue_offset
@@ -316,6 +317,9 @@ typedef struct LzmaGpuPlanOptions {
  * of the 32 lanes of a lane group side by side -- in a slot area per class
  * (LZGPU_ILV=0) */
 #define LZMA_GPU_PLAN_NO_ILV 16u
+/* A/B: interleaved rows for throughput waves of any width up to 64 lanes, not
+ * only whole 32-lane groups (LZGPU_ILV_ANY=1) */
+#define LZMA_GPU_PLAN_ILV_ANY 32u
 
 /* LzmaGpu_PlanBatchEx with explicit options (opt == NULL: as PlanBatchEx,
  * whose defaults take the LZGPU_* experiment variables of the environment,

@@ -711,7 +711,7 @@ static uint32_t device_cus() {
 // call time (LZGPU_KERNEL=global|throughput|latency|coop, LZGPU_MASK=1|2,
 // LZGPU_COOP=0|1, LZGPU_CUS, LZGPU_LANES, LZGPU_GROUPS, LZGPU_OCC,
 // LZGPU_PERSIST=0, LZGPU_CLASSES=1, LZGPU_SLICE_ALIGN8=1, LZGPU_KERNEL_LZMA2=1,
-// LZGPU_COOP_LAT=1, LZGPU_MERGE_LAT=0, LZGPU_ILV=0).  Only LzmaGpu_PlanBatchEx reads them;
+// LZGPU_COOP_LAT=1, LZGPU_MERGE_LAT=0, LZGPU_ILV=0, LZGPU_ILV_ANY=1).  Only LzmaGpu_PlanBatchEx reads them;
 // LzmaGpu_PlanBatchOpt takes its options from the caller alone.
 static LzmaGpuPlanOptions env_options() {
   LzmaGpuPlanOptions o;
@@ -741,7 +741,8 @@ static LzmaGpuPlanOptions env_options() {
             (env_int("LZGPU_KERNEL_LZMA2", 0) ? LZMA_GPU_PLAN_KERNEL_LZMA2 : 0u) |
             (env_int("LZGPU_COOP_LAT", 0) ? LZMA_GPU_PLAN_COOP_LAT : 0u) |
             (env_int("LZGPU_MERGE_LAT", 1) ? 0u : LZMA_GPU_PLAN_NO_MERGE_LAT) |
-            (env_int("LZGPU_ILV", 1) ? 0u : LZMA_GPU_PLAN_NO_ILV);
+            (env_int("LZGPU_ILV", 1) ? 0u : LZMA_GPU_PLAN_NO_ILV) |
+            (env_int("LZGPU_ILV_ANY", 0) ? LZMA_GPU_PLAN_ILV_ANY : 0u);
   return o;
 }
 
@@ -956,7 +957,7 @@ static SRes plan_batch(LzmaGpuStreamDesc* descs, size_t n, uint32_t* order, Lzma
         c.flags |= LZMA_GPU_CLASS_HAS_LZMA2;
         break;
       }
-    static const bool ilv_any = env_int("LZGPU_ILV_ANY", 0) != 0;  // A/B: any lane count
+    const bool ilv_any = (o.flags & LZMA_GPU_PLAN_ILV_ANY) != 0;
     if (!(o.flags & LZMA_GPU_PLAN_NO_ILV) && c.lds_mask == LZGPU_LDS_MASK &&
         (c.lanes_per_group == 32 || c.lanes_per_group == 64 || (ilv_any && c.lanes_per_group <= 64))) {
       // lane-interleaved global sections: one column per resident lane (the
