@@ -700,6 +700,17 @@ struct BulkReaderFor<LZGPU_LDS_MASK_ALL | kCoopBit> {
   typedef GlobalReaderQ type;
 };
 
+// LZGPU_MB_PF per placement: the matched byte is prefetched at match end in
+// the throughput and cooperative kernels; the one-stream-per-wave latency
+// kernel loads it when the literal needs it -- the register the prefetch holds
+// across the next IsMatch decision costs it scratch spills at 4 waves per SIMD
+// (config 2 5.86 -> 6.12 GB/s, config 5 4.90 -> 5.03 without; config 3 and 4
+// within noise either way: profiles/r02_ilv/mbpf_latency_ab.log)
+template <uint32_t M>
+__host__ __device__ constexpr bool mb_pf_on() {
+  return LZGPU_MB_PF && (((M & kCoopBit) != 0u) || ((M & ~kIlvBit) == LZGPU_LDS_MASK));
+}
+
 // checkpoint hooks for readers without them: every NORMALIZE checks
 template <class Rd>
 __device__ __forceinline__ void rd_topup(Rd& rd) {
@@ -1422,7 +1433,7 @@ __device__ __forceinline__ void lz_literal(Rc<Rd>& rc, const Tab<M, Lo>& T, uint
 #endif
   } else {
 #if LZGPU_MB_PF
-    uint32_t mbyte = mb_pf;
+    uint32_t mbyte = mb_pf_on<M>() ? mb_pf : uint32_t(dic[ring_back(pos, r0, cap)]);
 #else
     uint32_t mbyte = dic[ring_back(pos, r0, cap)];
 #endif
@@ -1576,7 +1587,8 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
   if (full != 0 || total != 0) prev = dic[(pos == 0 ? cap : pos) - 1];
 #if LZGPU_MB_PF
   // byte at distance rep0, needed by a matched literal (state >= 7)
-  uint32_t mb_pf = (st >= 7) ? uint32_t(dic[ring_back(pos, r0, cap)]) : 0u;
+  uint32_t mb_pf = 0;
+  if constexpr (mb_pf_on<M>()) mb_pf = (st >= 7) ? uint32_t(dic[ring_back(pos, r0, cap)]) : 0u;
 #endif
 
   uint32_t ps = 0;
@@ -1646,7 +1658,8 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
 #endif
 #if LZGPU_LIT_UNIFIED && LZGPU_MB_PF
           if constexpr (((M >> S_LITP) & 1u) != 0u && ((M >> S_LITM) & 1u) == 0u)
-            lz_literal_unified<M>(rc, T, st, prev, total, full, lc, lp_mask, dic, pos, mb_pf);
+            lz_literal_unified<M>(rc, T, st, prev, total, full, lc, lp_mask, dic, pos,
+                                  mb_pf_on<M>() ? mb_pf : uint32_t(dic[ring_back(pos, r0, cap)]));
           else
 #endif
           lz_literal<M, !LZGPU_LIT_WC>(rc, T, st, prev, total, full, lc, lp_mask, dic, pos,
@@ -1761,7 +1774,7 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
           total++;
           st = (st < 7) ? 9 : 11;
 #if LZGPU_MB_PF
-          mb_pf = dic[ring_back(pos, r0, cap)];
+          if constexpr (mb_pf_on<M>()) mb_pf = dic[ring_back(pos, r0, cap)];
 #endif
           continue;
         }
@@ -1947,7 +1960,7 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
       prev = lz_copy(dic, pos, from, n, r0, cap);
       pos += n;
 #if LZGPU_MB_PF
-      mb_pf = dic[ring_back(pos, r0, cap)];
+      if constexpr (mb_pf_on<M>()) mb_pf = dic[ring_back(pos, r0, cap)];
 #endif
     }
     LZ_PROF_MARK(s, 2, t_prof);
