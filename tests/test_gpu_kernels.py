@@ -45,7 +45,11 @@ RES_DT = np.dtype([("res", "<i4"), ("status", "<i4"), ("dest_len", "<u8"), ("src
 # lanes; throughput_slices / throughput_slices_np: the same with per-stream
 # global slices (LZMA_GPU_PLAN_NO_ILV, the round-2 layout)
 ILV, PLAN_NO_ILV = 0x40000000, 16
-THR = ("throughput", "throughput_np", "throughput_slices", "throughput_slices_np")
+# throughput_reuse: planned for one CU, so a persistent lane decodes several
+# streams one after another in the same interleaved column (re-initialised per
+# stream)
+THR = ("throughput", "throughput_np", "throughput_slices", "throughput_slices_np",
+       "throughput_reuse")
 KERNELS = THR + ("latency", "coop", "coop_lat", "global")
 
 
@@ -96,6 +100,10 @@ def _check_plan(plan, kernel):
         if kernel == "throughput_np":
             # 32 lanes forced wherever the slices fit: interleaved rows for those
             assert any(c.lds_mask & ILV for c in cls)
+        if kernel == "throughput_reuse":
+            # fewer resident lanes than streams in every interleaved class
+            ilv = [c for c in cls if c.lds_mask & ILV]
+            assert ilv and any(c.n > c.slot_groups * c.lanes_per_group for c in ilv)
         assert plan.persistent == (0 if kernel.endswith("_np") else 1)
 
 
@@ -108,6 +116,8 @@ def _opts(L, kernel):
         # 32 streams per wave wherever the slices fit: the interleaved rows
         # without persistent lanes on every batch, not only lc+lp = 0 classes
         return L.plan_options("throughput", cus=8, persistent=2, lanes_per_group=32)
+    if kernel == "throughput_reuse":
+        return L.plan_options("throughput", cus=1, groups_per_cu=1, lanes_per_group=32)
     if kernel == "throughput_slices":
         return L.plan_options("throughput", cus=8, flags=PLAN_NO_ILV)
     if kernel == "throughput_slices_np":
