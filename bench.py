@@ -1,7 +1,7 @@
 """bench.py -- batch LZMA decode throughput on MI355X (BASELINE.json metric).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--scaling weak|strong]
-                    [--config cfg3|cfg2|cfg4|cfg5|xz|7z]
+                    [--config cfg3|cfg1|cfg2|cfg4|cfg5|xz|7z] [--streams S]
 
 One "step" = one launch of the batch decode kernel over the whole per-GPU
 batch (inputs already resident in HBM, outputs written to HBM).  Default
@@ -19,10 +19,13 @@ bracketed, MAX over ranks; value = all ranks' decompressed bytes / that time.
 Rank 0 prints ONE JSON line.  It carries the live roofline of the decode
 kernel (HIP events on the launch stream), the issue-side counters of the
 committed rocprof profile, an end-to-end (H2D + decode + D2H, pinned host
-buffers) rate, and the CPU baseline: the oracle restatement
-(oracle/liboracle.so, a checker, never the measured product) timed on every
-host core this job may use over the same batch.  Every timed batch is verified
-bit-exact against its plaintext afterwards.
+buffers) rate, and the CPU baseline: the reference's own LzmaDecode
+(oracle/_ref/libref_lzma.so, LzmaDec.c compiled in place, "kind": "reference";
+the oracle restatement oracle/liboracle.so, "kind": "port", where that library
+is absent) timed on every host core this job may use over the same batch, on
+rank 0 after the timed region at any world size.  The output is poisoned and
+every timed step writes its own poisoned results array, so `verified` covers
+each timed launch (bit-exact output, exact per-stream results).
 
 --config cfg4: 1 MiB LZMA2 dict-reset blocks, 1024
 per GPU, one compressed file on rank 0 scattered to the peers over RCCL
@@ -65,6 +68,20 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def pool_map(fn, jobs, workers, chunksize=1):
+    """imap_unordered over a fork pool that is closed and joined when done,
+    never terminated: `with Pool()` calls terminate() on exit, which SIGTERMs
+    the workers -- forked under rocprofv3 they carry its signal handler, and
+    the profile record then shows an abort."""
+    pool = mp.get_context("fork").Pool(workers)
+    try:
+        for r in pool.imap_unordered(fn, jobs, chunksize=chunksize):
+            yield r
+    finally:
+        pool.close()
+        pool.join()
+
+
 def _compress_range(args):
     plain_path, n, lc, lp, pb, dsz, lo, hi = args
     mm = np.memmap(plain_path, dtype=np.uint8, mode="r")
@@ -100,10 +117,9 @@ def build_workload(cfg, first, count, workers):
         jobs = [(plain_path, n, lc, lp, pb, dsz, lo, min(lo + chunk, count))
                 for lo in range(0, count, chunk)]
         parts = [None] * count
-        with mp.get_context("fork").Pool(workers) as pool:
-            for lo, out in pool.imap_unordered(_compress_range, jobs):
-                for k, c in enumerate(out):
-                    parts[lo + k] = c
+        for lo, out in pool_map(_compress_range, jobs, workers):
+            for k, c in enumerate(out):
+                parts[lo + k] = c
         lens = np.array([len(c) for c in parts], dtype=np.uint64)
         comp = np.frombuffer(b"".join(parts), dtype=np.uint8)
         np.savez(comp_path, comp=comp, lens=lens)
@@ -199,6 +215,22 @@ def run_dry(args):
     elapsed = D.reduce_max(0.001 * (rank + 1))
     ranks = gather_ranks({"rank": rank, "first": first, "streams": mine})
     total = int(D.reduce_sum(float(mine)))
+    cpu = None
+    if rank == 0 and not args.no_cpu_baseline and args.config in CONFIGS:
+        # the same object shape the GPU run emits at any world size, on a small
+        # sample (the plumbing test: rank 0, after the timed region)
+        import native
+        _, n, lc, lp, pb, dsz, _ = CONFIGS[args.config]
+        ci = cpu_info()
+        m = 64
+        plain, comp, lens, props = build_workload(args.config, 0, m, 1)
+        offs = np.zeros(m, dtype=np.uint64)
+        offs[1:] = np.cumsum(lens)[:-1]
+        kind = "reference" if native.have_ref() else "port"
+        v, dt, mm, errs = cpu_baseline(comp, lens, offs, n, props, ci["usable"], m, kind)
+        cpu = {"value": round(v, 2), "unit": "MB/s", "cores": ci["usable"], "kind": kind,
+               "sample": f"{mm} streams of {args.config} (dry run), {dt:.3f}s", "cpu": ci,
+               "errors": int(errs)}
     if rank == 0:
         print(json.dumps({
             "metric": "decompressed MB/s (whole node), 64K-stream batch; bit-exact vs CPU LzmaDec",
@@ -206,10 +238,46 @@ def run_dry(args):
             "warmup": args.warmup, "scaling": args.scaling, "dry_run": True,
             "world": dist.get_world_size() if dist.is_initialized() else 1,
             "backend": dist.get_backend() if dist.is_initialized() else None,
-            "streams_total": total, "elapsed_max_s": elapsed, "ranks": ranks}), flush=True)
+            "streams_total": total, "elapsed_max_s": elapsed, "ranks": ranks,
+            "cpu_baseline": cpu}), flush=True)
     if world > 1:
         dist.destroy_process_group()
     return 0
+
+
+RES_DT = np.dtype([("res", "<i4"), ("status", "<i4"), ("dest_len", "<u8"), ("src_len", "<u8")])
+
+
+def timed_buffers(torch, dev, d_dst, count, steps):
+    """Poison for the timed loop (outside its events): the output is filled with
+    0xA5 and every timed step gets its OWN results array filled with 0xFF
+    (res = -1).  Afterwards the output must equal the plaintext and every
+    step's array must hold every stream's exact answer, so `verified` covers
+    each timed launch: one that decoded nothing leaves its array poisoned."""
+    d_dst.fill_(0xA5)
+    r = torch.full((max(steps, 1), count * 24), 0xFF, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+    return r
+
+
+def step_results(d_res_steps):
+    """Every timed step's results, as a (steps, count) structured array."""
+    raw = d_res_steps.cpu().numpy()
+    return np.stack([np.frombuffer(raw[k].tobytes(), dtype=RES_DT) for k in range(raw.shape[0])])
+
+
+def plan_kernels(plan):
+    """Names of the kernels a plan launches (one per LDS class, + the generic one)."""
+    names = []
+    for c in list(plan.classes)[:int(plan.n_classes)]:
+        if int(c.n) == 0:
+            continue
+        k = "lzgpu_decode_coop_kernel" if int(c.lds_mask) & 0x80000000 else "lzgpu_decode_lds_kernel"
+        if k not in names:
+            names.append(k)
+    if int(plan.n) > int(plan.n_lds):
+        names.append("lzgpu_decode_batch_kernel")
+    return " + ".join(names) if names else None
 
 
 def make_descs(lens, n, props, finish=1):
@@ -277,6 +345,173 @@ def measure_crc(L, torch, descs, d_desc, d_res, d_dst, plain, count, n, stream, 
             "verified": bool(np.array_equal(got, want))}
 
 
+# ---------------------------------------------------------------- config 1
+
+def run_cfg1(args):
+    """Config 1: ONE 1 MiB stream (lc3/lp0/pb2, 64 KiB dict) --
+    plumbing and bit-exactness of the single-stream path, timed beside the
+    reference's own LzmaDecode on one host core.  The stream is the committed
+    reference-encoded golden (tests/golden/cfg1_blob.bin; enwik8 is not
+    available offline: synthetic text).
+
+    value: the device-resident decode (the stream already in HBM, one launch of
+    the batch API with n = 1 on the wave-cooperative kernel, output left in
+    HBM), K steps between barrier + synchronize.  Beside it, over host buffers
+    (PCIe-inclusive, never `value`): the drop-in LzmaDecode, the fork's
+    DecodeToBuf loop (512 KiB in / 1 MiB out, 7zDec.c:567-648) and the
+    7zDec.c:127-171 DecodeToDic loop (16 KiB look windows over a whole-output
+    dictionary, the device mirror), each checked against the reference's
+    recorded answers.  One stream is one serial range-decoder chain: a GPU wave
+    decides it far slower than a CPU core does; the batch configs are where the
+    GPU's throughput is."""
+    import hashlib
+    import dist_bench as D
+    world, rank, local_rank = D.world_info()
+    gold = os.path.join(ROOT, "tests", "golden")
+    doc = json.load(open(os.path.join(gold, "cfg1_cases.json")))
+    comp = open(os.path.join(gold, "cfg1_blob.bin"), "rb").read()
+    props = bytes.fromhex(doc["props"])
+    n = doc["plaintext"]["bytes"]
+    want_sha = doc["plaintext"]["sha256"]
+    exp = {(c["kind"], c.get("dest_cap"), c.get("finish"), c.get("in_chunk"), c.get("win")):
+           c["expect"] for c in doc["cases"]}
+    import torch
+    import torch.distributed as dist
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    import lzmagpu as L
+
+    def sha(b):
+        return hashlib.sha256(b).hexdigest()
+
+    # ---- device-resident: one stream, batch API n = 1 (cooperative plan)
+    descs = L.make_descs([dict(src_off=0, src_len=len(comp), dst_off=0, dst_cap=n, props=props,
+                               finish=1, kind=L.KIND_LZMA)])
+    plan, order = L.plan_ex(descs, L.plan_options("coop"))
+    d_src = torch.frombuffer(bytearray(comp + bytes(16)), dtype=torch.uint8).to(dev)
+    d_dst = torch.empty(n + 16, dtype=torch.uint8, device=dev)
+    d_ws = torch.empty(max(int(plan.workspace_bytes), 16), dtype=torch.uint8, device=dev)
+    d_desc = torch.frombuffer(bytearray(bytes(descs)), dtype=torch.uint8).to(dev)
+    d_order = torch.frombuffer(bytearray(bytes(order)), dtype=torch.uint8).to(dev)
+    stream = torch.cuda.current_stream(dev)
+    sh = stream.cuda_stream
+
+    def step(res):
+        if L.decode_batch_device_ex(plan, d_desc.data_ptr(), d_order.data_ptr(), d_src.data_ptr(),
+                                    d_dst.data_ptr(), d_ws.data_ptr(), res.data_ptr(), sh):
+            raise RuntimeError("LzmaGpu_DecodeBatchEx failed: " + L.last_error())
+
+    d_res0 = torch.empty(24, dtype=torch.uint8, device=dev)
+    for _ in range(args.warmup):
+        step(d_res0)
+    torch.cuda.synchronize()
+    d_res_steps = timed_buffers(torch, dev, d_dst, 1, args.steps)
+    D.barrier()
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for k, (a, b) in enumerate(evs):
+        a.record(stream)
+        step(d_res_steps[k])
+        b.record(stream)
+    torch.cuda.synchronize()
+    D.barrier()
+    torch.cuda.synchronize()
+    elapsed = D.reduce_max(time.perf_counter() - t0, dev)
+    dec_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    e_end = exp[("lzma", n, 1, None, None)]
+    allres = step_results(d_res_steps)
+    ok = bool((allres["res"] == e_end["res"]).all() and (allres["status"] == e_end["status"]).all()
+              and (allres["dest_len"] == e_end["dest_len"]).all()
+              and (allres["src_len"] == e_end["src_len"]).all())
+    ok = ok and sha(d_dst[:n].cpu().numpy().tobytes()) == want_sha
+
+    # ---- host buffers through the drop-in API (PCIe-inclusive)
+    dropin = {}
+    t0 = time.perf_counter()
+    k_calls = max(1, min(args.steps, 5))
+    for _ in range(k_calls):
+        r = L.LzmaDecode(comp, props, n, 1)
+        ok = ok and (r[0], r[1], r[2], r[3], sha(r[4])) == (
+            e_end["res"], e_end["status"], e_end["dest_len"], e_end["src_len"], e_end["sha256"])
+    dt = (time.perf_counter() - t0) / k_calls
+    dropin["LzmaDecode"] = {"MBps": round(n / dt / 1e6, 3), "ms_per_call": round(dt * 1e3, 3)}
+    t0 = time.perf_counter()
+    r = L.LzmaUncompress(comp, props, n)
+    dt = time.perf_counter() - t0
+    e_any = exp[("lzma", n, 0, None, None)]
+    ok = ok and (r[0], r[1], r[2], sha(r[3])) == (e_any["res"], e_any["dest_len"],
+                                                  e_any["src_len"], e_any["sha256"])
+    dropin["LzmaUncompress"] = {"MBps": round(n / dt / 1e6, 3), "ms_per_call": round(dt * 1e3, 3)}
+    t0 = time.perf_counter()
+    calls, trace, out, used = L.stream_decode(comp, props, n, 1 << 19, 1 << 20, 0)
+    dt = time.perf_counter() - t0
+    e_st = exp[("stream", None, 0, 1 << 19, None)]
+    ok = ok and [list(t) for t in trace] == e_st["trace"] and sha(out) == e_st["sha256"]
+    dropin["DecodeToBuf_512K_in_1M_out"] = {"MBps": round(n / dt / 1e6, 3), "calls": calls}
+    t0 = time.perf_counter()
+    calls, trace, out, used = L.dic_decode(comp, props, n, 1 << 14)
+    dt = time.perf_counter() - t0
+    e_dic = exp[("dic", None, None, None, 1 << 14)]
+    ok = ok and [list(t) for t in trace] == e_dic["trace"] and sha(out) == e_dic["sha256"]
+    dropin["DecodeToDic_16K_windows"] = {"MBps": round(n / dt / 1e6, 3), "calls": calls,
+                                         "h2d_bytes_per_call": "its input window only "
+                                         "(device dictionary mirror)"}
+    ok = D.all_true(ok, dev)
+
+    cpu = None
+    if rank == 0 and not args.no_cpu_baseline:
+        import native
+        if native.have_ref():
+            lib, pre, kind = native.ref(), "ref", "reference"
+        else:
+            lib, pre, kind = native.oracle(), "orc", "port"
+        reps, t0 = 0, time.perf_counter()
+        while time.perf_counter() - t0 < 3.0 or reps < 3:
+            r = native.decode(lib, pre, comp, props, n, 1)
+            reps += 1
+        dt = (time.perf_counter() - t0) / reps
+        cpu = {"value": round(n / dt / 1e6, 2), "unit": "MB/s", "cores": 1, "kind": kind,
+               "impl": "the reference's LzmaDecode (LzmaDec.c:972, oracle/_ref/libref_lzma.so, "
+                       "gcc -O2, compiled in place)" if kind == "reference" else
+                       "oracle/lzma_oracle.c restatement",
+               "sample": f"the same 1 MiB stream decoded {reps} times on one core, "
+                         f"{dt * 1e3:.2f} ms per call",
+               "verified": sha(r[4]) == want_sha}
+        if kind == "reference":
+            _, _, out, _, ns = native.dic_decode(lib, pre, comp, props, n, 1 << 14)
+            cpu["DecodeToDic_16K_windows_MBps"] = round(n / (ns * 1e-9) / 1e6, 2)
+    value = world * n * args.steps / elapsed / 1e6
+    alg = len(comp) + 5 + n
+    achieved = alg / (dec_ms * 1e-3) / 1e9
+    if rank == 0:
+        print(json.dumps({
+            "metric": "decompressed MB/s, config 1: one 1 MiB stream (single-stream path)",
+            "value": round(value, 3), "unit": "MB/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u8",
+            "data": "synthetic text (1 MiB, seed 1), reference-encoded (tests/golden/cfg1_blob.bin)",
+            "config": {"workload": "1 stream x 1 MiB, lc3/lp0/pb2, 64 KiB dict (BASELINE config 1)",
+                       "compressed_bytes": len(comp),
+                       "kernel_plan": {"kernel": plan_kernels(plan),
+                                       "placement": hex(plan.classes[0].lds_mask)
+                                       if plan.n_classes else None}},
+            "roofline": {"bound": "issue", "priced_against": "hbm", "achieved": round(achieved, 4),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 8), "traffic": None,
+                         "kernel": plan_kernels(plan), "kernel_avg_ms": round(dec_ms, 4),
+                         "alg_bytes_per_launch": alg},
+            "dropin_host_buffers": dropin,
+            "cpu_baseline": cpu, "verified": ok}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+    if not ok:
+        sys.exit(3)
+
+
 # ---------------------------------------------------------------- config 4
 
 CFG4_BLOCK = 1 << 20     # 1 MiB dict-reset blocks (Lzma2Enc.c MT layout)
@@ -312,9 +547,8 @@ def build_cfg4_unique(workers):
         return parts, [int(c) for c in crcs]
     t0 = time.time()
     parts, crcs = [None] * CFG4_UNIQUE, [0] * CFG4_UNIQUE
-    with mp.get_context("fork").Pool(workers) as pool:
-        for i, c, crc in pool.imap_unordered(_compress_lzma2_block, range(CFG4_UNIQUE)):
-            parts[i], crcs[i] = c, crc
+    for i, c, crc in pool_map(_compress_lzma2_block, range(CFG4_UNIQUE), workers):
+        parts[i], crcs[i] = c, crc
     np.savez(path, comp=np.frombuffer(b"".join(parts), dtype=np.uint8),
              lens=np.array([len(c) for c in parts], dtype=np.uint64),
              crcs=np.array(crcs, dtype=np.uint64))
@@ -398,9 +632,10 @@ def run_cfg4(args):
         if world > 1:
             D.scatter_ranges(d_file if rank == 0 else None, ranges, out_view, rank, world)
 
-    def decode():
+    def decode(res=None):
+        res = d_res if res is None else res
         r = L.decode_batch_device_ex(plan, d_desc.data_ptr(), d_order.data_ptr(), d_src.data_ptr(),
-                                     d_dst.data_ptr(), d_ws.data_ptr(), d_res.data_ptr(), sh)
+                                     d_dst.data_ptr(), d_ws.data_ptr(), res.data_ptr(), sh)
         if r != 0:
             raise RuntimeError("LzmaGpu_DecodeBatchEx failed: " + L.last_error())
 
@@ -408,6 +643,10 @@ def run_cfg4(args):
         scatter()
         decode()
     torch.cuda.synchronize()
+    d_res_steps = timed_buffers(torch, dev, d_dst, B, args.steps)
+    if world > 1:
+        out_view.fill_(0xA5)  # the scatter must deliver this rank's bytes again
+        torch.cuda.synchronize()
     D.barrier()
     torch.cuda.synchronize()
     ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
@@ -416,7 +655,7 @@ def run_cfg4(args):
         ev[i][0].record(stream)
         scatter()
         ev[i][1].record(stream)
-        decode()
+        decode(d_res_steps[i])
         ev[i][2].record(stream)
     torch.cuda.synchronize()
     D.barrier()
@@ -456,12 +695,13 @@ def run_cfg4(args):
                   "verified": D.all_true(g_ok, dev)}
         del whole
 
-    # verify: per-block results and the CRC of every decoded block (on the GPU)
-    res = np.frombuffer(d_res.cpu().numpy().tobytes(), dtype=np.dtype(
-        [("res", "<i4"), ("status", "<i4"), ("dest_len", "<u8"), ("src_len", "<u8")]))
+    # verify every timed launch: per-block results of each step, and the CRC of
+    # every decoded block (on the GPU) of the poisoned-then-decoded output
+    res = step_results(d_res_steps)
+    d_res = d_res_steps[args.steps - 1]
     ok = bool((res["res"] == 0).all() and (res["status"] == 2).all() and
-              (res["dest_len"] == np.array([u for _, _, u in mine])).all() and
-              (res["src_len"] == np.array([ln for _, ln, _ in mine])).all())
+              (res["dest_len"] == np.array([u for _, _, u in mine])[None, :]).all() and
+              (res["src_len"] == np.array([ln for _, ln, _ in mine])[None, :]).all())
     base, crange, total = L.crc32_plan_decoded(descs)
     d_base = torch.frombuffer(bytearray(base), dtype=torch.uint8).to(dev)
     d_range = torch.frombuffer(bytearray(crange), dtype=torch.uint8).to(dev)
@@ -476,7 +716,7 @@ def run_cfg4(args):
     ok = D.all_true(ok, dev)
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and not args.no_cpu_baseline:  # after the timed region, any world size
         cpu = cfg4_cpu_baseline(parts, cpus)
     total_bytes = world * B * CFG4_BLOCK * args.steps
     value = total_bytes / elapsed / 1e6
@@ -504,7 +744,7 @@ def run_cfg4(args):
                                     "gather": gather}},
             "roofline": {"bound": "issue", "priced_against": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
-                         "traffic": None, "kernel": "lzgpu_decode_lds_kernel",
+                         "traffic": None, "kernel": plan_kernels(plan),
                          "kernel_avg_ms": round(dec_ms, 4), "alg_bytes_per_launch": alg},
             "cpu_baseline": cpu, "verified": ok}), flush=True)
     if world > 1:
@@ -534,10 +774,9 @@ def build_cfg5(workers, first, count):
         return (z["comp"], z["lens"], z["props"], z["n"], z["fin"], z["crc"])
     t0 = time.time()
     out = [None] * count
-    with mp.get_context("fork").Pool(workers) as pool:
-        for i, c, props, n, fin, crc in pool.imap_unordered(
-                _cfg5_stream, range(first, first + count), chunksize=64):
-            out[i - first] = (c, props, n, fin, crc)
+    for i, c, props, n, fin, crc in pool_map(_cfg5_stream, range(first, first + count),
+                                             workers, chunksize=64):
+        out[i - first] = (c, props, n, fin, crc)
     comp = np.frombuffer(b"".join(o[0] for o in out), dtype=np.uint8)
     lens = np.array([len(o[0]) for o in out], dtype=np.uint64)
     props = np.frombuffer(b"".join(o[1] for o in out), dtype=np.uint8).reshape(count, 5)
@@ -589,35 +828,37 @@ def run_cfg5(args):
     stream = torch.cuda.current_stream(dev)
     sh = stream.cuda_stream
 
-    def step():
+    def step(res=None):
+        res = d_res if res is None else res
         r = L.decode_batch_device_ex(plan, d_desc.data_ptr(), d_order.data_ptr(), d_src.data_ptr(),
-                                     d_dst.data_ptr(), d_ws.data_ptr(), d_res.data_ptr(), sh)
+                                     d_dst.data_ptr(), d_ws.data_ptr(), res.data_ptr(), sh)
         if r != 0:
             raise RuntimeError("LzmaGpu_DecodeBatchEx failed: " + L.last_error())
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    d_res_steps = timed_buffers(torch, dev, d_dst, count, args.steps)
     D.barrier()
     torch.cuda.synchronize()
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
            for _ in range(args.steps)]
     t0 = time.perf_counter()
-    for a, b in evs:
+    for k, (a, b) in enumerate(evs):
         a.record(stream)
-        step()
+        step(d_res_steps[k])
         b.record(stream)
     torch.cuda.synchronize()
     D.barrier()
     torch.cuda.synchronize()
     elapsed = D.reduce_max(time.perf_counter() - t0, dev)
     dec_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
-    res = np.frombuffer(d_res.cpu().numpy().tobytes(), dtype=np.dtype(
-        [("res", "<i4"), ("status", "<i4"), ("dest_len", "<u8"), ("src_len", "<u8")]))
-    want_status = np.where(fin == 1, 1, 2)
+    res = step_results(d_res_steps)
+    d_res = d_res_steps[args.steps - 1]
+    want_status = np.where(fin == 1, 1, 2)[None, :]
     ok = bool((res["res"] == 0).all() and (res["status"] == want_status).all() and
-              (res["dest_len"] == nout).all() and
-              (res["src_len"][fin == 1] == lens[fin == 1]).all())
+              (res["dest_len"] == nout[None, :]).all() and
+              (res["src_len"][:, fin == 1] == lens[None, fin == 1]).all())
     base, crange, total = L.crc32_plan_decoded(descs)
     d_base = torch.frombuffer(bytearray(base), dtype=torch.uint8).to(dev)
     d_range = torch.frombuffer(bytearray(crange), dtype=torch.uint8).to(dev)
@@ -632,7 +873,7 @@ def run_cfg5(args):
     alg = int(lens.sum()) + 5 * count + total_out
     achieved = alg / (dec_ms * 1e-3) / 1e9
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and not args.no_cpu_baseline:  # after the timed region, any world size
         thr = cpus
         m = min(count, 2048)
         orc_n = nout[:m]
@@ -658,7 +899,7 @@ def run_cfg5(args):
                        "kernel_plan": {"lds_streams": int(plan.n_lds), "classes": cls}},
             "roofline": {"bound": "issue", "priced_against": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
-                         "traffic": None, "kernel": "lzgpu_decode_lds_kernel",
+                         "traffic": None, "kernel": plan_kernels(plan),
                          "kernel_avg_ms": round(dec_ms, 4), "alg_bytes_per_launch": alg},
             "cpu_baseline": cpu, "verified": ok}), flush=True)
     if world > 1:
@@ -742,7 +983,7 @@ def cfg4_cpu_baseline(parts, threads):
     dt1, _ = run(sample[:8], 1)
     return {"value": round(len(sample) * CFG4_BLOCK / dt / 1e6, 2), "unit": "MB/s",
             "cores": threads, "kind": kind,
-            "impl": "oracle/_ref/libref.so: the reference's Lzma2Dec.c + LzmaDec.c compiled in "
+            "impl": "oracle/_ref/libref_lzma.so: the reference's Lzma2Dec.c + LzmaDec.c compiled in "
                     "place" if kind == "reference" else "oracle/lzma_oracle.c restatement",
             "sample": f"{len(sample)} distinct 1 MiB blocks, {threads} threads, {dt:.2f}s; "
                       f"1-core: 8 blocks in {dt1:.2f}s",
@@ -751,7 +992,7 @@ def cfg4_cpu_baseline(parts, threads):
 
 def cpu_baseline(comp, lens, offs, n, props, threads, sample_streams, impl="port"):
     """A CPU LzmaDecode over a bounded sample: impl "reference" = the reference's
-    own LzmaDec.c (oracle/_ref/libref.so, compiled in place with gcc -O2),
+    own LzmaDec.c (oracle/_ref/libref_lzma.so, compiled in place with gcc -O2),
     "port" = the oracle restatement (oracle/liboracle.so)."""
     import native
     m = min(sample_streams, len(lens))
@@ -822,9 +1063,8 @@ def build_xz_file(workers, nblocks):
     else:
         t0 = time.time()
         parts = [None] * XZ_UNIQUE
-        with mp.get_context("fork").Pool(workers) as pool:
-            for i, blk, unp, n in pool.imap_unordered(_xz_unique_block, range(XZ_UNIQUE)):
-                parts[i] = (blk, unp, n)
+        for i, blk, unp, n in pool_map(_xz_unique_block, range(XZ_UNIQUE), workers):
+            parts[i] = (blk, unp, n)
         np.savez(path, blob=np.frombuffer(b"".join(p[0] for p in parts), dtype=np.uint8),
                  meta=np.array([(len(p[0]), p[1], p[2]) for p in parts], dtype=np.uint64))
         log(f"[xz] encoded {XZ_UNIQUE} blocks in {time.time() - t0:.1f}s")
@@ -889,11 +1129,12 @@ def run_xz(args):
     stream = torch.cuda.current_stream(dev)
     sh = stream.cuda_stream
 
-    def step(ev=None):
+    def step(ev=None, res=None):
+        res = d_res if res is None else res
         if ev:
             ev[0].record(stream)
         if L.decode_batch_device_ex(plan, d_desc.data_ptr(), d_order.data_ptr(), d_src.data_ptr(),
-                                    d_dst.data_ptr(), d_ws.data_ptr(), d_res.data_ptr(), sh):
+                                    d_dst.data_ptr(), d_ws.data_ptr(), res.data_ptr(), sh):
             raise RuntimeError(L.last_error())
         if ev:
             ev[1].record(stream)
@@ -913,25 +1154,27 @@ def run_xz(args):
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    d_res_steps = timed_buffers(torch, dev, d_dst, n, args.steps)
+    d_crc.fill_(-1)
     D.barrier()
     torch.cuda.synchronize()
     evs = [[torch.cuda.Event(enable_timing=True) for _ in range(4)] for _ in range(args.steps)]
     t0 = time.perf_counter()
     for i in range(args.steps):
-        step(evs[i])
+        step(evs[i], d_res_steps[i])
     torch.cuda.synchronize()
     D.barrier()
     torch.cuda.synchronize()
     elapsed = D.reduce_max(time.perf_counter() - t0, dev)
     ms = [float(np.mean([e[k].elapsed_time(e[k + 1]) for e in evs])) for k in range(3)]
-    # verify: every block decoded whole and its CRC-64 equals the stored check
-    res = np.frombuffer(d_res.cpu().numpy().tobytes(), dtype=np.int64).reshape(n, 3)
+    # verify every timed launch: each step's block results, and the CRC-64 of
+    # every block of the poisoned-then-decoded output equals the stored check
+    allres = step_results(d_res_steps)
     crc = d_crc.cpu().numpy().astype(np.uint64)
     want = np.array([int.from_bytes(xz[b.check_off:b.check_off + 8], "little") for b in blocks],
                     dtype=np.uint64)
-    res32 = np.frombuffer(d_res.cpu().numpy().tobytes(), dtype=np.int32).reshape(n, 6)
-    ok = bool((res32[:, 0] == 0).all() and (res32[:, 1] == 1).all() and
-              (res[:, 1] == np.array(lens)).all() and (crc == want).all())
+    ok = bool((allres["res"] == 0).all() and (allres["status"] == 1).all() and
+              (allres["dest_len"] == np.array(lens)[None, :]).all() and (crc == want).all())
     ok = D.all_true(ok, dev)
     comp_bytes = len(xz)
     value = total * world * args.steps / elapsed / 1e6
@@ -950,7 +1193,7 @@ def run_xz(args):
                        "kernel_ms": {"lzma2_batch": round(ms[0], 4), "bcj_x86": round(ms[1], 4),
                                      "crc64": round(ms[2], 4)},
                        "parallelism": f"{world} rank(s), one xz file each, no collective"},
-            "roofline": {"bound": "issue", "priced_against": "hbm", "kernel": "lzgpu_decode_lds_kernel (LZMA2 items)",
+            "roofline": {"bound": "issue", "priced_against": "hbm", "kernel": f"{plan_kernels(plan)} (LZMA2 items)",
                          "achieved": round(dec_gbps, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(dec_gbps / HBM_PEAK_GBS, 6), "traffic": None,
                          "alg_bytes_per_launch": alg_dec},
@@ -1032,11 +1275,12 @@ def run_7z(args):
     stream = torch.cuda.current_stream(dev)
     sh = stream.cuda_stream
 
-    def step(ev=None):
+    def step(ev=None, res=None):
+        res = d_res if res is None else res
         if ev:
             ev[0].record(stream)
         if L.decode_batch_device_ex(plan, d_desc.data_ptr(), d_order.data_ptr(), d_src.data_ptr(),
-                                    d_dst.data_ptr(), d_ws.data_ptr(), d_res.data_ptr(), sh):
+                                    d_dst.data_ptr(), d_ws.data_ptr(), res.data_ptr(), sh):
             raise RuntimeError(L.last_error())
         if ev:
             ev[1].record(stream)
@@ -1050,23 +1294,25 @@ def run_7z(args):
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    d_res_steps = timed_buffers(torch, dev, d_dst, n, args.steps)
+    d_crc.fill_(-1)
     D.barrier()
     torch.cuda.synchronize()
     evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
     t0 = time.perf_counter()
     for i in range(args.steps):
-        step(evs[i])
+        step(evs[i], d_res_steps[i])
     torch.cuda.synchronize()
     D.barrier()
     torch.cuda.synchronize()
     elapsed = D.reduce_max(time.perf_counter() - t0, dev)
     ms = [float(np.mean([e[k].elapsed_time(e[k + 1]) for e in evs])) for k in range(2)]
-    res32 = np.frombuffer(d_res.cpu().numpy().tobytes(), dtype=np.int32).reshape(n, 6)
-    res64 = np.frombuffer(d_res.cpu().numpy().tobytes(), dtype=np.int64).reshape(n, 3)
+    allres = step_results(d_res_steps)
     crc = d_crc.cpu().numpy().astype(np.uint32)
     want = np.array([f.crc for f in files], dtype=np.uint32)
-    ok = bool((res32[:, 0] == 0).all() and (res64[:, 1] == np.array([f.unpack_size for f in folders])).all()
-              and (res64[:, 2] == np.array([f.pack_size for f in folders])).all()
+    ok = bool((allres["res"] == 0).all()
+              and (allres["dest_len"] == np.array([f.unpack_size for f in folders])[None, :]).all()
+              and (allres["src_len"] == np.array([f.pack_size for f in folders])[None, :]).all()
               and (crc == want).all())
     # the C-ABI call end to end once (host buffers: upload, open, decode, CRCs, download)
     t0 = time.perf_counter()
@@ -1092,7 +1338,7 @@ def run_7z(args):
                        "open_ms_host": round(open_ms, 3),
                        "extract_api_ms_pcie_inclusive": round(api_ms, 3),
                        "parallelism": f"{world} rank(s), one archive each, no collective"},
-            "roofline": {"bound": "issue", "priced_against": "hbm", "kernel": "lzgpu_decode_lds_kernel (7z LZMA folders)",
+            "roofline": {"bound": "issue", "priced_against": "hbm", "kernel": f"{plan_kernels(plan)} (7z LZMA folders)",
                          "achieved": round(dec_gbps, 3), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(dec_gbps / HBM_PEAK_GBS, 6), "traffic": None,
                          "alg_bytes_per_launch": alg_dec},
@@ -1284,8 +1530,11 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
                     help="weak: a full batch per GPU; strong: one batch split over the GPUs")
-    ap.add_argument("--config", default="cfg3", choices=sorted(CONFIGS) + ["cfg4", "cfg5", "xz", "7z"])
-    ap.add_argument("--streams", type=int, default=0, help="cfg5: streams per GPU (32768)")
+    ap.add_argument("--config", default="cfg3",
+                    choices=sorted(CONFIGS) + ["cfg1", "cfg4", "cfg5", "xz", "7z"])
+    ap.add_argument("--streams", type=int, default=0,
+                    help="streams per GPU: cfg5 (default 32768), or a share of cfg3 / cfg2's "
+                         "batch (strong-scaling emulation on one GPU)")
     ap.add_argument("--blocks", type=int, default=1024, help="cfg4: LZMA2 blocks per GPU")
     ap.add_argument("--no-gather", action="store_true",
                     help="cfg4: skip the optional gather of decoded blocks on rank 0")
@@ -1302,6 +1551,8 @@ def main():
         return launch_ranks(args.gpus)  # spawns the ranks; touches no GPU here
     if args.dry_run:
         return run_dry(args)
+    if args.config == "cfg1":
+        return run_cfg1(args)
     if args.config == "cfg4":
         return run_cfg4(args)
     if args.config == "cfg5":
@@ -1319,9 +1570,23 @@ def main():
     workers = max(1, min(16, cpu["usable"] // max(1, world) if world > 1 else cpu["usable"]))
 
     count_cfg, n, lc, lp, pb, dsz, desc_txt = CONFIGS[args.config]
+    if args.streams:
+        # a per-GPU share of the config's batch on one GPU (strong-scaling
+        # emulation: 65,536 / N streams of config 3, 4,096 / N of config 2)
+        count_cfg = args.streams
+        desc_txt = f"{count_cfg} of the {CONFIGS[args.config][0]} streams of " + desc_txt
     first, count = rank_streams(count_cfg, world, rank, args.scaling)
     # workload first: the compression pool forks before this process touches the GPU
-    plain, comp, lens, props = build_workload(args.config, first, count, workers)
+    if args.streams and world == 1 and count <= CONFIGS[args.config][0]:
+        # a share of the full batch: its first `count` streams (one cached encode
+        # serves every share of the sweep)
+        full = CONFIGS[args.config][0]
+        plain, comp, lens, props = build_workload(args.config, 0, full, workers)
+        plain = plain[:count * n]
+        comp = comp[:int(lens[:count].sum())]
+        lens = lens[:count]
+    else:
+        plain, comp, lens, props = build_workload(args.config, first, count, workers)
 
     import torch
     import torch.distributed as dist
@@ -1342,15 +1607,17 @@ def main():
     stream = torch.cuda.current_stream(dev)
     sh = stream.cuda_stream
 
-    def step():
+    def step(res=None):
+        res = d_res if res is None else res
         r = L.decode_batch_device_ex(plan, d_desc.data_ptr(), d_order.data_ptr(), d_src.data_ptr(),
-                                     d_dst.data_ptr(), d_ws.data_ptr(), d_res.data_ptr(), sh)
+                                     d_dst.data_ptr(), d_ws.data_ptr(), res.data_ptr(), sh)
         if r != 0:
             raise RuntimeError("LzmaGpu_DecodeBatch failed: " + L.last_error())
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    d_res_steps = timed_buffers(torch, dev, d_dst, count, args.steps)
     D.barrier()
     torch.cuda.synchronize()
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -1358,7 +1625,7 @@ def main():
     t0 = time.perf_counter()
     for i in range(args.steps):
         evs[i][0].record(stream)
-        step()
+        step(d_res_steps[i])
         evs[i][1].record(stream)
     torch.cuda.synchronize()
     D.barrier()
@@ -1367,17 +1634,17 @@ def main():
     kern_ms = [a.elapsed_time(b) for a, b in evs]
     elapsed = D.reduce_max(elapsed_mine, dev)  # slowest rank sets the job time
 
-    # ---- verify (bit-exact vs plaintext + per-stream result invariants)
-    res = np.frombuffer(d_res.cpu().numpy().tobytes(), dtype=np.dtype(
-        [("res", "<i4"), ("status", "<i4"), ("dest_len", "<u8"), ("src_len", "<u8")]))
-    ok = bool((res["res"] == 0).all() and (res["status"] == 1).all() and
-              (res["dest_len"] == n).all() and (res["src_len"] == lens).all())
+    # ---- verify every timed launch (bit-exact vs plaintext + exact results)
+    allres = step_results(d_res_steps)
+    ok = bool((allres["res"] == 0).all() and (allres["status"] == 1).all() and
+              (allres["dest_len"] == n).all() and (allres["src_len"] == lens[None, :]).all())
     out = d_dst.cpu().numpy()
     ok = ok and bool(np.array_equal(out, plain))
     ok = D.all_true(ok, dev)
     if not ok:
-        log(f"[rank {rank}] VERIFY FAILED: res={np.unique(res['res'])} "
-            f"status={np.unique(res['status'])}")
+        log(f"[rank {rank}] VERIFY FAILED: res={np.unique(allres['res'])} "
+            f"status={np.unique(allres['status'])}")
+    d_res = d_res_steps[args.steps - 1]
 
     print_prof(L)
     crc = measure_crc(L, torch, descs, d_desc, d_res, d_dst, plain, count, n, stream, dev,
@@ -1405,13 +1672,15 @@ def main():
                           "e2e_MBps": e2e["value"] if e2e else None})
 
     cpu_base = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and not args.no_cpu_baseline:
+        # rank 0 after the timed region at every world size (the
+        # reference CPU path timed in the same run); the job's whole CPU quota
         import native
         thr = cpu["usable"]
         kind = "reference" if native.have_ref() else "port"
         v, dt, m, errs = cpu_baseline(comp, lens, offs, n, props, thr, count, kind)
         v1, dt1, m1, _ = cpu_baseline(comp, lens, offs, n, props, 1, max(64, count // 32), kind)
-        impl = ("oracle/_ref/libref.so: the reference's own LzmaDec.c (LzmaDecode, "
+        impl = ("oracle/_ref/libref_lzma.so: the reference's own LzmaDec.c (LzmaDecode, "
                 "LzmaDec.c:972) compiled in place with gcc -O2 by oracle/Makefile.ref"
                 if kind == "reference" else
                 "oracle/lzma_oracle.c: this build's C restatement of LzmaDec.c "
@@ -1436,7 +1705,7 @@ def main():
     secondary = None
     if rank == 0 and world == 1 and args.config == "cfg3" and not args.no_secondary:
         # reported with their own `verified`; the headline's stands on config 3 alone
-        secondary = run_secondary(("cfg2", "cfg4", "cfg5"))
+        secondary = run_secondary(("cfg1", "cfg2", "cfg4", "cfg5"))
 
     if rank == 0:
         line = {
@@ -1464,8 +1733,7 @@ def main():
                          "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
                          "traffic": traffic,
-                         "kernel": "lzgpu_decode_lds_kernel" if plan.n_lds else
-                                   "lzgpu_decode_batch_kernel",
+                         "kernel": plan_kernels(plan),
                          "kernel_avg_ms": round(avg_kern_ms, 4),
                          "alg_bytes_per_launch": alg_bytes,
                          "issue": issue,

@@ -144,6 +144,19 @@ SRes LzmaDecode(Byte *dest, SizeT *destLen, const Byte *src, SizeT *srcLen,
                 const Byte *propData, unsigned propSize, ELzmaFinishMode finishMode,
                 ELzmaStatus *status, ISzAlloc *alloc);
 
+/* Device mirror of a decoder (dictionary interface).  LzmaDec_DecodeToDic /
+ * LzmaDec_DecodeToBuf keep the decoder's dictionary, probability table and
+ * state on the GPU between calls (keyed by the CLzmaDec address, its dic,
+ * dicBufSize and probs allocation, and the current device): a call uploads
+ * its input only -- plus, once per mirror, the dictionary history a
+ * continuing decoder needs -- and downloads the bytes it decoded, the state
+ * and the table.  Bytes of dic the CALLER writes between calls are not seen
+ * by the decoder while the mirror lives; LzmaGpu_DecoderRelease(p) drops it
+ * (as do LzmaDec_FreeProbs / LzmaDec_Free and any change of dic, dicBufSize
+ * or probs), so the next call starts from the host copy.  Mirrors beyond
+ * 256 decoders or 16 GiB are evicted least recently used first. */
+void LzmaGpu_DecoderRelease(const CLzmaDec *p);
+
 /* ---------------------------------------------------------------- drop-in LzmaLib.h */
 
 int LzmaUncompress(unsigned char *dest, size_t *destLen, const unsigned char *src,
@@ -320,6 +333,12 @@ typedef struct LzmaGpuPlanOptions {
 /* A/B: interleaved rows for throughput waves of any width up to 64 lanes, not
  * only whole 32-lane groups (LZGPU_ILV_ANY=1) */
 #define LZMA_GPU_PLAN_ILV_ANY 32u
+/* throughput classes whose batch does not fill the CU at full wave width
+ * (fewer than lanes x workgroups streams per CU, e.g. a strong-scaling share)
+ * run narrower waves at the same workgroups per CU instead of full-width
+ * waves on part of the SIMDs, and the throughput regime starts at 16 streams
+ * per CU instead of 64 (LZGPU_THR_FIT=1) */
+#define LZMA_GPU_PLAN_THR_FIT 64u
 
 /* LzmaGpu_PlanBatchEx with explicit options (opt == NULL: as PlanBatchEx,
  * whose defaults take the LZGPU_* experiment variables of the environment,

@@ -1,0 +1,809 @@
+// dropin_capi.hip -- the drop-in decoder symbols of LzmaDec.h, LzmaLib.h and
+// Lzma2Dec.h (include/lzma_gpu.h part 1).
+//
+// Every decode runs on the GPU.  What stays on the host is what the reference
+// keeps outside its decoder loop: property parsing (LzmaDec.c:898-922),
+// ISzAlloc bookkeeping (LzmaDec.c:880-970) and the LZMA2 chunk-header walk of
+// the streaming interface (Lzma2Dec.c:170-328), whose LZMA chunks are decoded by
+// the GPU LzmaDec_DecodeToDic.
+//
+// One-call decodes (LzmaDecode, LzmaUncompress, Lzma2Decode) are one-item
+// batches planned onto the wave-cooperative kernel (whole table in LDS where it
+// fits): upload the compressed bytes, decode, download the output.
+//
+// The dictionary interface keeps a DEVICE MIRROR per decoder object (keyed by
+// the CLzmaDec address, its dic / dicBufSize / probs and the device): the
+// dictionary, the probability table and the session state stay on the GPU
+// between calls, so a call uploads only its input (plus, once per mirror, the
+// history a continuing decoder needs) and downloads only the bytes it decoded,
+// the ~200-byte state and the table.  The 7zDec pattern (16 KiB look windows over
+// a whole-folder dic, 7zDec.c:133-171) is therefore linear in the folder size;
+// round 2 re-uploaded the whole dicBufSize every call.  DecodeToBuf runs its
+// whole ring loop (LzmaDec.c:840-878) in ONE launch on the device ring and
+// downloads the caller's output once; the host ring is rebuilt from it.
+//
+// The mirror's contract: bytes of `dic` the caller writes between calls (other
+// than through this library) are not seen by the decoder unless `dic`,
+// `dicBufSize` or the probs allocation change, or LzmaGpu_DecoderRelease(p) is
+// called -- the reference reads them (its dictionary IS the caller's buffer).
+// No caller in the reference does that; every decoder-written byte is
+// downloaded, so host and device copies agree.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstddef>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <exception>
+#include <memory>
+#include <mutex>
+#include <new>
+#include <vector>
+
+#include "lzma_device.h"
+#include "lzma_gpu_internal.h"
+
+using lzgpu_host::CallScratch;
+using lzgpu_host::DevBuf;
+using lzgpu_host::ensure_device;
+using lzgpu_host::hip_ok;
+using lzgpu_host::set_error;
+
+namespace {
+
+uint32_t probs_for(uint32_t lc, uint32_t lp) { return lzgpu::num_probs(lc, lp); }
+
+// RAII borrow of a pooled call scratch (buffers + its own stream)
+struct ScratchLease {
+  CallScratch* s = lzgpu_host::scratch_acquire();
+  ~ScratchLease() {
+    if (s) {
+      (void)hipStreamSynchronize(s->stream);
+      lzgpu_host::scratch_release(s);
+    }
+  }
+};
+
+// ------------------------------------------------------------------ one-call decodes
+
+// LzmaDecode-style one call over host buffers: a one-item batch on the
+// cooperative kernel (LzmaGpu_PlanBatchOpt with LZMA_GPU_KERNEL_COOP: one
+// 32-lane wave, the whole table in LDS where it fits -- the generic all-global
+// kernel only for lc + lp too wide for LDS).
+SRes gpu_one_call(uint8_t kind, Byte* dest, SizeT* destLen, const Byte* src, SizeT* srcLen,
+                  const Byte* props, unsigned propSize, ELzmaFinishMode finishMode,
+                  int* status_out) {
+  const SizeT in_size = *srcLen, out_size = *destLen;
+  *srcLen = 0;
+  *destLen = 0;
+  if (!ensure_device()) return SZ_ERROR_FAIL;
+  struct Meta {  // one upload: the descriptor and its lane order
+    LzmaGpuStreamDesc d;
+    uint32_t order;
+    uint32_t pad[3];
+  } m;
+  memset(&m, 0, sizeof m);
+  m.d.src_len = in_size;
+  m.d.dst_cap = out_size;
+  memcpy(m.d.props, props, std::min<unsigned>(propSize, 5));
+  m.d.props_size = uint8_t(std::min<unsigned>(propSize, 255));
+  m.d.finish_mode = uint8_t(finishMode);
+  m.d.kind = kind;
+  LzmaGpuPlan plan;
+  LzmaGpuPlanOptions o;
+  memset(&o, 0, sizeof o);
+  o.kernel = LZMA_GPU_KERNEL_COOP;
+  {
+    const SRes pr = LzmaGpu_PlanBatchOpt(&m.d, 1, &m.order, &plan, &o);
+    if (pr != SZ_OK) return pr;
+  }
+  ScratchLease L;
+  if (!L.s) return SZ_ERROR_FAIL;
+  CallScratch& S = *L.s;
+  const size_t in_pad = (size_t(in_size) + 15) & ~size_t(15);
+  uint8_t* d_io = static_cast<uint8_t*>(S.buf[0].get(in_pad + out_size + 16));
+  void* d_ws = S.buf[1].get(size_t(plan.workspace_bytes));
+  uint8_t* d_meta = static_cast<uint8_t*>(S.buf[2].get(sizeof(Meta) + sizeof(LzmaGpuResult)));
+  if (!d_io || !d_ws || !d_meta) {
+    set_error("LzmaDecode: device allocation failed");
+    return SZ_ERROR_MEM;
+  }
+  const hipStream_t st = S.stream;
+  LzmaGpuResult r;
+  if (in_size && !hip_ok(hipMemcpyAsync(d_io, src, in_size, hipMemcpyHostToDevice, st), "upload src"))
+    return SZ_ERROR_FAIL;
+  if (!hip_ok(hipMemcpyAsync(d_meta, &m, sizeof m, hipMemcpyHostToDevice, st), "upload desc"))
+    return SZ_ERROR_FAIL;
+  LzmaGpuResult* d_res = reinterpret_cast<LzmaGpuResult*>(d_meta + sizeof(Meta));
+  if (LzmaGpu_DecodeBatchEx(&plan, reinterpret_cast<LzmaGpuStreamDesc*>(d_meta),
+                            reinterpret_cast<uint32_t*>(d_meta + offsetof(Meta, order)), d_io,
+                            d_io + in_pad, d_ws, d_res, st) != SZ_OK)
+    return SZ_ERROR_FAIL;
+  if (!hip_ok(hipMemcpyAsync(&r, d_res, sizeof r, hipMemcpyDeviceToHost, st), "download result") ||
+      !hip_ok(hipStreamSynchronize(st), "decode kernel"))
+    return SZ_ERROR_FAIL;
+  if (r.dest_len > out_size) {
+    set_error("LzmaDecode: kernel reported more output than its capacity");
+    return SZ_ERROR_FAIL;
+  }
+  if (r.dest_len &&
+      (!hip_ok(hipMemcpyAsync(dest, d_io + in_pad, r.dest_len, hipMemcpyDeviceToHost, st),
+               "download output") ||
+       !hip_ok(hipStreamSynchronize(st), "download output")))
+    return SZ_ERROR_FAIL;
+  *destLen = r.dest_len;
+  *srcLen = r.src_len;
+  *status_out = r.status;
+  return r.res;
+}
+
+// ------------------------------------------------------------------ dictionary mirrors
+
+struct Mirror {
+  const CLzmaDec* key = nullptr;
+  int dev = 0;
+  const Byte* dic = nullptr;
+  SizeT dic_buf_size = 0;
+  const CLzmaProb* probs = nullptr;
+  uint32_t num_probs = 0;
+  DevBuf block;  // [session | probs | dic]
+  DevBuf io;     // this call's input (+ DecodeToBuf output)
+  bool history = false;    // device dic holds every byte the decoder wrote since its dic init
+  bool probs_dev = false;  // device table == host table (downloaded after every call)
+  uint64_t tick = 0;
+  std::mutex busy;  // one call at a time per decoder object (the reference's contract)
+};
+
+constexpr size_t kSessBytes = 256;  // LzgpuSession (192 B) rounded up
+constexpr size_t kMirrorMaxCount = 256;
+constexpr size_t kMirrorMaxBytes = size_t(16) << 30;
+
+struct Registry {
+  std::mutex mu;
+  std::vector<std::shared_ptr<Mirror>> v;
+  uint64_t tick = 0;
+};
+Registry& registry() {
+  static Registry* r = new Registry();  // process lifetime (HIP teardown order)
+  return *r;
+}
+
+size_t probs_area(uint32_t num_probs) { return (size_t(num_probs) * 2 + 255) & ~size_t(255); }
+
+// The mirror of decoder p on device dev (created on first use).  A mirror whose
+// dic / dicBufSize / probs allocation no longer match p is reset: its device
+// copies no longer describe p.  Least recently used mirrors nobody is using are
+// evicted beyond kMirrorMaxCount or kMirrorMaxBytes (an evicted decoder's next
+// call rebuilds its mirror: correctness never depends on one existing).
+std::shared_ptr<Mirror> mirror_get(const CLzmaDec* p, int dev) {
+  Registry& R = registry();
+  std::lock_guard<std::mutex> g(R.mu);
+  std::shared_ptr<Mirror> m;
+  for (auto& e : R.v)
+    if (e->key == p && e->dev == dev) {
+      m = e;
+      break;
+    }
+  if (!m) {
+    m = std::make_shared<Mirror>();
+    m->key = p;
+    m->dev = dev;
+    R.v.push_back(m);
+  }
+  if (m->dic != p->dic || m->dic_buf_size != p->dicBufSize || m->probs != p->probs ||
+      m->num_probs != p->numProbs) {
+    m->dic = p->dic;
+    m->dic_buf_size = p->dicBufSize;
+    m->probs = p->probs;
+    m->num_probs = p->numProbs;
+    m->history = false;
+    m->probs_dev = false;
+  }
+  m->tick = ++R.tick;
+  // eviction: oldest idle mirrors first
+  size_t bytes = 0;
+  for (auto& e : R.v) bytes += e->block.cap + e->io.cap;
+  while (R.v.size() > kMirrorMaxCount || bytes > kMirrorMaxBytes) {
+    size_t victim = R.v.size();
+    for (size_t i = 0; i < R.v.size(); ++i)
+      if (R.v[i].use_count() == 1 && (victim == R.v.size() || R.v[i]->tick < R.v[victim]->tick))
+        victim = i;
+    if (victim == R.v.size()) break;  // all in use
+    bytes -= R.v[victim]->block.cap + R.v[victim]->io.cap;
+    R.v.erase(R.v.begin() + ptrdiff_t(victim));
+  }
+  return m;
+}
+
+// existing mirror of p on dev, or null
+std::shared_ptr<Mirror> mirror_find(const CLzmaDec* p, int dev) {
+  Registry& R = registry();
+  std::lock_guard<std::mutex> g(R.mu);
+  for (auto& e : R.v)
+    if (e->key == p && e->dev == dev) return e;
+  return nullptr;
+}
+
+void mirror_drop(const CLzmaDec* p) {
+  Registry& R = registry();
+  std::lock_guard<std::mutex> g(R.mu);
+  R.v.erase(std::remove_if(R.v.begin(), R.v.end(),
+                           [&](const std::shared_ptr<Mirror>& e) { return e->key == p; }),
+            R.v.end());
+}
+
+// The host wrote dic[off, off + n) itself (an LZMA2 stored chunk,
+// Lzma2Dec.c:159-166): write it through to the device copy.  Without a live
+// mirror there is nothing to keep in step (the next call rebuilds it).
+bool mirror_host_wrote(const CLzmaDec* p, SizeT off, SizeT n) {
+  if (n == 0) return true;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return false;
+  std::shared_ptr<Mirror> m = mirror_find(p, dev);
+  if (!m) return true;
+  std::lock_guard<std::mutex> busy(m->busy);
+  if (m->dic != p->dic || m->dic_buf_size != p->dicBufSize || !m->history || !m->block.p)
+    return true;  // stale or not yet holding history: rebuilt from the host on next use
+  ScratchLease L;
+  uint8_t* d_dic = static_cast<uint8_t*>(m->block.p) + kSessBytes + probs_area(m->num_probs);
+  if (!L.s ||
+      !hip_ok(hipMemcpyAsync(d_dic + off, p->dic + off, n, hipMemcpyHostToDevice, L.s->stream),
+              "dictionary write-through") ||
+      !hip_ok(hipStreamSynchronize(L.s->stream), "dictionary write-through")) {
+    m->history = false;
+    return false;
+  }
+  return true;
+}
+
+// One LzmaDec_DecodeToDic (mode 0) or LzmaDec_DecodeToBuf (mode 1) call on the
+// GPU over a host CLzmaDec, through its mirror.
+SRes gpu_session_call(CLzmaDec* p, int mode, SizeT dicLimit, const Byte* src, SizeT in_size,
+                      SizeT* in_used, Byte* dest, SizeT* destLen, ELzmaFinishMode finishMode,
+                      ELzmaStatus* status) {
+  int dev = 0;
+  if (!hip_ok(hipGetDevice(&dev), "current device")) return SZ_ERROR_FAIL;
+  const uint32_t cells = lzgpu::table_cells(p->prop.lc, p->prop.lp, p->prop.pb);
+  if (p->probs == nullptr || cells > p->numProbs) {
+    set_error("LzmaDec: probabilities not allocated for the current props");
+    return SZ_ERROR_PARAM;
+  }
+  std::shared_ptr<Mirror> m;
+  try {
+    m = mirror_get(p, dev);
+  } catch (const std::exception&) {
+    set_error("LzmaDec: host allocation failed");
+    return SZ_ERROR_MEM;
+  }
+  std::lock_guard<std::mutex> busy(m->busy);
+  ScratchLease L;
+  if (!L.s) return SZ_ERROR_FAIL;
+  const hipStream_t st = L.s->stream;
+  const size_t pa = probs_area(p->numProbs);
+  const size_t out_room = mode == 1 ? size_t(*destLen) : 0;
+  const void* blk_before = m->block.p;
+  uint8_t* blk = static_cast<uint8_t*>(m->block.get(kSessBytes + pa + p->dicBufSize + 16));
+  const size_t in_pad = (size_t(in_size) + 15) & ~size_t(15);
+  uint8_t* d_io = static_cast<uint8_t*>(m->io.get(in_pad + out_room + 16));
+  if (!blk || !d_io) {
+    m->history = m->probs_dev = false;
+    set_error("LzmaDec: device allocation failed");
+    return SZ_ERROR_MEM;
+  }
+  if (blk != blk_before) m->history = m->probs_dev = false;  // fresh or regrown: nothing held
+  LzgpuSession* d_sess = reinterpret_cast<LzgpuSession*>(blk);
+  uint16_t* d_probs = reinterpret_cast<uint16_t*>(blk + kSessBytes);
+  uint8_t* d_dic = blk + kSessBytes + pa;
+
+  auto fail = [&](const char* what) {
+    (void)hipStreamSynchronize(st);
+    m->history = m->probs_dev = false;  // device state unknown; the host object is untouched
+    set_error(what);
+    return SZ_ERROR_FAIL;
+  };
+  // the table: the device copy is current after every successful call
+  if (!m->probs_dev &&
+      hipMemcpyAsync(d_probs, p->probs, size_t(cells) * 2, hipMemcpyHostToDevice, st) != hipSuccess)
+    return fail("LzmaDec: upload probs");
+  // history: only a decoder continuing a dictionary reads bytes it did not
+  // write in this call (LzmaDec.c:165-166,176,216,376-408 read dic only when
+  // processedPos or checkDicSize is non-zero); uploaded once per mirror
+  const bool need_hist = p->processedPos != 0 || p->checkDicSize != 0;
+  if (need_hist && !m->history && p->dicBufSize &&
+      hipMemcpyAsync(d_dic, p->dic, p->dicBufSize, hipMemcpyHostToDevice, st) != hipSuccess)
+    return fail("LzmaDec: upload dictionary");
+  if (in_size && hipMemcpyAsync(d_io, src, in_size, hipMemcpyHostToDevice, st) != hipSuccess)
+    return fail("LzmaDec: upload src");
+
+  LzgpuSession q;
+  memset(&q, 0, sizeof q);
+  q.lc = p->prop.lc;
+  q.lp = p->prop.lp;
+  q.pb = p->prop.pb;
+  q.dict_size = p->prop.dicSize;
+  q.probs = d_probs;
+  q.dic = d_dic;
+  q.in = d_io;
+  q.dic_buf_size = p->dicBufSize;
+  q.dic_pos = p->dicPos;
+  q.dic_limit = dicLimit;
+  q.in_len = in_size;
+  q.range = p->range;
+  q.code = p->code;
+  q.processed_pos = p->processedPos;
+  q.check_dic_size = p->checkDicSize;
+  q.state = p->state;
+  for (int i = 0; i < 4; ++i) q.reps[i] = p->reps[i];
+  q.remain_len = p->remainLen;
+  q.need_flush = p->needFlush ? 1 : 0;
+  q.need_init_state = p->needInitState ? 1 : 0;
+  q.temp_buf_size = p->tempBufSize;
+  memcpy(q.temp_buf, p->tempBuf, LZMA_REQUIRED_INPUT_MAX);
+  q.finish_mode = finishMode;
+  q.mode = mode;
+  q.out = d_io + in_pad;
+  q.out_len = out_room;
+  const SizeT pos0 = p->dicPos;
+  if (hipMemcpyAsync(d_sess, &q, sizeof q, hipMemcpyHostToDevice, st) != hipSuccess)
+    return fail("LzmaDec: upload session");
+  const int lr = cells <= kSessCoopMaxCells ? lzgpu_launch_session_coop(d_sess, 1, cells, 1, st)
+                                            : lzgpu_launch_session(d_sess, 1, st);
+  if (lr != 0) return fail("LzmaDec: session kernel launch failed");
+  // state + table back in one copy (the table sits right after the state)
+  std::vector<uint8_t> back;
+  try {
+    back.resize(kSessBytes + size_t(cells) * 2);
+  } catch (const std::exception&) {
+    (void)hipStreamSynchronize(st);
+    m->history = m->probs_dev = false;
+    set_error("LzmaDec: host allocation failed");
+    return SZ_ERROR_MEM;
+  }
+  if (hipMemcpyAsync(back.data(), blk, back.size(), hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess)
+    return fail("LzmaDec: session kernel");
+  memcpy(&q, back.data(), sizeof q);
+  // the decoded bytes: DecodeToDic's new dictionary bytes, DecodeToBuf's output
+  if (mode == 0) {
+    if (q.dic_pos < pos0 || q.dic_pos > p->dicBufSize) return fail("LzmaDec: bad session state");
+    if (q.dic_pos > pos0 &&
+        (hipMemcpyAsync(p->dic + pos0, d_dic + pos0, q.dic_pos - pos0, hipMemcpyDeviceToHost, st) !=
+             hipSuccess ||
+         hipStreamSynchronize(st) != hipSuccess))
+      return fail("LzmaDec: download dictionary");
+  } else {
+    if (q.out_len > out_room || q.dic_pos > p->dicBufSize) return fail("LzmaDec: bad session state");
+    if (q.out_len &&
+        (hipMemcpyAsync(dest, d_io + in_pad, q.out_len, hipMemcpyDeviceToHost, st) != hipSuccess ||
+         hipStreamSynchronize(st) != hipSuccess))
+      return fail("LzmaDec: download output");
+    // the host ring gets the same bytes the device ring got (LzmaDec.c:849-866:
+    // each pass writes from dicPos, wrapping to 0 at dicBufSize)
+    SizeT pos = pos0, left = q.out_len;
+    const Byte* from = dest;
+    while (left) {
+      if (pos == p->dicBufSize) pos = 0;
+      const SizeT k = std::min<SizeT>(left, p->dicBufSize - pos);
+      memcpy(p->dic + pos, from, k);
+      pos += k;
+      from += k;
+      left -= k;
+    }
+    *destLen = q.out_len;
+  }
+  memcpy(p->probs, back.data() + kSessBytes, size_t(cells) * 2);
+  p->dicPos = q.dic_pos;
+  p->range = q.range;
+  p->code = q.code;
+  p->processedPos = q.processed_pos;
+  p->checkDicSize = q.check_dic_size;
+  p->state = q.state;
+  for (int i = 0; i < 4; ++i) p->reps[i] = q.reps[i];
+  p->remainLen = q.remain_len;
+  p->needFlush = int(q.need_flush);
+  p->needInitState = int(q.need_init_state);
+  p->tempBufSize = q.temp_buf_size;
+  memcpy(p->tempBuf, q.temp_buf, LZMA_REQUIRED_INPUT_MAX);
+  p->buf = src + q.in_used;
+  m->history = true;
+  m->probs_dev = true;
+  *in_used = q.in_used;
+  *status = ELzmaStatus(q.status);
+  return q.res;
+}
+
+}  // namespace
+
+extern "C" {
+
+// ------------------------------------------------------------------ props + allocation
+
+SRes LzmaProps_Decode(CLzmaProps* p, const Byte* data, unsigned size) {
+  uint32_t lc, lp, pb, dict;
+  if (size < LZMA_PROPS_SIZE) return SZ_ERROR_UNSUPPORTED;
+  int r = lzgpu::lz_props_parse(data, size, lc, lp, pb, dict);
+  // the reference stores dicSize before rejecting a bad lc/lp/pb byte
+  p->dicSize = dict;
+  if (r != SZ_OK) return r;
+  p->lc = lc;
+  p->lp = lp;
+  p->pb = pb;
+  return SZ_OK;
+}
+
+void LzmaDec_FreeProbs(CLzmaDec* p, ISzAlloc* alloc) {
+  mirror_drop(p);
+  alloc->Free(alloc, p->probs);
+  p->probs = nullptr;
+}
+
+static void free_dict(CLzmaDec* p, ISzAlloc* alloc) {
+  alloc->Free(alloc, p->dic);
+  p->dic = nullptr;
+}
+
+void LzmaDec_Free(CLzmaDec* p, ISzAlloc* alloc) {
+  LzmaDec_FreeProbs(p, alloc);
+  free_dict(p, alloc);
+}
+
+static SRes alloc_probs(CLzmaDec* p, const CLzmaProps* np, ISzAlloc* alloc) {
+  const uint32_t n = probs_for(np->lc, np->lp);
+  if (p->probs == nullptr || n != p->numProbs) {
+    LzmaDec_FreeProbs(p, alloc);
+    p->probs = static_cast<CLzmaProb*>(alloc->Alloc(alloc, size_t(n) * sizeof(CLzmaProb)));
+    p->numProbs = n;
+    if (p->probs == nullptr) return SZ_ERROR_MEM;
+  }
+  return SZ_OK;
+}
+
+SRes LzmaDec_AllocateProbs(CLzmaDec* p, const Byte* props, unsigned propsSize, ISzAlloc* alloc) {
+  CLzmaProps np;
+  SRes r = LzmaProps_Decode(&np, props, propsSize);
+  if (r != SZ_OK) return r;
+  r = alloc_probs(p, &np, alloc);
+  if (r != SZ_OK) return r;
+  p->prop = np;
+  return SZ_OK;
+}
+
+SRes LzmaDec_Allocate(CLzmaDec* p, const Byte* props, unsigned propsSize, ISzAlloc* alloc) {
+  CLzmaProps np;
+  SRes r = LzmaProps_Decode(&np, props, propsSize);
+  if (r != SZ_OK) return r;
+  r = alloc_probs(p, &np, alloc);
+  if (r != SZ_OK) return r;
+  const SizeT dsz = np.dicSize;
+  if (p->dic == nullptr || dsz != p->dicBufSize) {
+    free_dict(p, alloc);
+    p->dic = static_cast<Byte*>(alloc->Alloc(alloc, dsz));
+    if (p->dic == nullptr) {
+      LzmaDec_FreeProbs(p, alloc);
+      return SZ_ERROR_MEM;
+    }
+  }
+  p->dicBufSize = dsz;
+  p->prop = np;
+  return SZ_OK;
+}
+
+void LzmaDec_InitDicAndState(CLzmaDec* p, Bool initDic, Bool initState) {
+  p->needFlush = 1;
+  p->remainLen = 0;
+  p->tempBufSize = 0;
+  if (initDic) {
+    p->processedPos = 0;
+    p->checkDicSize = 0;
+    p->needInitState = 1;
+  }
+  if (initState) p->needInitState = 1;
+}
+
+void LzmaDec_Init(CLzmaDec* p) {
+  p->dicPos = 0;
+  LzmaDec_InitDicAndState(p, 1, 1);
+}
+
+void LzmaGpu_DecoderRelease(const CLzmaDec* p) { mirror_drop(p); }
+
+// ------------------------------------------------------------------ decode entry points
+
+SRes LzmaDec_DecodeToDic(CLzmaDec* p, SizeT dicLimit, const Byte* src, SizeT* srcLen,
+                         ELzmaFinishMode finishMode, ELzmaStatus* status) {
+  const SizeT in_size = *srcLen;
+  *srcLen = 0;
+  *status = LZMA_STATUS_NOT_SPECIFIED;
+  if (!ensure_device()) return SZ_ERROR_FAIL;
+  if (dicLimit > p->dicBufSize || (p->dic == nullptr && p->dicBufSize != 0)) {
+    set_error("LzmaDec_DecodeToDic: dicLimit beyond dicBufSize");
+    return SZ_ERROR_PARAM;
+  }
+  return gpu_session_call(p, 0, dicLimit, src, in_size, srcLen, nullptr, nullptr, finishMode,
+                          status);
+}
+
+SRes LzmaDec_DecodeToBuf(CLzmaDec* p, Byte* dest, SizeT* destLen, const Byte* src, SizeT* srcLen,
+                         ELzmaFinishMode finishMode, ELzmaStatus* status) {
+  const SizeT in_size = *srcLen;
+  *srcLen = 0;
+  if (!ensure_device()) {
+    *destLen = 0;
+    return SZ_ERROR_FAIL;
+  }
+  if (p->dic == nullptr || p->dicBufSize == 0 || p->dicPos > p->dicBufSize) {
+    *destLen = 0;
+    set_error("LzmaDec_DecodeToBuf: no dictionary ring");
+    return SZ_ERROR_PARAM;
+  }
+  SizeT out = *destLen;
+  const SRes r = gpu_session_call(p, 1, 0, src, in_size, srcLen, dest, &out, finishMode, status);
+  *destLen = r == SZ_ERROR_FAIL || r == SZ_ERROR_MEM || r == SZ_ERROR_PARAM ? 0 : out;
+  return r;
+}
+
+SRes LzmaDecode(Byte* dest, SizeT* destLen, const Byte* src, SizeT* srcLen, const Byte* propData,
+                unsigned propSize, ELzmaFinishMode finishMode, ELzmaStatus* status,
+                ISzAlloc* alloc) {
+  const SizeT in_size = *srcLen, out_size = *destLen;
+  *srcLen = 0;
+  *destLen = 0;
+  if (in_size < 5) return SZ_ERROR_INPUT_EOF;
+  CLzmaProps np;
+  SRes r = LzmaProps_Decode(&np, propData, propSize);
+  if (r != SZ_OK) return r;
+  // honour the caller's allocator contract: the reference allocates the
+  // probability table through it and reports SZ_ERROR_MEM when that fails
+  void* host_probs = alloc->Alloc(alloc, size_t(probs_for(np.lc, np.lp)) * sizeof(CLzmaProb));
+  if (host_probs == nullptr) return SZ_ERROR_MEM;
+  SizeT sl = in_size, dl = out_size;
+  int st = -1;
+  r = gpu_one_call(LZMA_GPU_KIND_LZMA, dest, &dl, src, &sl, propData, propSize, finishMode, &st);
+  alloc->Free(alloc, host_probs);
+  *srcLen = sl;
+  *destLen = dl;
+  if (st >= 0) *status = ELzmaStatus(st);
+  return r;
+}
+
+static void* lib_alloc(void*, size_t n) { return malloc(n ? n : 1); }
+static void lib_free(void*, void* a) { free(a); }
+static ISzAlloc g_lib_alloc = {lib_alloc, lib_free};
+
+int LzmaUncompress(unsigned char* dest, size_t* destLen, const unsigned char* src, SizeT* srcLen,
+                   const unsigned char* props, size_t propsSize) {
+  ELzmaStatus status;
+  return LzmaDecode(dest, destLen, src, srcLen, props, unsigned(propsSize), LZMA_FINISH_ANY,
+                    &status, &g_lib_alloc);
+}
+
+// ------------------------------------------------------------------ LZMA2
+
+enum {
+  S2_CONTROL, S2_UNPACK0, S2_UNPACK1, S2_PACK0, S2_PACK1, S2_PROP, S2_DATA, S2_DATA_CONT,
+  S2_FINISHED, S2_ERROR
+};
+
+static SRes lzma2_props(Byte prop, Byte* props) {
+  if (prop > 40) return SZ_ERROR_UNSUPPORTED;
+  const UInt32 dict = (prop == 40) ? 0xFFFFFFFFu : ((2u | (prop & 1u)) << (prop / 2 + 11));
+  props[0] = 4;  // lc+lp budget of LZMA2 (Lzma2Dec.c:36,67)
+  props[1] = Byte(dict);
+  props[2] = Byte(dict >> 8);
+  props[3] = Byte(dict >> 16);
+  props[4] = Byte(dict >> 24);
+  return SZ_OK;
+}
+
+SRes Lzma2Dec_AllocateProbs(CLzma2Dec* p, Byte prop, ISzAlloc* alloc) {
+  Byte props[LZMA_PROPS_SIZE];
+  SRes r = lzma2_props(prop, props);
+  if (r != SZ_OK) return r;
+  return LzmaDec_AllocateProbs(&p->decoder, props, LZMA_PROPS_SIZE, alloc);
+}
+
+SRes Lzma2Dec_Allocate(CLzma2Dec* p, Byte prop, ISzAlloc* alloc) {
+  Byte props[LZMA_PROPS_SIZE];
+  SRes r = lzma2_props(prop, props);
+  if (r != SZ_OK) return r;
+  return LzmaDec_Allocate(&p->decoder, props, LZMA_PROPS_SIZE, alloc);
+}
+
+void Lzma2Dec_Init(CLzma2Dec* p) {
+  p->state = S2_CONTROL;
+  p->needInitDic = 1;
+  p->needInitState = 1;
+  p->needInitProp = 1;
+  LzmaDec_Init(&p->decoder);
+}
+
+static int lzma2_header(CLzma2Dec* p, Byte b) {
+  const bool copy = (p->control & 0x80) == 0;
+  switch (p->state) {
+    case S2_CONTROL:
+      p->control = b;
+      if (b == 0) return S2_FINISHED;
+      if ((b & 0x80) == 0) {
+        if ((b & 0x7F) > 2) return S2_ERROR;
+        p->unpackSize = 0;
+      } else {
+        p->unpackSize = UInt32(b & 0x1F) << 16;
+      }
+      return S2_UNPACK0;
+    case S2_UNPACK0:
+      p->unpackSize |= UInt32(b) << 8;
+      return S2_UNPACK1;
+    case S2_UNPACK1:
+      p->unpackSize |= b;
+      p->unpackSize++;
+      return copy ? S2_DATA : S2_PACK0;
+    case S2_PACK0:
+      p->packSize = UInt32(b) << 8;
+      return S2_PACK1;
+    case S2_PACK1:
+      p->packSize |= b;
+      p->packSize++;
+      if (((p->control >> 5) & 3) >= 2) return S2_PROP;
+      return p->needInitProp ? S2_ERROR : S2_DATA;
+    case S2_PROP: {
+      if (b >= 225) return S2_ERROR;
+      unsigned lc = b % 9;
+      b /= 9;
+      unsigned pb = b / 5, lp = b % 5;
+      if (lc + lp > 4) return S2_ERROR;
+      p->decoder.prop.lc = lc;
+      p->decoder.prop.lp = lp;
+      p->decoder.prop.pb = pb;
+      p->needInitProp = 0;
+      return S2_DATA;
+    }
+  }
+  return S2_ERROR;
+}
+
+SRes Lzma2Dec_DecodeToDic(CLzma2Dec* p, SizeT dicLimit, const Byte* src, SizeT* srcLen,
+                          ELzmaFinishMode finishMode, ELzmaStatus* status) {
+  const SizeT in_size = *srcLen;
+  *srcLen = 0;
+  *status = LZMA_STATUS_NOT_SPECIFIED;
+  if (!ensure_device()) return SZ_ERROR_FAIL;
+  while (p->state != S2_FINISHED) {
+    const SizeT pos0 = p->decoder.dicPos;
+    if (p->state == S2_ERROR) return SZ_ERROR_DATA;
+    if (pos0 == dicLimit && finishMode == LZMA_FINISH_ANY) {
+      *status = LZMA_STATUS_NOT_FINISHED;
+      return SZ_OK;
+    }
+    if (p->state != S2_DATA && p->state != S2_DATA_CONT) {
+      if (*srcLen == in_size) {
+        *status = LZMA_STATUS_NEEDS_MORE_INPUT;
+        return SZ_OK;
+      }
+      (*srcLen)++;
+      p->state = lzma2_header(p, *src++);
+      continue;
+    }
+    SizeT out_cur = dicLimit - pos0, in_cur = in_size - *srcLen;
+    ELzmaFinishMode fin_cur = LZMA_FINISH_ANY;
+    if (p->unpackSize <= out_cur) {
+      out_cur = p->unpackSize;
+      fin_cur = LZMA_FINISH_END;
+    }
+    if ((p->control & 0x80) == 0) {
+      if (*srcLen == in_size) {
+        *status = LZMA_STATUS_NEEDS_MORE_INPUT;
+        return SZ_OK;
+      }
+      if (p->state == S2_DATA) {
+        const bool reset = (p->control == 1);
+        if (reset)
+          p->needInitProp = p->needInitState = 1;
+        else if (p->needInitDic)
+          return SZ_ERROR_DATA;
+        p->needInitDic = 0;
+        LzmaDec_InitDicAndState(&p->decoder, reset, 0);
+      }
+      if (in_cur > out_cur) in_cur = out_cur;
+      if (in_cur == 0) return SZ_ERROR_DATA;
+      // stored chunk: a plain copy into the dictionary (Lzma2Dec.c:159-166),
+      // written through to the decoder's device mirror
+      CLzmaDec* d = &p->decoder;
+      memcpy(d->dic + d->dicPos, src, in_cur);
+      if (!mirror_host_wrote(d, d->dicPos, in_cur)) return SZ_ERROR_FAIL;
+      d->dicPos += in_cur;
+      if (d->checkDicSize == 0 && d->prop.dicSize - d->processedPos <= in_cur)
+        d->checkDicSize = d->prop.dicSize;
+      d->processedPos += UInt32(in_cur);
+      src += in_cur;
+      *srcLen += in_cur;
+      p->unpackSize -= UInt32(in_cur);
+      p->state = (p->unpackSize == 0) ? S2_CONTROL : S2_DATA_CONT;
+    } else {
+      if (p->state == S2_DATA) {
+        const int mode = (p->control >> 5) & 3;
+        const bool init_dic = (mode == 3), init_state = (mode > 0);
+        if ((!init_dic && p->needInitDic) || (!init_state && p->needInitState))
+          return SZ_ERROR_DATA;
+        LzmaDec_InitDicAndState(&p->decoder, init_dic, init_state);
+        p->needInitDic = 0;
+        p->needInitState = 0;
+        p->state = S2_DATA_CONT;
+      }
+      if (in_cur > p->packSize) in_cur = p->packSize;
+      SRes r = LzmaDec_DecodeToDic(&p->decoder, pos0 + out_cur, src, &in_cur, fin_cur, status);
+      src += in_cur;
+      *srcLen += in_cur;
+      p->packSize -= UInt32(in_cur);
+      const SizeT produced = p->decoder.dicPos - pos0;
+      p->unpackSize -= UInt32(produced);
+      if (r != SZ_OK) return r;
+      if (*status == LZMA_STATUS_NEEDS_MORE_INPUT) return r;
+      if (in_cur == 0 && produced == 0) {
+        if (*status != LZMA_STATUS_MAYBE_FINISHED_WITHOUT_MARK || p->unpackSize != 0 ||
+            p->packSize != 0)
+          return SZ_ERROR_DATA;
+        p->state = S2_CONTROL;
+      }
+      if (*status == LZMA_STATUS_MAYBE_FINISHED_WITHOUT_MARK) *status = LZMA_STATUS_NOT_FINISHED;
+    }
+  }
+  *status = LZMA_STATUS_FINISHED_WITH_MARK;
+  return SZ_OK;
+}
+
+SRes Lzma2Dec_DecodeToBuf(CLzma2Dec* p, Byte* dest, SizeT* destLen, const Byte* src,
+                          SizeT* srcLen, ELzmaFinishMode finishMode, ELzmaStatus* status) {
+  SizeT out_left = *destLen, in_left = *srcLen;
+  *srcLen = 0;
+  *destLen = 0;
+  for (;;) {
+    SizeT in_cur = in_left, lim, start;
+    ELzmaFinishMode fin_cur;
+    CLzmaDec* d = &p->decoder;
+    if (d->dicPos == d->dicBufSize) d->dicPos = 0;
+    start = d->dicPos;
+    if (out_left > d->dicBufSize - start) {
+      lim = d->dicBufSize;
+      fin_cur = LZMA_FINISH_ANY;
+    } else {
+      lim = start + out_left;
+      fin_cur = finishMode;
+    }
+    SRes r = Lzma2Dec_DecodeToDic(p, lim, src, &in_cur, fin_cur, status);
+    src += in_cur;
+    in_left -= in_cur;
+    *srcLen += in_cur;
+    const SizeT produced = d->dicPos - start;
+    memcpy(dest, d->dic + start, produced);
+    dest += produced;
+    out_left -= produced;
+    *destLen += produced;
+    if (r != SZ_OK) return r;
+    if (produced == 0 || out_left == 0) return SZ_OK;
+  }
+}
+
+SRes Lzma2Decode(Byte* dest, SizeT* destLen, const Byte* src, SizeT* srcLen, Byte prop,
+                 ELzmaFinishMode finishMode, ELzmaStatus* status, ISzAlloc* alloc) {
+  const SizeT in_size = *srcLen, out_size = *destLen;
+  *destLen = 0;
+  *srcLen = 0;
+  *status = LZMA_STATUS_NOT_SPECIFIED;
+  Byte props[LZMA_PROPS_SIZE];
+  SRes r = lzma2_props(prop, props);
+  if (r != SZ_OK) return r;
+  void* host_probs = alloc->Alloc(alloc, size_t(probs_for(4, 0)) * sizeof(CLzmaProb));
+  if (host_probs == nullptr) return SZ_ERROR_MEM;
+  SizeT sl = in_size, dl = out_size;
+  int st = -1;
+  r = gpu_one_call(LZMA_GPU_KIND_LZMA2, dest, &dl, src, &sl, &prop, 1, finishMode, &st);
+  if (r == SZ_OK && st == LZMA_STATUS_NEEDS_MORE_INPUT) r = SZ_ERROR_INPUT_EOF;  // Lzma2Dec.c:350
+  alloc->Free(alloc, host_probs);
+  *srcLen = sl;
+  *destLen = dl;
+  if (st >= 0) *status = ELzmaStatus(st);
+  return r;
+}
+
+}  // extern "C"

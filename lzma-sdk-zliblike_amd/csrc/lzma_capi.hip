@@ -1,20 +1,21 @@
-// lzma_capi.hip -- host side of liblzmagpu.so: the drop-in LzmaDec / LzmaLib /
-// Lzma2Dec symbols and the batch extension (include/lzma_gpu.h).
+// lzma_capi.hip -- host side of liblzmagpu.so: the batch extension
+// (include/lzma_gpu.h: planner, batch launches, streaming sessions, LZMA2
+// block splitter), the 7zCrc.h drop-ins and the library's shared host state
+// (device check, per-device call scratch and class-stream pools).  The
+// LzmaDec / LzmaLib / Lzma2Dec drop-ins are in dropin_capi.hip.
 //
-// Every decode runs on the GPU.  What stays on the host is what the reference
-// keeps outside its decoder loop: property parsing (LzmaDec.c:898-922),
-// ISzAlloc bookkeeping (LzmaDec.c:880-970), the DecodeToBuf ring-to-caller
-// copy loop (LzmaDec.c:840-878) and the LZMA2 chunk-header walk of the
-// streaming interface (Lzma2Dec.c:170-328), whose LZMA chunks are decoded by
-// the GPU LzmaDec_DecodeToDic.  Without a HIP device every decode entry
-// returns SZ_ERROR_FAIL (no CPU fallback).
+// Without a HIP device every decode entry returns SZ_ERROR_FAIL (no CPU
+// fallback).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <exception>
+#include <mutex>
+#include <new>
 #include <numeric>
 #include <string>
 #include <vector>
@@ -41,599 +42,52 @@ int device_count() {
   return n;
 }
 
+// set once the library has started the HIP runtime with a device present
+std::atomic<bool> g_runtime_up{false};
+
 bool ensure_device() {
-  static int count = -1;
-  if (count < 0) count = device_count();
+  static std::once_flag once;
+  static int count = 0;
+  std::call_once(once, [] {
+    count = device_count();
+    if (count > 0) g_runtime_up.store(true);
+  });
   if (count <= 0) {
     set_error("liblzmagpu: no HIP device available (GPU decoder only, no CPU fallback)");
-    static bool warned = false;
-    if (!warned) {
-      warned = true;
+    static std::atomic<bool> warned{false};
+    if (!warned.exchange(true))
       fprintf(stderr, "liblzmagpu: no HIP device available -- decode calls return SZ_ERROR_FAIL\n");
-    }
     return false;
   }
   return true;
 }
 
-// Grow-only device buffer, one set per host thread (the reference API is
-// re-entrant per decoder object; these buffers are per-call scratch).
-struct DevBuf {
-  void* p = nullptr;
-  size_t cap = 0;
-  int dev = -1;
-  void* get(size_t n) {
-    int d = 0;
-    (void)hipGetDevice(&d);
-    if (n == 0) n = 16;
-    if (p && cap >= n && dev == d) return p;
-    size_t want = std::max(n, cap * 2);
-    if (p && dev == d) (void)hipFree(p);
-    p = nullptr;
-    cap = 0;
-    if (hipMalloc(&p, want) != hipSuccess) {
-      p = nullptr;
-      if (hipMalloc(&p, n) != hipSuccess) { p = nullptr; return nullptr; }
-      want = n;
-    }
-    cap = want;
-    dev = d;
-    return p;
-  }
-};
-
-struct Scratch {
-  DevBuf probs, dic, src, sess, desc, res, dst, crc_meta, crc_chunks;
-};
-
-Scratch& scratch() {
-  static thread_local Scratch* s = new Scratch();  // intentionally leaked at exit
-  return *s;
+// CUs the planner and launchers size for: the current device's, cached per
+// device, once ensure_device() has started the runtime; before that (a
+// launcher process that plans before it starts its ranks) MI355X's 256, with
+// no HIP call -- planning alone never initialises the GPU.
+uint32_t device_cus() {
+  if (!g_runtime_up.load()) return 256;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kLzgpuMaxDevices) return 256;
+  static std::atomic<uint32_t> cache[kLzgpuMaxDevices];
+  uint32_t c = cache[dev].load();
+  if (c) return c;
+  int v = 0;
+  if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0)
+    return 256;
+  cache[dev].store(uint32_t(v));
+  return uint32_t(v);
 }
-
-uint32_t probs_for(uint32_t lc, uint32_t lp) { return lzgpu::num_probs(lc, lp); }
 
 int env_int(const char* name, int dflt) {
   const char* v = getenv(name);
   return (v && *v) ? atoi(v) : dflt;
 }
 
-// Run one DecodeToDic on the GPU over a host-resident CLzmaDec.
-SRes gpu_decode_to_dic(CLzmaDec* p, SizeT dicLimit, const Byte* src, SizeT* srcLen,
-                       ELzmaFinishMode finishMode, ELzmaStatus* status) {
-  const SizeT in_size = *srcLen;
-  *srcLen = 0;
-  *status = LZMA_STATUS_NOT_SPECIFIED;
-  if (!ensure_device()) return SZ_ERROR_FAIL;
-  if (dicLimit > p->dicBufSize || (p->dic == nullptr && p->dicBufSize != 0)) {
-    set_error("LzmaDec_DecodeToDic: dicLimit beyond dicBufSize");
-    return SZ_ERROR_PARAM;
-  }
-  Scratch& sc = scratch();
-  // compact device layout (lzma_device.h): lo + hi for the current lc/lp/pb,
-  // never more than the numProbs cells LzmaDec_AllocateProbs allocated
-  const uint32_t nprobs = lzgpu::table_cells(p->prop.lc, p->prop.lp, p->prop.pb);
-  void* d_probs = sc.probs.get(size_t(nprobs) * 2);
-  void* d_dic = sc.dic.get(p->dicBufSize);
-  void* d_src = sc.src.get(in_size);
-  LzgpuSession* d_sess = static_cast<LzgpuSession*>(sc.sess.get(sizeof(LzgpuSession)));
-  if (!d_probs || !d_dic || !d_src || !d_sess) {
-    set_error("LzmaDec_DecodeToDic: device allocation failed");
-    return SZ_ERROR_MEM;
-  }
-  if (p->probs && !hip_ok(hipMemcpy(d_probs, p->probs, size_t(nprobs) * 2, hipMemcpyHostToDevice),
-                          "upload probs"))
-    return SZ_ERROR_FAIL;
-  if (p->dicBufSize &&
-      !hip_ok(hipMemcpy(d_dic, p->dic, p->dicBufSize, hipMemcpyHostToDevice), "upload dic"))
-    return SZ_ERROR_FAIL;
-  if (in_size && !hip_ok(hipMemcpy(d_src, src, in_size, hipMemcpyHostToDevice), "upload src"))
-    return SZ_ERROR_FAIL;
-
-  LzgpuSession q;
-  memset(&q, 0, sizeof q);
-  q.lc = p->prop.lc;
-  q.lp = p->prop.lp;
-  q.pb = p->prop.pb;
-  q.dict_size = p->prop.dicSize;
-  q.probs = static_cast<uint16_t*>(d_probs);
-  q.dic = static_cast<uint8_t*>(d_dic);
-  q.in = static_cast<const uint8_t*>(d_src);
-  q.dic_buf_size = p->dicBufSize;
-  q.dic_pos = p->dicPos;
-  q.dic_limit = dicLimit;
-  q.in_len = in_size;
-  q.range = p->range;
-  q.code = p->code;
-  q.processed_pos = p->processedPos;
-  q.check_dic_size = p->checkDicSize;
-  q.state = p->state;
-  for (int i = 0; i < 4; ++i) q.reps[i] = p->reps[i];
-  q.remain_len = p->remainLen;
-  q.need_flush = p->needFlush ? 1 : 0;
-  q.need_init_state = p->needInitState ? 1 : 0;
-  q.temp_buf_size = p->tempBufSize;
-  memcpy(q.temp_buf, p->tempBuf, LZMA_REQUIRED_INPUT_MAX);
-  q.finish_mode = finishMode;
-  q.mode = 0;
-  const SizeT pos0 = p->dicPos;
-
-  if (!hip_ok(hipMemcpy(d_sess, &q, sizeof q, hipMemcpyHostToDevice), "upload session"))
-    return SZ_ERROR_FAIL;
-  if (lzgpu_launch_session(d_sess, 1, nullptr) != 0) {
-    set_error("session kernel launch failed");
-    return SZ_ERROR_FAIL;
-  }
-  if (!hip_ok(hipMemcpy(&q, d_sess, sizeof q, hipMemcpyDeviceToHost), "download session"))
-    return SZ_ERROR_FAIL;
-  if (p->probs &&
-      !hip_ok(hipMemcpy(p->probs, d_probs, size_t(nprobs) * 2, hipMemcpyDeviceToHost),
-              "download probs"))
-    return SZ_ERROR_FAIL;
-  if (q.dic_pos > pos0 &&
-      !hip_ok(hipMemcpy(p->dic + pos0, static_cast<uint8_t*>(d_dic) + pos0, q.dic_pos - pos0,
-                        hipMemcpyDeviceToHost),
-              "download dic"))
-    return SZ_ERROR_FAIL;
-
-  p->dicPos = q.dic_pos;
-  p->range = q.range;
-  p->code = q.code;
-  p->processedPos = q.processed_pos;
-  p->checkDicSize = q.check_dic_size;
-  p->state = q.state;
-  for (int i = 0; i < 4; ++i) p->reps[i] = q.reps[i];
-  p->remainLen = q.remain_len;
-  p->needFlush = int(q.need_flush);
-  p->needInitState = int(q.need_init_state);
-  p->tempBufSize = q.temp_buf_size;
-  memcpy(p->tempBuf, q.temp_buf, LZMA_REQUIRED_INPUT_MAX);
-  p->buf = src + q.in_used;
-  *srcLen = q.in_used;
-  *status = ELzmaStatus(q.status);
-  return q.res;
-}
-
-// LzmaDecode-style one-call over host buffers, as a 1-stream GPU batch.
-SRes gpu_one_call(uint8_t kind, Byte* dest, SizeT* destLen, const Byte* src, SizeT* srcLen,
-                  const Byte* props, unsigned propSize, ELzmaFinishMode finishMode,
-                  int* status_out) {
-  const SizeT in_size = *srcLen, out_size = *destLen;
-  *srcLen = 0;
-  *destLen = 0;
-  if (!ensure_device()) return SZ_ERROR_FAIL;
-  LzmaGpuStreamDesc d;
-  memset(&d, 0, sizeof d);
-  d.src_len = in_size;
-  d.dst_cap = out_size;
-  memcpy(d.props, props, std::min<unsigned>(propSize, 5));
-  d.props_size = uint8_t(std::min<unsigned>(propSize, 255));
-  d.finish_mode = uint8_t(finishMode);
-  d.kind = kind;
-  size_t ws = LzmaGpu_PlanBatch(&d, 1, nullptr);
-  Scratch& sc = scratch();
-  void* d_src = sc.src.get(in_size);
-  void* d_dst = sc.dst.get(out_size);
-  void* d_ws = sc.probs.get(ws);
-  void* d_desc = sc.desc.get(sizeof d);
-  void* d_res = sc.res.get(sizeof(LzmaGpuResult));
-  if (!d_src || !d_dst || !d_ws || !d_desc || !d_res) {
-    set_error("device allocation failed");
-    return SZ_ERROR_MEM;
-  }
-  if (in_size && !hip_ok(hipMemcpy(d_src, src, in_size, hipMemcpyHostToDevice), "upload src"))
-    return SZ_ERROR_FAIL;
-  if (!hip_ok(hipMemcpy(d_desc, &d, sizeof d, hipMemcpyHostToDevice), "upload desc"))
-    return SZ_ERROR_FAIL;
-  if (lzgpu_launch_decode_batch(static_cast<LzmaGpuStreamDesc*>(d_desc), nullptr, 1,
-                                static_cast<uint8_t*>(d_src), static_cast<uint8_t*>(d_dst),
-                                static_cast<uint16_t*>(d_ws), static_cast<LzmaGpuResult*>(d_res),
-                                nullptr) != 0) {
-    set_error("decode kernel launch failed");
-    return SZ_ERROR_FAIL;
-  }
-  LzmaGpuResult r;
-  if (!hip_ok(hipMemcpy(&r, d_res, sizeof r, hipMemcpyDeviceToHost), "download result"))
-    return SZ_ERROR_FAIL;
-  if (r.dest_len &&
-      !hip_ok(hipMemcpy(dest, d_dst, r.dest_len, hipMemcpyDeviceToHost), "download output"))
-    return SZ_ERROR_FAIL;
-  *destLen = r.dest_len;
-  *srcLen = r.src_len;
-  *status_out = r.status;
-  return r.res;
-}
-
 }  // namespace
 
 extern "C" {
-
-// ------------------------------------------------------------------ props + allocation
-
-SRes LzmaProps_Decode(CLzmaProps* p, const Byte* data, unsigned size) {
-  uint32_t lc, lp, pb, dict;
-  if (size < LZMA_PROPS_SIZE) return SZ_ERROR_UNSUPPORTED;
-  int r = lzgpu::lz_props_parse(data, size, lc, lp, pb, dict);
-  // the reference stores dicSize before rejecting a bad lc/lp/pb byte
-  p->dicSize = dict;
-  if (r != SZ_OK) return r;
-  p->lc = lc;
-  p->lp = lp;
-  p->pb = pb;
-  return SZ_OK;
-}
-
-void LzmaDec_FreeProbs(CLzmaDec* p, ISzAlloc* alloc) {
-  alloc->Free(alloc, p->probs);
-  p->probs = nullptr;
-}
-
-static void free_dict(CLzmaDec* p, ISzAlloc* alloc) {
-  alloc->Free(alloc, p->dic);
-  p->dic = nullptr;
-}
-
-void LzmaDec_Free(CLzmaDec* p, ISzAlloc* alloc) {
-  LzmaDec_FreeProbs(p, alloc);
-  free_dict(p, alloc);
-}
-
-static SRes alloc_probs(CLzmaDec* p, const CLzmaProps* np, ISzAlloc* alloc) {
-  const uint32_t n = probs_for(np->lc, np->lp);
-  if (p->probs == nullptr || n != p->numProbs) {
-    LzmaDec_FreeProbs(p, alloc);
-    p->probs = static_cast<CLzmaProb*>(alloc->Alloc(alloc, size_t(n) * sizeof(CLzmaProb)));
-    p->numProbs = n;
-    if (p->probs == nullptr) return SZ_ERROR_MEM;
-  }
-  return SZ_OK;
-}
-
-SRes LzmaDec_AllocateProbs(CLzmaDec* p, const Byte* props, unsigned propsSize, ISzAlloc* alloc) {
-  CLzmaProps np;
-  SRes r = LzmaProps_Decode(&np, props, propsSize);
-  if (r != SZ_OK) return r;
-  r = alloc_probs(p, &np, alloc);
-  if (r != SZ_OK) return r;
-  p->prop = np;
-  return SZ_OK;
-}
-
-SRes LzmaDec_Allocate(CLzmaDec* p, const Byte* props, unsigned propsSize, ISzAlloc* alloc) {
-  CLzmaProps np;
-  SRes r = LzmaProps_Decode(&np, props, propsSize);
-  if (r != SZ_OK) return r;
-  r = alloc_probs(p, &np, alloc);
-  if (r != SZ_OK) return r;
-  const SizeT dsz = np.dicSize;
-  if (p->dic == nullptr || dsz != p->dicBufSize) {
-    free_dict(p, alloc);
-    p->dic = static_cast<Byte*>(alloc->Alloc(alloc, dsz));
-    if (p->dic == nullptr) {
-      LzmaDec_FreeProbs(p, alloc);
-      return SZ_ERROR_MEM;
-    }
-  }
-  p->dicBufSize = dsz;
-  p->prop = np;
-  return SZ_OK;
-}
-
-void LzmaDec_InitDicAndState(CLzmaDec* p, Bool initDic, Bool initState) {
-  p->needFlush = 1;
-  p->remainLen = 0;
-  p->tempBufSize = 0;
-  if (initDic) {
-    p->processedPos = 0;
-    p->checkDicSize = 0;
-    p->needInitState = 1;
-  }
-  if (initState) p->needInitState = 1;
-}
-
-void LzmaDec_Init(CLzmaDec* p) {
-  p->dicPos = 0;
-  LzmaDec_InitDicAndState(p, 1, 1);
-}
-
-// ------------------------------------------------------------------ decode entry points
-
-SRes LzmaDec_DecodeToDic(CLzmaDec* p, SizeT dicLimit, const Byte* src, SizeT* srcLen,
-                         ELzmaFinishMode finishMode, ELzmaStatus* status) {
-  return gpu_decode_to_dic(p, dicLimit, src, srcLen, finishMode, status);
-}
-
-SRes LzmaDec_DecodeToBuf(CLzmaDec* p, Byte* dest, SizeT* destLen, const Byte* src, SizeT* srcLen,
-                         ELzmaFinishMode finishMode, ELzmaStatus* status) {
-  SizeT out_left = *destLen, in_left = *srcLen;
-  *srcLen = 0;
-  *destLen = 0;
-  for (;;) {
-    SizeT in_cur = in_left, lim, start;
-    ELzmaFinishMode fin_cur;
-    if (p->dicPos == p->dicBufSize) p->dicPos = 0;
-    start = p->dicPos;
-    if (out_left > p->dicBufSize - start) {
-      lim = p->dicBufSize;
-      fin_cur = LZMA_FINISH_ANY;
-    } else {
-      lim = start + out_left;
-      fin_cur = finishMode;
-    }
-    SRes r = LzmaDec_DecodeToDic(p, lim, src, &in_cur, fin_cur, status);
-    src += in_cur;
-    in_left -= in_cur;
-    *srcLen += in_cur;
-    const SizeT produced = p->dicPos - start;
-    memcpy(dest, p->dic + start, produced);
-    dest += produced;
-    out_left -= produced;
-    *destLen += produced;
-    if (r != SZ_OK) return r;
-    if (produced == 0 || out_left == 0) return SZ_OK;
-  }
-}
-
-SRes LzmaDecode(Byte* dest, SizeT* destLen, const Byte* src, SizeT* srcLen, const Byte* propData,
-                unsigned propSize, ELzmaFinishMode finishMode, ELzmaStatus* status,
-                ISzAlloc* alloc) {
-  const SizeT in_size = *srcLen, out_size = *destLen;
-  *srcLen = 0;
-  *destLen = 0;
-  if (in_size < 5) return SZ_ERROR_INPUT_EOF;
-  CLzmaProps np;
-  SRes r = LzmaProps_Decode(&np, propData, propSize);
-  if (r != SZ_OK) return r;
-  // honour the caller's allocator contract: the reference allocates the
-  // probability table through it and reports SZ_ERROR_MEM when that fails
-  void* host_probs = alloc->Alloc(alloc, size_t(probs_for(np.lc, np.lp)) * sizeof(CLzmaProb));
-  if (host_probs == nullptr) return SZ_ERROR_MEM;
-  SizeT sl = in_size, dl = out_size;
-  int st = -1;
-  r = gpu_one_call(LZMA_GPU_KIND_LZMA, dest, &dl, src, &sl, propData, propSize, finishMode, &st);
-  alloc->Free(alloc, host_probs);
-  *srcLen = sl;
-  *destLen = dl;
-  if (st >= 0) *status = ELzmaStatus(st);
-  return r;
-}
-
-static void* lib_alloc(void*, size_t n) { return malloc(n ? n : 1); }
-static void lib_free(void*, void* a) { free(a); }
-static ISzAlloc g_lib_alloc = {lib_alloc, lib_free};
-
-int LzmaUncompress(unsigned char* dest, size_t* destLen, const unsigned char* src, SizeT* srcLen,
-                   const unsigned char* props, size_t propsSize) {
-  ELzmaStatus status;
-  return LzmaDecode(dest, destLen, src, srcLen, props, unsigned(propsSize), LZMA_FINISH_ANY,
-                    &status, &g_lib_alloc);
-}
-
-// ------------------------------------------------------------------ LZMA2
-
-enum {
-  S2_CONTROL, S2_UNPACK0, S2_UNPACK1, S2_PACK0, S2_PACK1, S2_PROP, S2_DATA, S2_DATA_CONT,
-  S2_FINISHED, S2_ERROR
-};
-
-static SRes lzma2_props(Byte prop, Byte* props) {
-  if (prop > 40) return SZ_ERROR_UNSUPPORTED;
-  const UInt32 dict = (prop == 40) ? 0xFFFFFFFFu : ((2u | (prop & 1u)) << (prop / 2 + 11));
-  props[0] = 4;  // lc+lp budget of LZMA2 (Lzma2Dec.c:36,67)
-  props[1] = Byte(dict);
-  props[2] = Byte(dict >> 8);
-  props[3] = Byte(dict >> 16);
-  props[4] = Byte(dict >> 24);
-  return SZ_OK;
-}
-
-SRes Lzma2Dec_AllocateProbs(CLzma2Dec* p, Byte prop, ISzAlloc* alloc) {
-  Byte props[LZMA_PROPS_SIZE];
-  SRes r = lzma2_props(prop, props);
-  if (r != SZ_OK) return r;
-  return LzmaDec_AllocateProbs(&p->decoder, props, LZMA_PROPS_SIZE, alloc);
-}
-
-SRes Lzma2Dec_Allocate(CLzma2Dec* p, Byte prop, ISzAlloc* alloc) {
-  Byte props[LZMA_PROPS_SIZE];
-  SRes r = lzma2_props(prop, props);
-  if (r != SZ_OK) return r;
-  return LzmaDec_Allocate(&p->decoder, props, LZMA_PROPS_SIZE, alloc);
-}
-
-void Lzma2Dec_Init(CLzma2Dec* p) {
-  p->state = S2_CONTROL;
-  p->needInitDic = 1;
-  p->needInitState = 1;
-  p->needInitProp = 1;
-  LzmaDec_Init(&p->decoder);
-}
-
-static int lzma2_header(CLzma2Dec* p, Byte b) {
-  const bool copy = (p->control & 0x80) == 0;
-  switch (p->state) {
-    case S2_CONTROL:
-      p->control = b;
-      if (b == 0) return S2_FINISHED;
-      if ((b & 0x80) == 0) {
-        if ((b & 0x7F) > 2) return S2_ERROR;
-        p->unpackSize = 0;
-      } else {
-        p->unpackSize = UInt32(b & 0x1F) << 16;
-      }
-      return S2_UNPACK0;
-    case S2_UNPACK0:
-      p->unpackSize |= UInt32(b) << 8;
-      return S2_UNPACK1;
-    case S2_UNPACK1:
-      p->unpackSize |= b;
-      p->unpackSize++;
-      return copy ? S2_DATA : S2_PACK0;
-    case S2_PACK0:
-      p->packSize = UInt32(b) << 8;
-      return S2_PACK1;
-    case S2_PACK1:
-      p->packSize |= b;
-      p->packSize++;
-      if (((p->control >> 5) & 3) >= 2) return S2_PROP;
-      return p->needInitProp ? S2_ERROR : S2_DATA;
-    case S2_PROP: {
-      if (b >= 225) return S2_ERROR;
-      unsigned lc = b % 9;
-      b /= 9;
-      unsigned pb = b / 5, lp = b % 5;
-      if (lc + lp > 4) return S2_ERROR;
-      p->decoder.prop.lc = lc;
-      p->decoder.prop.lp = lp;
-      p->decoder.prop.pb = pb;
-      p->needInitProp = 0;
-      return S2_DATA;
-    }
-  }
-  return S2_ERROR;
-}
-
-SRes Lzma2Dec_DecodeToDic(CLzma2Dec* p, SizeT dicLimit, const Byte* src, SizeT* srcLen,
-                          ELzmaFinishMode finishMode, ELzmaStatus* status) {
-  const SizeT in_size = *srcLen;
-  *srcLen = 0;
-  *status = LZMA_STATUS_NOT_SPECIFIED;
-  if (!ensure_device()) return SZ_ERROR_FAIL;
-  while (p->state != S2_FINISHED) {
-    const SizeT pos0 = p->decoder.dicPos;
-    if (p->state == S2_ERROR) return SZ_ERROR_DATA;
-    if (pos0 == dicLimit && finishMode == LZMA_FINISH_ANY) {
-      *status = LZMA_STATUS_NOT_FINISHED;
-      return SZ_OK;
-    }
-    if (p->state != S2_DATA && p->state != S2_DATA_CONT) {
-      if (*srcLen == in_size) {
-        *status = LZMA_STATUS_NEEDS_MORE_INPUT;
-        return SZ_OK;
-      }
-      (*srcLen)++;
-      p->state = lzma2_header(p, *src++);
-      continue;
-    }
-    SizeT out_cur = dicLimit - pos0, in_cur = in_size - *srcLen;
-    ELzmaFinishMode fin_cur = LZMA_FINISH_ANY;
-    if (p->unpackSize <= out_cur) {
-      out_cur = p->unpackSize;
-      fin_cur = LZMA_FINISH_END;
-    }
-    if ((p->control & 0x80) == 0) {
-      if (*srcLen == in_size) {
-        *status = LZMA_STATUS_NEEDS_MORE_INPUT;
-        return SZ_OK;
-      }
-      if (p->state == S2_DATA) {
-        const bool reset = (p->control == 1);
-        if (reset)
-          p->needInitProp = p->needInitState = 1;
-        else if (p->needInitDic)
-          return SZ_ERROR_DATA;
-        p->needInitDic = 0;
-        LzmaDec_InitDicAndState(&p->decoder, reset, 0);
-      }
-      if (in_cur > out_cur) in_cur = out_cur;
-      if (in_cur == 0) return SZ_ERROR_DATA;
-      // stored chunk: a plain copy into the dictionary (Lzma2Dec.c:159-166)
-      CLzmaDec* d = &p->decoder;
-      memcpy(d->dic + d->dicPos, src, in_cur);
-      d->dicPos += in_cur;
-      if (d->checkDicSize == 0 && d->prop.dicSize - d->processedPos <= in_cur)
-        d->checkDicSize = d->prop.dicSize;
-      d->processedPos += UInt32(in_cur);
-      src += in_cur;
-      *srcLen += in_cur;
-      p->unpackSize -= UInt32(in_cur);
-      p->state = (p->unpackSize == 0) ? S2_CONTROL : S2_DATA_CONT;
-    } else {
-      if (p->state == S2_DATA) {
-        const int mode = (p->control >> 5) & 3;
-        const bool init_dic = (mode == 3), init_state = (mode > 0);
-        if ((!init_dic && p->needInitDic) || (!init_state && p->needInitState))
-          return SZ_ERROR_DATA;
-        LzmaDec_InitDicAndState(&p->decoder, init_dic, init_state);
-        p->needInitDic = 0;
-        p->needInitState = 0;
-        p->state = S2_DATA_CONT;
-      }
-      if (in_cur > p->packSize) in_cur = p->packSize;
-      SRes r = LzmaDec_DecodeToDic(&p->decoder, pos0 + out_cur, src, &in_cur, fin_cur, status);
-      src += in_cur;
-      *srcLen += in_cur;
-      p->packSize -= UInt32(in_cur);
-      const SizeT produced = p->decoder.dicPos - pos0;
-      p->unpackSize -= UInt32(produced);
-      if (r != SZ_OK) return r;
-      if (*status == LZMA_STATUS_NEEDS_MORE_INPUT) return r;
-      if (in_cur == 0 && produced == 0) {
-        if (*status != LZMA_STATUS_MAYBE_FINISHED_WITHOUT_MARK || p->unpackSize != 0 ||
-            p->packSize != 0)
-          return SZ_ERROR_DATA;
-        p->state = S2_CONTROL;
-      }
-      if (*status == LZMA_STATUS_MAYBE_FINISHED_WITHOUT_MARK) *status = LZMA_STATUS_NOT_FINISHED;
-    }
-  }
-  *status = LZMA_STATUS_FINISHED_WITH_MARK;
-  return SZ_OK;
-}
-
-SRes Lzma2Dec_DecodeToBuf(CLzma2Dec* p, Byte* dest, SizeT* destLen, const Byte* src,
-                          SizeT* srcLen, ELzmaFinishMode finishMode, ELzmaStatus* status) {
-  SizeT out_left = *destLen, in_left = *srcLen;
-  *srcLen = 0;
-  *destLen = 0;
-  for (;;) {
-    SizeT in_cur = in_left, lim, start;
-    ELzmaFinishMode fin_cur;
-    CLzmaDec* d = &p->decoder;
-    if (d->dicPos == d->dicBufSize) d->dicPos = 0;
-    start = d->dicPos;
-    if (out_left > d->dicBufSize - start) {
-      lim = d->dicBufSize;
-      fin_cur = LZMA_FINISH_ANY;
-    } else {
-      lim = start + out_left;
-      fin_cur = finishMode;
-    }
-    SRes r = Lzma2Dec_DecodeToDic(p, lim, src, &in_cur, fin_cur, status);
-    src += in_cur;
-    in_left -= in_cur;
-    *srcLen += in_cur;
-    const SizeT produced = d->dicPos - start;
-    memcpy(dest, d->dic + start, produced);
-    dest += produced;
-    out_left -= produced;
-    *destLen += produced;
-    if (r != SZ_OK) return r;
-    if (produced == 0 || out_left == 0) return SZ_OK;
-  }
-}
-
-SRes Lzma2Decode(Byte* dest, SizeT* destLen, const Byte* src, SizeT* srcLen, Byte prop,
-                 ELzmaFinishMode finishMode, ELzmaStatus* status, ISzAlloc* alloc) {
-  const SizeT in_size = *srcLen, out_size = *destLen;
-  *destLen = 0;
-  *srcLen = 0;
-  *status = LZMA_STATUS_NOT_SPECIFIED;
-  Byte props[LZMA_PROPS_SIZE];
-  SRes r = lzma2_props(prop, props);
-  if (r != SZ_OK) return r;
-  void* host_probs = alloc->Alloc(alloc, size_t(probs_for(4, 0)) * sizeof(CLzmaProb));
-  if (host_probs == nullptr) return SZ_ERROR_MEM;
-  SizeT sl = in_size, dl = out_size;
-  int st = -1;
-  r = gpu_one_call(LZMA_GPU_KIND_LZMA2, dest, &dl, src, &sl, &prop, 1, finishMode, &st);
-  if (r == SZ_OK && st == LZMA_STATUS_NEEDS_MORE_INPUT) r = SZ_ERROR_INPUT_EOF;  // Lzma2Dec.c:350
-  alloc->Free(alloc, host_probs);
-  *srcLen = sl;
-  *destLen = dl;
-  if (st >= 0) *status = ELzmaStatus(st);
-  return r;
-}
 
 // ------------------------------------------------------------------ batch extension
 
@@ -697,21 +151,11 @@ size_t LzmaGpu_PlanBatch(LzmaGpuStreamDesc* descs, size_t n, uint32_t* order) {
   }
 }
 
-// CUs the planner sizes for: the current device's, else MI355X's 256.
-static uint32_t device_cus() {
-  int dev = 0, v = 0, cnt = 0;
-  if (hipGetDeviceCount(&cnt) != hipSuccess || cnt <= 0) return 256;
-  if (hipGetDevice(&dev) != hipSuccess) return 256;
-  if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0)
-    return 256;
-  return uint32_t(v);
-}
-
 // Planner defaults with the experiment overrides of the environment, read at
 // call time (LZGPU_KERNEL=global|throughput|latency|coop, LZGPU_MASK=1|2,
 // LZGPU_COOP=0|1, LZGPU_CUS, LZGPU_LANES, LZGPU_GROUPS, LZGPU_OCC,
 // LZGPU_PERSIST=0, LZGPU_CLASSES=1, LZGPU_SLICE_ALIGN8=1, LZGPU_KERNEL_LZMA2=1,
-// LZGPU_COOP_LAT=1, LZGPU_MERGE_LAT=0, LZGPU_ILV=0, LZGPU_ILV_ANY=1).  Only LzmaGpu_PlanBatchEx reads them;
+// LZGPU_COOP_LAT=1, LZGPU_MERGE_LAT=0, LZGPU_ILV=0, LZGPU_ILV_ANY=1, LZGPU_THR_FIT=1).  Only LzmaGpu_PlanBatchEx reads them;
 // LzmaGpu_PlanBatchOpt takes its options from the caller alone.
 static LzmaGpuPlanOptions env_options() {
   LzmaGpuPlanOptions o;
@@ -742,7 +186,8 @@ static LzmaGpuPlanOptions env_options() {
             (env_int("LZGPU_COOP_LAT", 0) ? LZMA_GPU_PLAN_COOP_LAT : 0u) |
             (env_int("LZGPU_MERGE_LAT", 1) ? 0u : LZMA_GPU_PLAN_NO_MERGE_LAT) |
             (env_int("LZGPU_ILV", 1) ? 0u : LZMA_GPU_PLAN_NO_ILV) |
-            (env_int("LZGPU_ILV_ANY", 0) ? LZMA_GPU_PLAN_ILV_ANY : 0u);
+            (env_int("LZGPU_ILV_ANY", 0) ? LZMA_GPU_PLAN_ILV_ANY : 0u) |
+            (env_int("LZGPU_THR_FIT", 0) ? LZMA_GPU_PLAN_THR_FIT : 0u);
   return o;
 }
 
@@ -790,12 +235,22 @@ static LzmaGpuLdsClass plan_lds_class(uint32_t stride, uint64_t count, uint32_t 
     return v;
   };
   const uint64_t per_cu_batch = (count + cus - 1) / cus;
-  const bool thr = regime == 1 || (regime == 0 && per_cu >= 64 && per_cu_batch >= 64);
+  const bool fit = (o.flags & LZMA_GPU_PLAN_THR_FIT) != 0;
+  const bool thr = regime == 1 || (regime == 0 && per_cu >= 64 &&
+                                    (per_cu_batch >= 64 || (fit && per_cu_batch >= 16)));
   uint32_t lanes = 1, groups = 16;
   if (latency) *latency = !thr;
   if (thr) {
     lanes = std::max<uint32_t>(1, std::min<uint32_t>(32, pow2floor(std::max<uint32_t>(1, per_cu / 8))));
     groups = pow2floor(std::max<uint32_t>(1, std::min<uint32_t>(per_cu / lanes, 16)));
+    if (fit && per_cu_batch < uint64_t(lanes) * groups) {
+      // the batch does not fill the CU at full width: narrower waves, same
+      // workgroups per CU (>= 2 waves per SIMD) -- instead of full-width waves
+      // on a quarter of the SIMDs (a 16,384-stream batch is 64 streams per
+      // CU: 2 of 8 workgroups at 32 lanes)
+      lanes = std::max<uint32_t>(
+          1, pow2floor(uint32_t(std::max<uint64_t>(1, per_cu_batch / std::max<uint32_t>(groups, 1)))));
+    }
   } else {
     // one lane per wave: as many waves as LDS allows, up to the 16 the
     // register budget keeps resident; a power of two unless the caller
@@ -1034,30 +489,70 @@ SRes LzmaGpu_PlanBatchOpt(LzmaGpuStreamDesc* descs, size_t n, uint32_t* order, L
   return plan_batch_nothrow(descs, n, order, plan, opt ? *opt : env_options());
 }
 
-// Internal streams for concurrent class launches, one set per host thread and
-// device (created on first use, kept for the process: like the scratch
-// buffers, they are per-call resources the caller never sees).
+// Internal streams for concurrent class launches: a pool per device, guarded
+// by a mutex.  A call takes a set for the duration of its enqueueing and puts
+// it back; sets are created only when every existing one is taken, so the
+// pool grows to the number of threads that enqueue batches at the same time,
+// not to the number of threads that ever did.  Reusing a set from another
+// thread is safe: work on its streams only orders behind earlier work, and a
+// wait on an event captures the event's state at the time of the wait.
 struct ClassStreams {
-  hipStream_t s[LZMA_GPU_MAX_CLASSES];
-  hipEvent_t fork, join[LZMA_GPU_MAX_CLASSES];
-};
-static ClassStreams* class_streams() {
-  static thread_local ClassStreams* per_dev[64] = {};
+  hipStream_t s[LZMA_GPU_MAX_CLASSES] = {};
+  hipEvent_t fork = nullptr, join[LZMA_GPU_MAX_CLASSES] = {};
   int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-  if (!per_dev[dev]) {
-    ClassStreams* c = new ClassStreams();
-    bool ok = hipEventCreateWithFlags(&c->fork, hipEventDisableTiming) == hipSuccess;
-    for (int k = 0; k < LZMA_GPU_MAX_CLASSES && ok; ++k)
-      ok = hipStreamCreateWithFlags(&c->s[k], hipStreamNonBlocking) == hipSuccess &&
-           hipEventCreateWithFlags(&c->join[k], hipEventDisableTiming) == hipSuccess;
-    if (!ok) {
-      set_error("class streams: creation failed");
-      return nullptr;  // (a failed set is not cached: the next call retries)
-    }
-    per_dev[dev] = c;
+};
+static void destroy_class_streams(ClassStreams* c) {
+  if (!c) return;
+  for (int k = 0; k < LZMA_GPU_MAX_CLASSES; ++k) {
+    if (c->s[k]) (void)hipStreamDestroy(c->s[k]);
+    if (c->join[k]) (void)hipEventDestroy(c->join[k]);
   }
-  return per_dev[dev];
+  if (c->fork) (void)hipEventDestroy(c->fork);
+  delete c;
+}
+struct ClassStreamPool {
+  std::mutex mu;
+  std::vector<ClassStreams*> free_sets[kLzgpuMaxDevices];
+};
+static ClassStreamPool& class_stream_pool() {
+  static ClassStreamPool* p = new ClassStreamPool();  // process lifetime (HIP teardown order)
+  return *p;
+}
+static ClassStreams* class_streams_acquire() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kLzgpuMaxDevices) return nullptr;
+  ClassStreamPool& P = class_stream_pool();
+  {
+    std::lock_guard<std::mutex> g(P.mu);
+    if (!P.free_sets[dev].empty()) {
+      ClassStreams* c = P.free_sets[dev].back();
+      P.free_sets[dev].pop_back();
+      return c;
+    }
+  }
+  ClassStreams* c = new (std::nothrow) ClassStreams();
+  if (!c) return nullptr;
+  c->dev = dev;
+  bool ok = hipEventCreateWithFlags(&c->fork, hipEventDisableTiming) == hipSuccess;
+  for (int k = 0; k < LZMA_GPU_MAX_CLASSES && ok; ++k)
+    ok = hipStreamCreateWithFlags(&c->s[k], hipStreamNonBlocking) == hipSuccess &&
+         hipEventCreateWithFlags(&c->join[k], hipEventDisableTiming) == hipSuccess;
+  if (!ok) {
+    destroy_class_streams(c);  // whatever part of the set was created
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  return c;
+}
+static void class_streams_release(ClassStreams* c) {
+  if (!c) return;
+  ClassStreamPool& P = class_stream_pool();
+  std::lock_guard<std::mutex> g(P.mu);
+  try {
+    P.free_sets[c->dev].push_back(c);
+  } catch (const std::exception&) {
+    destroy_class_streams(c);
+  }
 }
 
 SRes LzmaGpu_DecodeBatchEx(const LzmaGpuPlan* plan, const LzmaGpuStreamDesc* d_descs,
@@ -1078,22 +573,35 @@ SRes LzmaGpu_DecodeBatchEx(const LzmaGpuPlan* plan, const LzmaGpuStreamDesc* d_d
   // previous one frees.  LZGPU_CLASS_STREAMS=0: one stream (A/B).
   uint32_t live = 0;
   for (uint32_t k = 0; k < plan->n_classes; ++k) live += plan->classes[k].n ? 1u : 0u;
+  {
+    uint64_t sum = 0;
+    for (uint32_t k = 0; k < plan->n_classes; ++k) sum += plan->classes[k].n;
+    if (sum > plan->n_lds) return SZ_ERROR_PARAM;
+  }
   const bool fork = live > 1 && env_int("LZGPU_CLASS_STREAMS", 1) != 0;
-  ClassStreams* cs = fork ? class_streams() : nullptr;
-  if (fork && !cs) return SZ_ERROR_FAIL;
-  if (cs && !hip_ok(hipEventRecord(cs->fork, st), "class fork")) return SZ_ERROR_FAIL;
+  // concurrent classes are a speed-up only: without a stream set (resource
+  // exhaustion) the classes run one after another on the caller's stream
+  ClassStreams* cs = fork ? class_streams_acquire() : nullptr;
+  if (cs && hipEventRecord(cs->fork, st) != hipSuccess) {
+    (void)hipGetLastError();
+    class_streams_release(cs);
+    cs = nullptr;
+  }
+  SRes ret = SZ_OK;
   uint64_t first = 0;
-  for (uint32_t k = 0; k < plan->n_classes; ++k) {
+  for (uint32_t k = 0; k < plan->n_classes && ret == SZ_OK; ++k) {
     const LzmaGpuLdsClass& c = plan->classes[k];
     if (c.n == 0) continue;
-    if (first + c.n > plan->n_lds) return SZ_ERROR_PARAM;
     const uint32_t max_groups = plan->persistent ? cus * c.groups_per_cu : 0u;
     uint32_t* queue = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(d_workspace) +
                                                   plan->queue_offset + 64 * k);
     hipStream_t sk = st;
     if (cs) {
       sk = cs->s[k];
-      if (!hip_ok(hipStreamWaitEvent(sk, cs->fork, 0), "class fork")) return SZ_ERROR_FAIL;
+      if (!hip_ok(hipStreamWaitEvent(sk, cs->fork, 0), "class fork")) {
+        ret = SZ_ERROR_FAIL;
+        break;
+      }
     }
     if (lzgpu_launch_decode_lds(d_descs, d_order + first, uint32_t(c.n), d_src, d_dst, ws,
                                 d_results, c.lanes_per_group, c.lds_cells_per_lane,
@@ -1101,13 +609,18 @@ SRes LzmaGpu_DecodeBatchEx(const LzmaGpuPlan* plan, const LzmaGpuStreamDesc* d_d
                                 c.flags, LzgpuSlots{c.slot_off, c.slot_cells, c.slot_groups},
                                 sk) != 0) {
       set_error("LDS decode kernel launch failed");
-      return SZ_ERROR_FAIL;
+      ret = SZ_ERROR_FAIL;
+      break;
     }
     if (cs && (!hip_ok(hipEventRecord(cs->join[k], sk), "class join") ||
-               !hip_ok(hipStreamWaitEvent(st, cs->join[k], 0), "class join")))
-      return SZ_ERROR_FAIL;
+               !hip_ok(hipStreamWaitEvent(st, cs->join[k], 0), "class join"))) {
+      ret = SZ_ERROR_FAIL;
+      break;
+    }
     first += c.n;
   }
+  class_streams_release(cs);
+  if (ret != SZ_OK) return ret;
   const uint32_t n_lds = uint32_t(plan->n_lds), n_glob = uint32_t(plan->n - plan->n_lds);
   if (n_glob && lzgpu_launch_decode_batch(d_descs, d_order + n_lds, n_glob, d_src, d_dst, ws,
                                           d_results, st) != 0) {
@@ -1369,32 +882,39 @@ void CrcGenerateTable(void) {}  // tables are compile-time constants on the devi
 static uint32_t crc_host_one(uint32_t init, const void* data, size_t size, uint32_t xorout) {
   if (!ensure_device()) return 0;
   if (size == 0) return init ^ xorout;
-  Scratch& S = scratch();
+  lzgpu_host::CallScratch* S = lzgpu_host::scratch_acquire();
+  if (!S) return 0;
   const uint64_t cap = size;
   const size_t nch = CrcGpu_PlanChunks(&cap, 1, nullptr, nullptr);
-  std::vector<uint32_t> meta(1 + nch, 0);
-  CrcGpu_PlanChunks(&cap, 1, meta.data(), meta.data() + 1);
-  const uint64_t ol[2] = {0, cap};
-  uint8_t* d_data = static_cast<uint8_t*>(S.src.get(size));
-  uint8_t* d_meta = static_cast<uint8_t*>(S.crc_meta.get(16 + 4 * (1 + nch) + 8));
-  uint32_t* d_chunks = static_cast<uint32_t*>(S.crc_chunks.get(4 * (nch + 1)));
+  // one upload: [offset, length | chunk base | chunk ranges]
+  std::vector<uint32_t> meta(4 + 1 + nch, 0);
+  meta[2] = uint32_t(cap);
+  meta[3] = uint32_t(cap >> 32);
+  CrcGpu_PlanChunks(&cap, 1, meta.data() + 4, meta.data() + 5);
+  uint8_t* d_data = static_cast<uint8_t*>(S->buf[0].get(size));
+  uint8_t* d_meta = static_cast<uint8_t*>(S->buf[1].get(4 * meta.size() + 8));
+  uint32_t* d_chunks = static_cast<uint32_t*>(S->buf[2].get(4 * (nch + 1)));
+  uint32_t out = 0;
+  const hipStream_t st = S->stream;
   if (!d_data || !d_meta || !d_chunks) {
     set_error("CRC: device allocation failed");
-    return 0;
+  } else {
+    uint64_t* d_ol = reinterpret_cast<uint64_t*>(d_meta);
+    uint32_t* d_base = reinterpret_cast<uint32_t*>(d_meta + 16);
+    uint32_t* d_crc = reinterpret_cast<uint32_t*>(d_meta + 4 * meta.size());
+    if (hip_ok(hipMemcpyAsync(d_data, data, size, hipMemcpyHostToDevice, st), "CRC H2D") &&
+        hip_ok(hipMemcpyAsync(d_meta, meta.data(), 4 * meta.size(), hipMemcpyHostToDevice, st),
+               "CRC H2D") &&
+        lzgpu_launch_crc_arrays(d_data, d_ol, d_ol + 1, 1, d_base, d_base + 1, uint32_t(nch), init,
+                                xorout, d_chunks, d_crc, st) == 0 &&
+        hip_ok(hipMemcpyAsync(&out, d_crc, 4, hipMemcpyDeviceToHost, st), "CRC D2H") &&
+        hip_ok(hipStreamSynchronize(st), "CRC kernel")) {
+    } else {
+      out = 0;
+    }
   }
-  uint64_t* d_ol = reinterpret_cast<uint64_t*>(d_meta);
-  uint32_t* d_base = reinterpret_cast<uint32_t*>(d_meta + 16);
-  uint32_t* d_crc = d_base + 1 + nch;
-  uint32_t out = 0;
-  if (!hip_ok(hipMemcpy(d_data, data, size, hipMemcpyHostToDevice), "CRC H2D") ||
-      !hip_ok(hipMemcpy(d_ol, ol, 16, hipMemcpyHostToDevice), "CRC H2D") ||
-      !hip_ok(hipMemcpy(d_base, meta.data(), 4 * (1 + nch), hipMemcpyHostToDevice), "CRC H2D"))
-    return 0;
-  if (lzgpu_launch_crc_arrays(d_data, d_ol, d_ol + 1, 1, d_base, d_base + 1, uint32_t(nch), init,
-                              xorout, d_chunks, d_crc, nullptr) != 0 ||
-      !hip_ok(hipDeviceSynchronize(), "CRC kernel") ||
-      !hip_ok(hipMemcpy(&out, d_crc, 4, hipMemcpyDeviceToHost), "CRC D2H"))
-    return 0;
+  (void)hipStreamSynchronize(st);  // host buffers are reused after return
+  lzgpu_host::scratch_release(S);
   return out;
 }
 
@@ -1416,4 +936,58 @@ namespace lzgpu_host {
 bool ensure_device() { return ::ensure_device(); }
 void set_error(const char* what) { ::set_error(what); }
 bool hip_ok(hipError_t e, const char* what) { return ::hip_ok(e, what); }
+uint32_t device_cus() { return ::device_cus(); }
+
+namespace {
+struct ScratchPool {
+  std::mutex mu;
+  std::vector<CallScratch*> free_sets[kLzgpuMaxDevices];
+};
+ScratchPool& scratch_pool() {
+  static ScratchPool* p = new ScratchPool();  // process lifetime (HIP teardown order)
+  return *p;
+}
+}  // namespace
+
+CallScratch* scratch_acquire() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kLzgpuMaxDevices) {
+    ::set_error("scratch: no current device");
+    return nullptr;
+  }
+  ScratchPool& P = scratch_pool();
+  {
+    std::lock_guard<std::mutex> g(P.mu);
+    if (!P.free_sets[dev].empty()) {
+      CallScratch* s = P.free_sets[dev].back();
+      P.free_sets[dev].pop_back();
+      return s;
+    }
+  }
+  CallScratch* s = new (std::nothrow) CallScratch();
+  if (!s) {
+    ::set_error("scratch: host allocation failed");
+    return nullptr;
+  }
+  s->dev = dev;
+  if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess) {
+    (void)hipGetLastError();
+    ::set_error("scratch: stream creation failed");
+    delete s;
+    return nullptr;
+  }
+  return s;
+}
+
+void scratch_release(CallScratch* s) {
+  if (!s) return;
+  ScratchPool& P = scratch_pool();
+  std::lock_guard<std::mutex> g(P.mu);
+  try {
+    P.free_sets[s->dev].push_back(s);
+  } catch (const std::exception&) {
+    (void)hipStreamDestroy(s->stream);
+    delete s;
+  }
+}
 }  // namespace lzgpu_host

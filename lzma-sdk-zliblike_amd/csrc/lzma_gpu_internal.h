@@ -6,11 +6,22 @@
 
 #include "lzma_lane.h"
 
+// Devices the library keeps per-device state for (launch attributes, class
+// streams, CU counts, dictionary mirrors).
+constexpr int kLzgpuMaxDevices = 64;
+
 extern "C" int lzgpu_launch_decode_batch(const LzmaGpuStreamDesc* d_descs, const uint32_t* d_order,
                                          uint32_t n, const uint8_t* d_src, uint8_t* d_dst,
                                          uint16_t* d_ws, LzmaGpuResult* d_results,
                                          hipStream_t stream);
 extern "C" int lzgpu_launch_session(LzgpuSession* d_sess, uint32_t n, hipStream_t stream);
+// cooperative sessions: one 32-lane wave per session, tables of at most
+// lds_cells cells staged in LDS for the call; max_groups 0 = one per session
+extern "C" int lzgpu_launch_session_coop(LzgpuSession* d_sess, uint32_t n, uint32_t lds_cells,
+                                         uint32_t max_groups, hipStream_t stream);
+// largest table (cells) the cooperative session kernel stages in LDS: lc+lp <= 4
+// at any pb (LZMA2's bound, 28 KiB) and wider LZMA tables up to 64 KiB
+constexpr uint32_t kSessCoopMaxCells = 32768;
 // Slot area of a lane-interleaved class (LZMA_GPU_PLAN_ILV): `off` cells into
 // the workspace, `cells` rows of kIlv cells per lane group, room for `groups`
 // workgroups.
@@ -56,6 +67,9 @@ namespace lzgpu_host {
 bool ensure_device();
 void set_error(const char* what);
 bool hip_ok(hipError_t e, const char* what);
+// CUs of the current device once the library has started the HIP runtime
+// (ensure_device), else MI355X's 256 without touching the runtime
+uint32_t device_cus();
 
 // host CRC-32 for container metadata (7zCrc.c semantics; headers, a few
 // bytes per block -- decoded data is checked on the GPU)
@@ -74,6 +88,52 @@ inline uint32_t crc32_host(const uint8_t* p, size_t n) {
   for (size_t i = 0; i < n; ++i) c = t[(c ^ p[i]) & 0xFFu] ^ (c >> 8);
   return c ^ 0xFFFFFFFFu;
 }
+
+// Grow-only device buffer on one device (per-call scratch of the host-buffer
+// entry points; pooled per device, see CallScratch).
+struct DevBuf {
+  void* p = nullptr;
+  size_t cap = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  ~DevBuf() {
+    if (p) (void)hipFree(p);
+  }
+  void* get(size_t n) {
+    if (n == 0) n = 16;
+    if (p && cap >= n) return p;
+    size_t want = n > cap * 2 ? n : cap * 2;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    if (hipMalloc(&p, want) != hipSuccess) {
+      (void)hipGetLastError();
+      p = nullptr;
+      if (hipMalloc(&p, n) != hipSuccess) {
+        (void)hipGetLastError();
+        p = nullptr;
+        return nullptr;
+      }
+      want = n;
+    }
+    cap = want;
+    return p;
+  }
+};
+
+// Scratch of one host-buffer call (LzmaDecode, LzmaUncompress, the CRC
+// drop-ins, ...): device buffers plus a non-blocking stream of its own, taken
+// from a per-device pool for the call and returned after it.  The pool grows
+// to the number of calls in flight at once, not to the number of threads that
+// ever called (nothing is thread-local, nothing leaks per thread).
+struct CallScratch {
+  DevBuf buf[4];
+  hipStream_t stream = nullptr;
+  int dev = 0;
+};
+CallScratch* scratch_acquire();  // current device; nullptr (error set) on failure
+void scratch_release(CallScratch* s);
 
 // owning device array for the container drivers' per-call buffers
 template <class T>

@@ -16,9 +16,31 @@
 // The per-lane work is in lzma_lane.h.
 #include <hip/hip_runtime.h>
 
+#include <mutex>
+#include <set>
+#include <utility>
+
 #include "lzma_gpu_internal.h"
 
 using namespace lzgpu;
+
+// Dynamic-LDS limit of a kernel raised to the CU's 160 KiB once per device
+// (the attribute is per device: a process driving several GPUs, or threads
+// whose first launches race, each get it set before their launch).
+static int allow_full_lds(const void* kfn) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kLzgpuMaxDevices) return -1;
+  static std::mutex mu;
+  static std::set<std::pair<const void*, int>> done;
+  std::lock_guard<std::mutex> g(mu);
+  if (done.count({kfn, dev})) return 0;
+  if (hipFuncSetAttribute(kfn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) !=
+      hipSuccess)
+    return -1;
+  done.insert({kfn, dev});
+  return 0;
+}
+
 
 __global__ void __launch_bounds__(64) lzgpu_decode_batch_kernel(
     const LzmaGpuStreamDesc* __restrict__ descs, const uint32_t* __restrict__ order, uint32_t n,
@@ -107,6 +129,55 @@ __global__ void __launch_bounds__(64) lzgpu_session_kernel(LzgpuSession* __restr
   lane_session(sess[lane]);
 }
 
+// One DecodeToDic / DecodeToBuf call per workgroup of one 32-lane wave on a
+// device-resident decoder (the drop-in LzmaDec_DecodeToDic / DecodeToBuf of a
+// host CLzmaDec, and small session batches): the wave-cooperative decoder with
+// the session's whole table staged in LDS for the call -- loaded from
+// q.probs, decoded on (literal trees by lane speculation, every other table
+// access an LDS round trip instead of a global one), written back.  Placement
+// 0x7FF keeps the all-global layout's offsets, so the copy is a straight one.
+// Dynamic LDS: the widest table of the batch's sessions (the launcher checks).
+constexpr uint32_t kSessCoopMask = LZGPU_LDS_MASK_ALL | kCoopBit;
+__global__ void __launch_bounds__(32) lzgpu_session_coop_kernel(LzgpuSession* __restrict__ sess,
+                                                                 uint32_t n, uint32_t lds_cells) {
+  extern __shared__ uint32_t lz_smem[];
+  lds_u16* lo = (lds_u16*)((uint16_t*)lz_smem);
+  for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
+    LzgpuSession q = sess[i];
+    const uint32_t cells = table_cells(q.lc, q.lp, q.pb);
+    if (cells > lds_cells) {  // planned for narrower tables: refuse, state untouched
+      if (threadIdx.x == 0) {
+        sess[i].res = kErrMem;
+        sess[i].status = kStNone;
+      }
+      continue;
+    }
+    gu16* gp = (gu16*)q.probs;
+    for (uint32_t j = threadIdx.x; j < cells; j += blockDim.x) lo[j] = gp[j];
+    __syncthreads();
+    lane_session<kSessCoopMask>(q, lo);
+    __syncthreads();
+    for (uint32_t j = threadIdx.x; j < cells; j += blockDim.x) gp[j] = lo[j];
+    if (threadIdx.x == 0) sess[i] = q;
+    __syncthreads();
+  }
+}
+
+extern "C" int lzgpu_launch_session_coop(LzgpuSession* d_sess, uint32_t n, uint32_t lds_cells,
+                                         uint32_t max_groups, hipStream_t stream) {
+  if (n == 0) return 0;
+  const size_t lds = size_t(lds_cells) * 2;
+  if (lds_cells == 0 || lds > 160 * 1024) return -1;
+  if (lds > 64 * 1024 &&
+      allow_full_lds(reinterpret_cast<const void*>(lzgpu_session_coop_kernel)) != 0)
+    return -1;
+  uint32_t grid = n;
+  if (max_groups && grid > max_groups) grid = max_groups;
+  hipLaunchKernelGGL(lzgpu_session_coop_kernel, dim3(grid), dim3(32), lds, stream, d_sess, n,
+                     lds_cells);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
 extern "C" int lzgpu_launch_decode_batch(const LzmaGpuStreamDesc* d_descs, const uint32_t* d_order,
                                          uint32_t n, const uint8_t* d_src, uint8_t* d_dst,
                                          uint16_t* d_ws, LzmaGpuResult* d_results,
@@ -125,12 +196,8 @@ static int launch_lds(const LzmaGpuStreamDesc* d_descs, const uint32_t* d_order,
                       LzmaGpuResult* d_results, uint32_t lanes, uint32_t stride,
                       uint32_t groups_per_cu, uint32_t max_groups, uint32_t* d_queue,
                       const LzgpuSlots& sl, hipStream_t stream) {
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(lzgpu_decode_lds_kernel<W, M, K2>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    attr_set = true;
-  }
+  if (allow_full_lds(reinterpret_cast<const void*>(lzgpu_decode_lds_kernel<W, M, K2>)) != 0)
+    return -1;
   if (hipMemsetAsync(d_queue, 0, sizeof(uint32_t), stream) != hipSuccess) return -1;
   // pad each workgroup's LDS so that exactly groups_per_cu fit on a CU (an
   // even split over its four SIMDs), whatever the dispatcher would pack
@@ -161,12 +228,8 @@ static int launch_coop(const LzmaGpuStreamDesc* d_descs, const uint32_t* d_order
                        const uint8_t* d_src, uint8_t* d_dst, uint16_t* d_ws,
                        LzmaGpuResult* d_results, uint32_t stride, uint32_t groups_per_cu,
                        uint32_t max_groups, uint32_t* d_queue, hipStream_t stream) {
-  static bool attr_set = false;
-  if (!attr_set) {
-    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(lzgpu_decode_coop_kernel<W, M, K2>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    attr_set = true;
-  }
+  if (allow_full_lds(reinterpret_cast<const void*>(lzgpu_decode_coop_kernel<W, M, K2>)) != 0)
+    return -1;
   if (hipMemsetAsync(d_queue, 0, sizeof(uint32_t), stream) != hipSuccess) return -1;
   size_t lds = size_t(stride) * 2;
   if (groups_per_cu) {

@@ -196,16 +196,23 @@ __device__ __forceinline__ LzmaGpuResult lane_decode_lds(const LzmaGpuStreamDesc
 
 // One LzmaDec_DecodeToDic call (LzmaDec.c:719-838) on a device-resident
 // decoder (compact layout, all sections in q.probs, for the current lc/lp/pb).
+// M = 0: the table is used in place (lo = gl = q.probs); M = every section in
+// LDS | kCoopBit: the cooperative session kernel staged q.probs into `lo` (the
+// offsets of placement 0x7FF equal those of the all-global layout).
+template <uint32_t M = 0u, class Lo = gu16*>
 __device__ __forceinline__ int session_to_dic(LzgpuSession& q, uint64_t dic_limit,
                                               const gbyte* in, uint64_t& in_len, int fin,
-                                              int& status) {
-  LzStateT<gu16*> s;
+                                              int& status, Lo lo = Lo()) {
+  LzStateT<Lo> s;
   s.lc = q.lc;
   s.lp = q.lp;
   s.pb = q.pb;
   s.dict_size = q.dict_size;
   s.gl = (gu16*)q.probs;
-  s.lo = s.gl;
+  if constexpr (M == 0u)
+    s.lo = s.gl;
+  else
+    s.lo = lo;
   s.dic = (gbyte*)q.dic;
   s.cap = q.dic_buf_size;
   s.pos = q.dic_pos;
@@ -223,7 +230,7 @@ __device__ __forceinline__ int session_to_dic(LzgpuSession& q, uint64_t dic_limi
   s.need_state_init = q.need_init_state;
   s.tmp_n = q.temp_buf_size;
   for (int i = 0; i < int(kLookahead); ++i) s.tmp[i] = q.temp_buf[i];
-  const int res = lz_decode_to_dic<true, 0u>(s, dic_limit, in, in_len, fin, status);
+  const int res = lz_decode_to_dic<true, M>(s, dic_limit, in, in_len, fin, status);
   q.dic_pos = s.pos;
   q.range = s.range;
   q.code = s.code;
@@ -247,11 +254,15 @@ __device__ __forceinline__ int session_to_dic(LzgpuSession& q, uint64_t dic_limi
 // dic_buf_size bytes; each pass decodes up to the ring end or the caller's
 // remaining room, copies the new bytes to `out`, and stops on an error, on a
 // pass that produced nothing, or when `out` is full).
-__device__ __forceinline__ void lane_session(LzgpuSession& q) {
+// Under the cooperative placement every lane of the wave runs the call and
+// has itself stored every dictionary byte, so the produced bytes are copied out
+// lane-strided (each lane reads only bytes it wrote).
+template <uint32_t M = 0u, class Lo = gu16*>
+__device__ __forceinline__ void lane_session(LzgpuSession& q, Lo lo = Lo()) {
   int status = kStNone;
   if (q.mode != 1) {
     uint64_t sl = q.in_len;
-    q.res = session_to_dic(q, q.dic_limit, (const gbyte*)q.in, sl, q.finish_mode, status);
+    q.res = session_to_dic<M>(q, q.dic_limit, (const gbyte*)q.in, sl, q.finish_mode, status, lo);
     q.status = status;
     q.in_used = sl;
     return;
@@ -273,12 +284,19 @@ __device__ __forceinline__ void lane_session(LzgpuSession& q) {
       fin = q.finish_mode;
     }
     uint64_t in_cur = in_left;
-    res = session_to_dic(q, lim, in + in_done, in_cur, fin, status);
+    res = session_to_dic<M>(q, lim, in + in_done, in_cur, fin, status, lo);
     in_done += in_cur;
     in_left -= in_cur;
     const uint64_t produced = q.dic_pos - start;
     const gbyte* from = (const gbyte*)q.dic + start;
-    for (uint64_t i = 0; i < produced; ++i) out[out_done + i] = from[i];
+#ifndef LZGPU_HOST_EMU
+    if constexpr ((M & kCoopBit) != 0u) {
+      for (uint64_t i = threadIdx.x; i < produced; i += blockDim.x) out[out_done + i] = from[i];
+    } else
+#endif
+    {
+      for (uint64_t i = 0; i < produced; ++i) out[out_done + i] = from[i];
+    }
     out_done += produced;
     out_left -= produced;
     if (res != kOk || produced == 0 || out_left == 0) break;

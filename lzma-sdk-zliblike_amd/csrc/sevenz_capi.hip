@@ -354,9 +354,13 @@ SRes read_substreams(Sd& s, Ar& a, SubStreams& ss) {
     if (t == kCRC || t == kSize || t == kEnd) break;
     RINOK7(skip_data(s));
   }
-  // a folder's substreams after its first each need a size (>= 1 header byte):
-  // more than that cannot be described by the bytes left
-  if (uint64_t(ss.n) > uint64_t(s.n) + a.folders.size()) return SZ_ERROR_ARCHIVE;
+  // With a kSize section a folder's substreams after its first each need a
+  // size (>= 1 header byte): more than that cannot be described by the bytes
+  // left.  Without one the reference takes any count it can allocate (sizes
+  // of all but a folder's last substream stay unset there); counts past 2^24
+  // fail as its allocation would (SZ_ERROR_MEM) instead of being attempted.
+  if (t == kSize && uint64_t(ss.n) > uint64_t(s.n) + a.folders.size()) return SZ_ERROR_ARCHIVE;
+  if (ss.n > (1u << 24)) return SZ_ERROR_MEM;
   ss.sizes.assign(ss.n, 0);
   ss.defined.assign(ss.n, 0);
   ss.digests.assign(ss.n, 0);
@@ -516,9 +520,12 @@ SRes read_header(Archive& x, Sd& s) {
   if (t != kFilesInfo) return SZ_ERROR_ARCHIVE;
   uint32_t nf;
   RINOK7(rd_num32(s, &nf));
-  // file properties cost >= 1 bit per file (kEmptyStream) or >= 2 bytes (names);
-  // a count the header bytes left cannot describe is malformed, not allocated
-  if (uint64_t(nf) > 8 * uint64_t(s.n) + 64) return SZ_ERROR_ARCHIVE;
+  // A file with a stream needs no header byte of its own (no name, sizes and
+  // CRCs from the substreams: 7zIn.c:986-1104 accepts that); an empty-stream
+  // file costs >= 1 bit of the kEmptyStream vector.  A count beyond both is
+  // malformed, not allocated.
+  if (uint64_t(nf) > 8 * uint64_t(s.n) + 64 + (have_ss ? uint64_t(ss.n) : 0))
+    return SZ_ERROR_ARCHIVE;
   x.files.assign(nf, FileItem());
   std::vector<Byte> empty_stream, empty_file, defined;
   uint32_t n_empty = 0;

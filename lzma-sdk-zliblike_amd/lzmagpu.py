@@ -187,6 +187,7 @@ _sig = {
     "LzmaDec_InitDicAndState": (None, [ctypes.POINTER(CLzmaDec), ctypes.c_int, ctypes.c_int]),
     "LzmaDec_DecodeToDic": (ctypes.c_int, [ctypes.POINTER(CLzmaDec), ctypes.c_size_t, _P, _sp, ctypes.c_int, _ip]),
     "LzmaDec_DecodeToBuf": (ctypes.c_int, [ctypes.POINTER(CLzmaDec), _P, _sp, _P, _sp, ctypes.c_int, _ip]),
+    "LzmaGpu_DecoderRelease": (None, [ctypes.POINTER(CLzmaDec)]),
     "LzmaDecode": (ctypes.c_int, [_P, _sp, _P, _sp, ctypes.c_char_p, ctypes.c_uint, ctypes.c_int, _ip, ctypes.POINTER(ISzAlloc)]),
     "LzmaUncompress": (ctypes.c_int, [_P, _sp, _P, _sp, ctypes.c_char_p, ctypes.c_size_t]),
     "Lzma2Dec_AllocateProbs": (ctypes.c_int, [ctypes.POINTER(CLzma2Dec), ctypes.c_ubyte, ctypes.POINTER(ISzAlloc)]),
@@ -351,6 +352,47 @@ def stream_decode(src, props, out_total, in_chunk, out_chunk, finish, max_calls=
     finally:
         _lib.LzmaDec_Free(ctypes.byref(dec), ctypes.byref(g_alloc))
     return len(trace), trace, out.raw[:out_pos], in_pos
+
+
+def dic_decode(src, props, out_total, win, max_calls=100000, out=None):
+    """The 7zDec.c:127-171 (SzDecodeLzma) loop over LzmaDec_DecodeToDic:
+    LzmaDec_AllocateProbs, dic = the whole output buffer (dicBufSize =
+    out_total), LzmaDec_Init, then DecodeToDic(out_total, FINISH_END) over look
+    windows of at most `win` input bytes -- the same contract as the oracle's
+    orc_lzma_dic_decode.  `out` (optional): a ctypes buffer of >= out_total bytes
+    to decode into.  Returns (calls, trace[(res, status, srcLen, dicPos)],
+    out bytes, in_used)."""
+    dec = CLzmaDec()
+    dec.dic = None
+    dec.probs = None
+    r = _lib.LzmaDec_AllocateProbs(ctypes.byref(dec), bytes(props), 5, ctypes.byref(g_alloc))
+    if r != SZ_OK:
+        return -r, [], b"", 0
+    sbuf = _buf(src)
+    if out is None:
+        out = ctypes.create_string_buffer(max(out_total, 1))
+    dec.dic = ctypes.addressof(out)
+    dec.dicBufSize = out_total
+    _lib.LzmaDec_Init(ctypes.byref(dec))
+    base_s = ctypes.addressof(sbuf)
+    in_pos = 0
+    trace = []
+    try:
+        while len(trace) < max_calls:
+            sl = ctypes.c_size_t(min(len(src) - in_pos, win))
+            pos0 = dec.dicPos
+            st = ctypes.c_int(-1)
+            res = _lib.LzmaDec_DecodeToDic(ctypes.byref(dec), out_total, base_s + in_pos,
+                                           ctypes.byref(sl), LZMA_FINISH_END, ctypes.byref(st))
+            trace.append((res, st.value, sl.value, dec.dicPos))
+            in_pos += sl.value
+            if res != SZ_OK:
+                break
+            if dec.dicPos == out_total or (sl.value == 0 and dec.dicPos == pos0):
+                break
+    finally:
+        _lib.LzmaDec_FreeProbs(ctypes.byref(dec), ctypes.byref(g_alloc))
+    return len(trace), trace, out.raw[:dec.dicPos], in_pos
 
 
 # ---------------------------------------------------------------- batch API

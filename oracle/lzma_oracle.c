@@ -759,6 +759,47 @@ int orc_lzma_stream_decode(const uint8_t *props, const uint8_t *src, size_t src_
   return calls;
 }
 
+/* The 7zDec.c:127-171 (SzDecodeLzma) loop: dic = the caller's whole output
+ * buffer, LzmaDec_DecodeToDic(out_total, FINISH_END) over look windows of at
+ * most `win` input bytes -- same contract as ref_lzma_dic_decode in
+ * ref_lzma_shim.c (trace = {res, status, srcLen, dicPos} per call). */
+int orc_lzma_dic_decode(const uint8_t *props, const uint8_t *src, size_t src_total,
+                        uint8_t *out, size_t out_total, size_t win, long long *trace,
+                        int max_calls, size_t *out_len, size_t *in_used) {
+  orc_dec d;
+  size_t in_pos = 0;
+  int calls = 0, res;
+  memset(&d, 0, sizeof d);
+  res = orc_props_parse(&d.pr, props, 5);
+  if (res != RES_OK) { *out_len = 0; *in_used = 0; return -res; }
+  d.nprobs = orc_num_probs(&d.pr);
+  d.probs = (uint16_t *)malloc((size_t)d.nprobs * sizeof(uint16_t));
+  if (!d.probs) { *out_len = 0; *in_used = 0; return -RES_MEM; }
+  d.dic = out;
+  d.dic_cap = out_total;
+  orc_init(&d);
+  while (calls < max_calls) {
+    size_t sl = src_total - in_pos, pos0 = d.dic_pos;
+    int st = -1;
+    if (sl > win) sl = win;
+    res = orc_decode_to_dic(&d, out_total, src + in_pos, &sl, FIN_END, &st);
+    if (trace) {
+      trace[4 * calls + 0] = res;
+      trace[4 * calls + 1] = st;
+      trace[4 * calls + 2] = (long long)sl;
+      trace[4 * calls + 3] = (long long)d.dic_pos;
+    }
+    calls++;
+    in_pos += sl;
+    if (res != RES_OK) break;
+    if (d.dic_pos == d.dic_cap || (sl == 0 && d.dic_pos == pos0)) break;
+  }
+  free(d.probs);
+  *out_len = d.dic_pos;
+  *in_used = in_pos;
+  return calls;
+}
+
 /* ---------------------------------------------------------------- LZMA2 */
 
 enum {

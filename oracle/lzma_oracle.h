@@ -36,6 +36,13 @@ int orc_lzma_stream_decode(const uint8_t *props, const uint8_t *src, size_t src_
                            size_t out_chunk, int finish_mode, long long *trace,
                            int max_calls, size_t *out_len, size_t *in_used);
 
+/* The 7zDec.c:127-171 loop: LzmaDec_DecodeToDic (FINISH_END) over a dictionary
+ * that is the whole output, input in look windows of at most `win` bytes --
+ * same contract as ref_lzma_dic_decode in ref_lzma_shim.c. */
+int orc_lzma_dic_decode(const uint8_t *props, const uint8_t *src, size_t src_total,
+                        uint8_t *out, size_t out_total, size_t win, long long *trace,
+                        int max_calls, size_t *out_len, size_t *in_used);
+
 /* LZMA2 over a flat dictionary (Lzma2Dec.c:90-289, 7zDec.c:181-202 usage). */
 int orc_lzma2_decode(uint8_t *dst, size_t *dst_len, const uint8_t *src, size_t *src_len,
                      uint8_t prop, int finish_mode, int *status);

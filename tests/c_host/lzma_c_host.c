@@ -9,6 +9,8 @@
  *   lzma_c_host PROPS_FILE STREAM_FILE OUT_SIZE IN_CHUNK OUT_CHUNK
  *
  * One line per API: name res status destLen srcLen crc32(output) [calls].
+ * LzmaDec_DecodeToDic drives the 7zDec.c:127-171 loop (dic = the whole
+ * output, look windows of IN_CHUNK input bytes, FINISH_END).
  * The streaming loop is the fork's SzDecodeLzmaToFileWithBuf shape
  * (7zDec.c:567-648): input fed IN_CHUNK bytes at a time, output windows of
  * OUT_CHUNK bytes, FINISH_ANY, until the output total or the end mark.
@@ -93,6 +95,34 @@ int main(int argc, char **argv) {
     }
     printf("LzmaDec_DecodeToBuf %d %d %zu %zu %08x %zu\n", (int)r, (int)st, out_pos, in_pos,
            (unsigned)CrcCalc(out, out_pos), calls);
+  }
+  { /* LzmaDec.h dictionary interface, the 7zDec.c:127-171 (SzDecodeLzma) shape:
+       dic = the whole output buffer, DecodeToDic(FINISH_END) over look windows of
+       IN_CHUNK input bytes */
+    CLzmaDec dec;
+    size_t in_pos = 0, calls = 0;
+    SRes r;
+    ELzmaStatus st = LZMA_STATUS_NOT_SPECIFIED;
+    LzmaDec_Construct(&dec);
+    dec.dicPos = 0;
+    memset(out, 0, out_size);
+    r = LzmaDec_AllocateProbs(&dec, props, LZMA_PROPS_SIZE, &g_Alloc);
+    if (r == SZ_OK) {
+      dec.dic = out;
+      dec.dicBufSize = out_size;
+      LzmaDec_Init(&dec);
+      for (;;) {
+        SizeT sl = ns - in_pos, pos0 = dec.dicPos;
+        if (sl > in_chunk) sl = in_chunk;
+        r = LzmaDec_DecodeToDic(&dec, out_size, src + in_pos, &sl, LZMA_FINISH_END, &st);
+        calls++;
+        in_pos += sl;
+        if (r != SZ_OK || dec.dicPos == dec.dicBufSize || (sl == 0 && dec.dicPos == pos0)) break;
+      }
+      LzmaDec_FreeProbs(&dec, &g_Alloc);
+    }
+    printf("LzmaDec_DecodeToDic %d %d %zu %zu %08x %zu\n", (int)r, (int)st, (size_t)dec.dicPos,
+           in_pos, (unsigned)CrcCalc(out, dec.dicPos), calls);
   }
   free(out);
   free(src);

@@ -1,7 +1,7 @@
 """Generate tests/golden/sz_cases.json + sz_blob.bin from the REFERENCE 7z
 reader (SzArEx_Open + SzArEx_Extract, 7zIn.c / 7zDec.c) compiled in place.
 
-Run in the build container only (needs oracle/_ref/libref.so from
+Run in the build container only (needs oracle/_ref/libref.so (container library) from
 `make -f oracle/Makefile.ref`):
 
     python tests/golden/make_golden_7z.py
@@ -194,7 +194,7 @@ def _copy_size_mismatch(f):
 
 
 def main():
-    lib = native._load(native.REF_SO)
+    lib = native.ref_cont()
     lib.ref_7z_extract.restype = ctypes.c_int
     lib.ref_7z_extract.argtypes = [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_char_p,
                                    ctypes.c_size_t, _sp, ctypes.c_void_p, ctypes.c_void_p,

@@ -51,7 +51,7 @@ def ref_decode(lib, m, c, j, r, out_size, overlap=False):
 
 
 def main():
-    lib = native.ref()
+    lib = native.ref_cont()
     blob = bytearray()
     seen = {}
 

@@ -72,7 +72,7 @@ def branchy(kind, seed, n):
 
 
 def main():
-    lib = native.ref()
+    lib = native.ref_cont()
     for k in KINDS:
         f = getattr(lib, k + "_Convert")
         f.restype = ctypes.c_size_t

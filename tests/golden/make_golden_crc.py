@@ -1,6 +1,6 @@
 """Generate tests/golden/crc_cases.json from the REFERENCE CRC-32 (7zCrc.c).
 
-Run in the build container only (needs oracle/_ref/libref.so from
+Run in the build container only (needs oracle/_ref/libref.so (container library) from
 `make -f oracle/Makefile.ref`, which compiles 7zCrc.c / 7zCrcOpt.c /
 CpuArch.c in place):
 
@@ -30,7 +30,7 @@ def case_bytes(c):
 
 
 def main():
-    lib = native._load(native.REF_SO)
+    lib = native.ref_cont()
     lib.CrcGenerateTable.restype = None
     lib.CrcGenerateTable()
     upd, calc = native.crc_funcs(lib, "CrcUpdate", "CrcCalc")

@@ -1,7 +1,7 @@
 """Generate tests/golden/xz_cases.json + xz_blob.bin from the REFERENCE xz
 decoder (XzUnpacker_Code, XzDec.c) and x86 BCJ (x86_Convert, Bra86.c).
 
-Run in the build container only (needs oracle/_ref/libref.so from
+Run in the build container only (needs oracle/_ref/libref.so (container library) from
 `make -f oracle/Makefile.ref`, which compiles XzDec.c, Xz.c, XzCrc64.c,
 Sha256.c and the branch converters in place):
 
@@ -57,7 +57,7 @@ def x86_like(seed, n):
 
 
 def main():
-    lib = native._load(native.REF_SO)
+    lib = native.ref_cont()
     lib.ref_xz_decode.restype = ctypes.c_int
     lib.ref_xz_decode.argtypes = [ctypes.c_char_p, _sp, ctypes.c_char_p, _sp, _ip, _ip]
     lib.ref_x86_convert.restype = ctypes.c_size_t

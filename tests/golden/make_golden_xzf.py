@@ -3,7 +3,7 @@ carry the filters beyond x86 (Delta, PPC, IA64, ARM, ARMT, SPARC and chains
 of them), decoded by the REFERENCE xz decoder (XzUnpacker_Code, XzDec.c, whose
 BraState_Code drives Bra.c / BraIA64.c / Delta.c).
 
-Run in the build container only (needs oracle/_ref/libref.so from
+Run in the build container only (needs oracle/_ref/libref.so (container library) from
 `make -f oracle/Makefile.ref`):
 
     python tests/golden/make_golden_xzf.py
@@ -37,7 +37,7 @@ FID = {"PPC": lzma.FILTER_POWERPC, "IA64": lzma.FILTER_IA64, "ARM": lzma.FILTER_
 
 
 def main():
-    lib = native._load(native.REF_SO)
+    lib = native.ref_cont()
     lib.ref_xz_decode.restype = ctypes.c_int
     lib.ref_xz_decode.argtypes = [ctypes.c_char_p, _sp, ctypes.c_char_p, _sp, _ip, _ip]
     text = native.gen("text", 1900, 200000)

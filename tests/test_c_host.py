@@ -71,7 +71,7 @@ def test_c_host_builds_and_fails_loudly_without_gpu(tmp_path):
         {"id": lzma.FILTER_LZMA1, "dict_size": 1 << 16, "lc": 3, "lp": 0, "pb": 2}])
     out = _run(str(tmp_path), bytes([0x5D]) + (1 << 16).to_bytes(4, "little"), comp,
                len(data), 1000, 4096)
-    for name in ("LzmaUncompress", "LzmaDecode", "LzmaDec_DecodeToBuf"):
+    for name in ("LzmaUncompress", "LzmaDecode", "LzmaDec_DecodeToBuf", "LzmaDec_DecodeToDic"):
         assert out[name][0] == "11", (name, out[name])  # SZ_ERROR_FAIL, nothing decoded
         assert out[name][2] == "0"
 
@@ -114,6 +114,9 @@ def test_gpu_c_host_matches_oracle(tmp_path):
         calls, trace, dec, used = native.stream_decode(orc, "orc", comp, props, n, in_chunk,
                                                        out_chunk, 0)
         assert out["LzmaDec_DecodeToBuf"] == [str(trace[-1][0]), str(trace[-1][1]), str(len(dec)),
+                                              str(used), "%08x" % zlib.crc32(dec), str(calls)]
+        calls, trace, dec, used, _ = native.dic_decode(orc, "orc", comp, props, n, in_chunk)
+        assert out["LzmaDec_DecodeToDic"] == [str(trace[-1][0]), str(trace[-1][1]), str(len(dec)),
                                               str(used), "%08x" % zlib.crc32(dec), str(calls)]
 
 

@@ -445,6 +445,48 @@ def test_cfg5_full_count_mixed_props(L, torch):
         assert out == plain
 
 
+def test_cfg5_full_length_1_to_256k(L, torch):
+    """BASELINE config 5 at its stated size: 32,768 streams, lc 0-4,
+    lp 0-2 (lc + lp <= 4), pb 0-4, dict 4K-1M, lengths log-uniform 1 KiB-256 KiB
+    (1.46 GB decompressed), end mark on half -- one planned batch, round trip to
+    the plaintext and exact per-stream results; a 512-stream sample (every 64th
+    stream) against the oracle's LzmaDecode, output and results.  Encoded by
+    liblzma preset 1 so the 1.5 GB encode fits a test (the encoder does not
+    affect decode parity; bench.py's cfg5 leg encodes preset 6)."""
+    count = 32768
+    with ThreadPoolExecutor(W.workers()) as ex:
+        parts = list(ex.map(lambda i: W.cfg5_stream(i, max_log2=8, preset=1), range(count)))
+    nout = np.array([len(p[0]) for p in parts], dtype=np.uint64)
+    lens = np.array([len(p[1]) for p in parts], dtype=np.uint64)
+    fin = np.array([p[3] for p in parts])
+    assert nout.min() >= 1024 and nout.max() <= 262144 and nout.max() > 200000
+    so = np.zeros(count, np.uint64)
+    so[1:] = np.cumsum(lens)[:-1]
+    do = np.zeros(count, np.uint64)
+    do[1:] = np.cumsum(nout)[:-1]
+    descs = L.make_descs([dict(src_off=int(so[i]), src_len=int(lens[i]), dst_off=int(do[i]),
+                               dst_cap=int(nout[i]), props=parts[i][2], finish=int(fin[i]))
+                          for i in range(count)])
+    comp = np.frombuffer(b"".join(p[1] for p in parts), dtype=np.uint8)
+    plan, res, d_dst = _device_decode(L, torch, descs, comp, int(nout.sum()))
+    assert plan.n_lds == count
+    want_status = np.where(fin == 1, 1, 2)
+    assert (res["res"] == 0).all() and (res["status"] == want_status).all()
+    assert (res["dest_len"] == nout).all()
+    assert (res["src_len"][fin == 1] == lens[fin == 1]).all()
+    out = d_dst[:int(nout.sum())].cpu().numpy()
+    for i in range(count):
+        assert out[int(do[i]):int(do[i] + nout[i])].tobytes() == parts[i][0], i
+    orc = native.oracle()
+    comp_b = comp.tobytes()
+    for i in range(0, count, 64):
+        s = comp_b[int(so[i]):int(so[i] + lens[i])]
+        e = native.decode(orc, "orc", s, parts[i][2], int(nout[i]), int(fin[i]))
+        assert (int(res["res"][i]), int(res["status"][i]), int(res["dest_len"][i]),
+                int(res["src_len"][i])) == e[:4], i
+        assert out[int(do[i]):int(do[i]) + e[2]].tobytes() == e[4], i
+
+
 def test_cfg4_1024_lzma2_blocks_coop_kernel(L, torch):
     """BASELINE config 4's per-GPU shard: 1,024 LZMA2 dict-reset blocks of 1 MiB
     (lc3/lp0/pb2, dict 1 MiB) in one file, split on the host by chunk headers,
