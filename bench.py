@@ -1599,7 +1599,11 @@ def main():
     comp_bytes = int(lens.sum())
     dev = torch.device("cuda", local_rank)
     d_src = torch.from_numpy(np.concatenate([comp, np.zeros(16, np.uint8)])).to(dev)
-    d_dst = torch.empty(count * n, dtype=torch.uint8, device=dev)
+    # LZGPU_SHADOW_BYTES: room behind the output for the attribution build's
+    # repeated output stores (lzma_device.h LZGPU_SHADOW_OUT); 0 otherwise
+    shadow = int(os.environ.get("LZGPU_SHADOW_BYTES", "0"))
+    d_dst_full = torch.empty(count * n + shadow, dtype=torch.uint8, device=dev)
+    d_dst = d_dst_full[:count * n]
     d_ws = torch.empty(max(ws_bytes, 16), dtype=torch.uint8, device=dev)
     d_desc = torch.frombuffer(bytearray(descs), dtype=torch.uint8).to(dev)
     d_order = torch.frombuffer(bytearray(order), dtype=torch.uint8).to(dev)

@@ -236,7 +236,7 @@ size_t LzmaGpu_PlanBatch(LzmaGpuStreamDesc *descs, size_t n, uint32_t *order);
  * LZGPU_OCC=<1|2|4 waves per SIMD>, LZGPU_CUS, LZGPU_COOP=0|1,
  * LZGPU_PERSIST=0 (one stream per lane), LZGPU_CLASSES=1 (one LDS launch),
  * LZGPU_SLICE_ALIGN8=1, LZGPU_KERNEL_LZMA2=1, LZGPU_COOP_LAT=1, LZGPU_MERGE_LAT=0, LZGPU_ILV=0,
- * LZGPU_ILV_ANY=1 (the
+ * LZGPU_ILV_ANY=1, LZGPU_THR_FIT=0 (the
  * LZMA_GPU_PLAN_* flags below); DecodeBatchEx reads LZGPU_CLASS_STREAMS=0
  * (classes launched one after another on the caller's stream).
  * workspace_bytes includes the LDS launches' work counters at queue_offset
@@ -333,12 +333,12 @@ typedef struct LzmaGpuPlanOptions {
 /* A/B: interleaved rows for throughput waves of any width up to 64 lanes, not
  * only whole 32-lane groups (LZGPU_ILV_ANY=1) */
 #define LZMA_GPU_PLAN_ILV_ANY 32u
-/* throughput classes whose batch does not fill the CU at full wave width
- * (fewer than lanes x workgroups streams per CU, e.g. a strong-scaling share)
- * run narrower waves at the same workgroups per CU instead of full-width
- * waves on part of the SIMDs, and the throughput regime starts at 16 streams
- * per CU instead of 64 (LZGPU_THR_FIT=1) */
-#define LZMA_GPU_PLAN_THR_FIT 64u
+/* Default: a single-class batch of 17 to 63 streams per CU in the latency
+ * regime (a strong-scaling share, e.g. 8,192 x 4 KiB on 256 CUs) runs waves
+ * of 2-4 streams so that every stream is resident at once, instead of
+ * one-stream waves in several rounds.  This flag restores the round-2 shape
+ * (LZGPU_THR_FIT=0). */
+#define LZMA_GPU_PLAN_NO_THR_FIT 64u
 
 /* LzmaGpu_PlanBatchEx with explicit options (opt == NULL: as PlanBatchEx,
  * whose defaults take the LZGPU_* experiment variables of the environment,

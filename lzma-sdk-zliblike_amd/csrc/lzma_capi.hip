@@ -155,7 +155,7 @@ size_t LzmaGpu_PlanBatch(LzmaGpuStreamDesc* descs, size_t n, uint32_t* order) {
 // call time (LZGPU_KERNEL=global|throughput|latency|coop, LZGPU_MASK=1|2,
 // LZGPU_COOP=0|1, LZGPU_CUS, LZGPU_LANES, LZGPU_GROUPS, LZGPU_OCC,
 // LZGPU_PERSIST=0, LZGPU_CLASSES=1, LZGPU_SLICE_ALIGN8=1, LZGPU_KERNEL_LZMA2=1,
-// LZGPU_COOP_LAT=1, LZGPU_MERGE_LAT=0, LZGPU_ILV=0, LZGPU_ILV_ANY=1, LZGPU_THR_FIT=1).  Only LzmaGpu_PlanBatchEx reads them;
+// LZGPU_COOP_LAT=1, LZGPU_MERGE_LAT=0, LZGPU_ILV=0, LZGPU_ILV_ANY=1, LZGPU_THR_FIT=0).  Only LzmaGpu_PlanBatchEx reads them;
 // LzmaGpu_PlanBatchOpt takes its options from the caller alone.
 static LzmaGpuPlanOptions env_options() {
   LzmaGpuPlanOptions o;
@@ -187,7 +187,7 @@ static LzmaGpuPlanOptions env_options() {
             (env_int("LZGPU_MERGE_LAT", 1) ? 0u : LZMA_GPU_PLAN_NO_MERGE_LAT) |
             (env_int("LZGPU_ILV", 1) ? 0u : LZMA_GPU_PLAN_NO_ILV) |
             (env_int("LZGPU_ILV_ANY", 0) ? LZMA_GPU_PLAN_ILV_ANY : 0u) |
-            (env_int("LZGPU_THR_FIT", 0) ? LZMA_GPU_PLAN_THR_FIT : 0u);
+            (env_int("LZGPU_THR_FIT", 1) ? 0u : LZMA_GPU_PLAN_NO_THR_FIT);
   return o;
 }
 
@@ -197,7 +197,8 @@ static LzmaGpuPlanOptions env_options() {
 // 2 = latency shape (one stream per wave) forced.
 static LzmaGpuLdsClass plan_lds_class(uint32_t stride, uint64_t count, uint32_t mask,
                                       uint32_t cus, int regime, const LzmaGpuPlanOptions& o,
-                                      bool* latency = nullptr, bool any_groups = false) {
+                                      bool* latency = nullptr, bool any_groups = false,
+                                      bool allow_fit = false) {
   LzmaGpuLdsClass c;
   memset(&c, 0, sizeof c);
   c.lds_mask = mask;
@@ -235,28 +236,34 @@ static LzmaGpuLdsClass plan_lds_class(uint32_t stride, uint64_t count, uint32_t 
     return v;
   };
   const uint64_t per_cu_batch = (count + cus - 1) / cus;
-  const bool fit = (o.flags & LZMA_GPU_PLAN_THR_FIT) != 0;
-  const bool thr = regime == 1 || (regime == 0 && per_cu >= 64 &&
-                                    (per_cu_batch >= 64 || (fit && per_cu_batch >= 16)));
+  const bool thr = regime == 1 || (regime == 0 && per_cu >= 64 && per_cu_batch >= 64);
   uint32_t lanes = 1, groups = 16;
   if (latency) *latency = !thr;
   if (thr) {
     lanes = std::max<uint32_t>(1, std::min<uint32_t>(32, pow2floor(std::max<uint32_t>(1, per_cu / 8))));
     groups = pow2floor(std::max<uint32_t>(1, std::min<uint32_t>(per_cu / lanes, 16)));
-    if (fit && per_cu_batch < uint64_t(lanes) * groups) {
-      // the batch does not fill the CU at full width: narrower waves, same
-      // workgroups per CU (>= 2 waves per SIMD) -- instead of full-width waves
-      // on a quarter of the SIMDs (a 16,384-stream batch is 64 streams per
-      // CU: 2 of 8 workgroups at 32 lanes)
-      lanes = std::max<uint32_t>(
-          1, pow2floor(uint32_t(std::max<uint64_t>(1, per_cu_batch / std::max<uint32_t>(groups, 1)))));
-    }
   } else {
     // one lane per wave: as many waves as LDS allows, up to the 16 the
     // register budget keeps resident; a power of two unless the caller
     // (a merged class, persistent lanes drawing from one queue) takes any
     groups = std::min<uint32_t>(per_cu, 16);
     if (!any_groups) groups = pow2floor(groups);
+    // Fitted latency shape (strong-scaling shares, profiles/r03_shares/): a
+    // batch of 17-63 streams per CU would run one-stream waves in two or more
+    // rounds; widen the waves instead so that every stream is resident at
+    // once -- 8,192 x 4 KiB (32 per CU): 2 lanes x 16 waves 5.64 ms vs 7.46 ms
+    // in two rounds (and vs 5.95 ms for 4-lane throughput waves).  Only for a
+    // batch that is one class (mixed-width batches merge their one-lane
+    // classes instead: config 5 4.58 GB/s fitted vs 5.00).
+    // LZMA_GPU_PLAN_NO_THR_FIT: the round-2 shape.
+    if (allow_fit && !(o.flags & LZMA_GPU_PLAN_NO_THR_FIT) && regime != 2 &&
+        per_cu_batch > groups && per_cu_batch < 64 && groups > 0) {
+      uint32_t want = uint32_t((per_cu_batch + groups - 1) / groups);
+      uint32_t l = 1;
+      while (l < want) l <<= 1;
+      while (l > 1 && uint64_t(l) * groups > per_cu) l >>= 1;
+      lanes = l;
+    }
   }
   const uint32_t over = o.lanes_per_group;
   if (over > 0 && over <= 64 && over * stride * 2 <= lds_per_cu) {
@@ -332,7 +339,7 @@ static SRes plan_batch(LzmaGpuStreamDesc* descs, size_t n, uint32_t* order, Lzma
   // lands in the latency regime is re-planned with the latency placement (more
   // tables in LDS, few streams per CU); few streams per CU go cooperative.
   auto plan_bucket = [&](const std::vector<uint32_t>& idx, uint32_t stride_lo,
-                         bool any_groups) -> LzmaGpuLdsClass {
+                         bool any_groups, bool allow_fit = false) -> LzmaGpuLdsClass {
     bool lat = false;
     const int regime = o.kernel == LZMA_GPU_KERNEL_THROUGHPUT ? 1 : 0;
     LzmaGpuLdsClass c = plan_lds_class(stride_lo, idx.size(), LZGPU_LDS_MASK, cus, regime, o,
@@ -344,7 +351,8 @@ static SRes plan_batch(LzmaGpuStreamDesc* descs, size_t n, uint32_t* order, Lzma
     for (uint32_t i : idx) stride_lat = std::max(stride_lat, w_lat[i]);
     if (stride_lat > kMaxLdsCells) return c;
     c = plan_lds_class(stride_lat, idx.size(), LZGPU_LDS_MASK_LAT, cus,
-                       o.kernel == LZMA_GPU_KERNEL_AUTO ? 0 : 2, o, nullptr, any_groups);
+                       o.kernel == LZMA_GPU_KERNEL_AUTO ? 0 : 2, o, nullptr, any_groups,
+                       allow_fit);
     // few streams per CU: the wave-cooperative kernel (all 32 lanes on one
     // stream, literal trees decided by lane speculation) -- config 4
     // 1.71 -> 2.85 GB/s and the xz leg 1.45 -> 2.36 at 4 streams per CU;
@@ -397,6 +405,8 @@ static SRes plan_batch(LzmaGpuStreamDesc* descs, size_t n, uint32_t* order, Lzma
       merged = t;
     }
   }
+  int n_buckets = 0;
+  for (int b = 0; b < LZMA_GPU_MAX_CLASSES; ++b) n_buckets += bucket_idx[b].empty() ? 0 : 1;
   size_t k = 0;
   uint64_t best = 0;
   std::vector<uint8_t> in_slots;  // items of lane-interleaved classes
@@ -405,7 +415,8 @@ static SRes plan_batch(LzmaGpuStreamDesc* descs, size_t n, uint32_t* order, Lzma
     if (bucket_idx[b].empty()) continue;
     std::stable_sort(bucket_idx[b].begin(), bucket_idx[b].end(), by_len);
     for (uint32_t i : bucket_idx[b]) order[k++] = i;
-    LzmaGpuLdsClass c = plan_bucket(bucket_idx[b], bucket_stride[b], b == merged);
+    LzmaGpuLdsClass c = plan_bucket(bucket_idx[b], bucket_stride[b], b == merged,
+                                    n_buckets == 1);
     if (o.flags & LZMA_GPU_PLAN_KERNEL_LZMA2) c.flags |= LZMA_GPU_CLASS_HAS_LZMA2;
     for (uint32_t i : bucket_idx[b])
       if (descs[i].kind == LZMA_GPU_KIND_LZMA2) {

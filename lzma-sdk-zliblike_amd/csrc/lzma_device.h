@@ -101,7 +101,7 @@ __host__ __device__ __forceinline__ Layout make_layout(uint32_t lc, uint32_t lp,
   Layout L;
   uint32_t a = 0, b = 0;
   // literal sections first: every literal tree starts 8-byte aligned in
-  // either table (LZGPU_LIT_2RT reads its cells four at a time)
+  // either table
   for (uint32_t k = 0; k < S_NSEC; ++k) {
     const uint32_t sec = k < 2 ? S_LITP + k : (k - 2 < S_LITP ? k - 2 : k);
     const uint32_t n = sec_cells(sec, lc, lp, pb);
@@ -167,25 +167,6 @@ typedef __attribute__((address_space(1))) uint32_t gu32;
 // to its column with cell arithmetic scaled by the row length.
 constexpr uint32_t kIlvBit = 0x40000000u;
 constexpr uint32_t kIlv = 32u;
-// LZGPU_ILV_PAIR (A/B flag): cells interleaved two at a time instead -- cells
-// 2k, 2k+1 of a lane side by side in row k (128 bytes for 32 lanes), so the two
-// children of a tree node come in one 32-bit read
-#ifndef LZGPU_ILV_PAIR
-#define LZGPU_ILV_PAIR 0
-#endif
-#if LZGPU_ILV_PAIR
-__host__ __device__ __forceinline__ uint32_t ilv_cell(uint32_t i) {
-  return ((i & ~1u) << 5) + (i & 1u);  // row i / 2 of 2 * kIlv cells, slot i % 2
-}
-struct GS {
-  gu16* p;     // the lane's column (two cells wide)
-  uint32_t i;  // logical cell
-  __device__ __forceinline__ GS operator+(uint32_t k) const { return GS{p, i + k}; }
-  __device__ __forceinline__ gu16& operator[](uint32_t k) const { return p[ilv_cell(i + k)]; }
-  __device__ __forceinline__ gu16& operator*() const { return p[ilv_cell(i)]; }
-};
-constexpr uint32_t kIlvLaneCells = 2u;
-#else
 struct GS {
   gu16* p;
   __device__ __forceinline__ GS operator+(uint32_t k) const { return GS{p + kIlv * k}; }
@@ -193,144 +174,29 @@ struct GS {
   __device__ __forceinline__ gu16& operator*() const { return *p; }
 };
 constexpr uint32_t kIlvLaneCells = 1u;
-#endif
 
-// Build-time code-shape switches (A/B'd on MI355X):
-//   LZGPU_NORM_BRANCHLESS  NORMALIZE as selects instead of a skip-able branch
-//   LZGPU_BIT_MASK         decision/update: 0 if/else, 1 mask arithmetic, 2 selects
-//                          with the shared-form update p - ((p - m) >> 5) (default)
-#ifndef LZGPU_NORM_BRANCHLESS
-#define LZGPU_NORM_BRANCHLESS 0
-#endif
-// branch-free NORMALIZE after a checkpoint (GlobalReaderQ) -- A/B flag
-#ifndef LZGPU_NORMU_BRANCHLESS
-#define LZGPU_NORMU_BRANCHLESS 0
-#endif
-#ifndef LZGPU_BIT_MASK
-#define LZGPU_BIT_MASK 2
-#endif
-//   LZGPU_TREE_PF      bit-trees read both children of the next level (one
-//                      32-bit read) while the current decision resolves
-//   LZGPU_MB_PF        the matched-literal byte dic[pos - rep0] is loaded as
-//                      soon as a match ends, not after the next IsMatch decision
-//   LZGPU_COPY_SHORT   overlapping matches (rep0 < 8) load the period once and
-//                      replicate it from registers instead of byte round trips
-//   LZGPU_READER16     input window refilled 16 bytes per load (one vmcnt drain
-//                      per 16 input bytes instead of per 4)
-//   LZGPU_COPY_V2      match copies: every 8-byte step is one batch of loads
-//                      (the tail too, stores predicated), and rep0 < 8 builds
-//                      the periodic pattern in a register once -- one load
-//                      round trip per 8 bytes instead of one per tail byte
-#ifndef LZGPU_TREE_PF
-#define LZGPU_TREE_PF 0
-#endif
-#ifndef LZGPU_MB_PF
-#define LZGPU_MB_PF 1
-#endif
-#ifndef LZGPU_COPY_SHORT
-#define LZGPU_COPY_SHORT 0
-#endif
-#ifndef LZGPU_READER16
-#define LZGPU_READER16 1
-#endif
-//   LZGPU_READER_SPLIT the 16-byte refill as two 8-byte loads into the two
-//                      halves' own registers
-#ifndef LZGPU_READER_SPLIT
-#define LZGPU_READER_SPLIT 0
-#endif
-//   LZGPU_LIT_2RT      plain literal tree in two memory round trips (levels
-//                      0-3 from one batch of reads, 4-7 from a second)
-#ifndef LZGPU_LIT_2RT
-#define LZGPU_LIT_2RT 0
-#endif
-//   LZGPU_LIT_UNIFIED  plain and matched literals on one instruction path
-//                      (lz_literal_unified) in the literal batch
-#ifndef LZGPU_LIT_UNIFIED
-#define LZGPU_LIT_UNIFIED 0
-#endif
-//   LZGPU_READER_Q     checkpoint reader (GlobalReaderQ): the literal batch's
-//                      IsMatch + literal decisions normalize without refill
-//                      checks; the window is topped up before IsMatch and
-//                      between the literal tree's two halves
-#ifndef LZGPU_READER_Q
-#define LZGPU_READER_Q 1
-#endif
-//   LZGPU_LIT_PF       plain literal tree (checkpoint reader) with the next
-//                      level's cell pair read ahead of each decision
-#ifndef LZGPU_LIT_PF
-#define LZGPU_LIT_PF 0
-#endif
-//   LZGPU_MATCH_FAT    match path with fewer dependent global round trips:
-//                      the whole length coder of a posState in one load batch
-//                      (LenHigh in 3), SpecPos in <= 2, Align in 1
-#ifndef LZGPU_MATCH_FAT
-#define LZGPU_MATCH_FAT 1
-#endif
-//   (applied to every placement but the throughput one, LZGPU_LDS_MASK: with
-//   up to 32 lanes per wave its extra load instructions cost more in the
-//   vector-memory pipeline than the round trips they save -- config 3 28.1 vs
-//   27.6 GB/s, config 5 +1.5 %)
-#ifndef LZGPU_COPY_V2
-#define LZGPU_COPY_V2 0
-#endif
-//   LZGPU_COPY_WIDE    match copies with unaligned 8-byte loads/stores (and a
-//                      register-built pattern when rep0 < 8)
-#ifndef LZGPU_COPY_WIDE
-#define LZGPU_COPY_WIDE 1
-#endif
-//   LZGPU_LIT_WC       literal batch output write-combined in a register
-#ifndef LZGPU_LIT_WC
-#define LZGPU_LIT_WC 0
-#endif
+// Build-time knobs still in use (A/B runs):
 //   LZGPU_LIT_BATCH    literals decoded per pass of the symbol loop before a
 //                      lane's match path runs (1 = one symbol per pass)
+//   LZGPU_PROF         profiling build: wave-uniform cycle stamps per region
+// The code shapes measured and rejected in rounds 1-2 (branch-free NORMALIZE,
+// tree child-pair prefetch, two-round-trip literal trees, unified plain /
+// matched literals, literal write-combining, byte-wise and batched-tail copies,
+// threshold / divergent batch exits, nontemporal input / output, pair-
+// interleaved rows, ...) were removed in round 3; their A/B evidence stays in
+// DESIGN.md §4 and profiles/.  The kept shapes are unconditional: decision and
+// update as selects in the shared form, the checkpoint reader in the bulk pass
+// of the throughput and cooperative placements (the 16-byte per-byte-checked
+// reader elsewhere), the matched byte prefetched at match end (throughput and
+// cooperative kernels), global bit trees three levels per load batch, the
+// length coder / SpecPos / Align in fewer round trips off the throughput
+// placement, the matched literal's eight all-match cells in one batch, match
+// copies with unaligned 8-byte accesses, the wave-uniform literal-batch exit.
 #ifndef LZGPU_LIT_BATCH
 #define LZGPU_LIT_BATCH 8
 #endif
-//   LZGPU_LIT_THR      with the uniform exit: leave the literal batch when fewer
-//                      than this % of the live lanes still decode literals
-//                      (0 = only when none does); LZGPU_LIT_BATCH is the cap
-#ifndef LZGPU_LIT_THR
-#define LZGPU_LIT_THR 0
-#endif
-//   LZGPU_MLIT_PF      matched literal with the matched-tree cells in global
-//                      memory: load the eight cells of the all-match path at
-//                      once (one round trip instead of up to eight)
-#ifndef LZGPU_MLIT_PF
-#define LZGPU_MLIT_PF 1
-#endif
-//   LZGPU_TAIL_LIT     decode the symbol after a match at the end of the match
-//                      path (a matched literal there, not in the plain batch)
-#ifndef LZGPU_TAIL_LIT
-#define LZGPU_TAIL_LIT 0
-#endif
 #ifndef LZGPU_PROF
 #define LZGPU_PROF 0
-#endif
-//   LZGPU_TREE_GPF     bit trees in global memory (length, slot, SpecPos, Align
-//                      under the default placement) read three levels per load
-//                      batch instead of one dependent round trip per bit
-#ifndef LZGPU_TREE_GPF
-#define LZGPU_TREE_GPF 1
-#endif
-//   LZGPU_UNIFORM_EXIT the literal batch loop exits only when every lane of
-//                      the wave is done (lanes drop out by a flag)
-//   LZGPU_IN_NT / LZGPU_OUT_NT  compressed input read / literal bytes written with
-//                      the nontemporal hint (A/B flags: input is read once, output
-//                      lines are written a byte at a time over a long time)
-#ifndef LZGPU_IN_NT
-#define LZGPU_IN_NT 0
-#endif
-#ifndef LZGPU_OUT_NT
-#define LZGPU_OUT_NT 0
-#endif
-#ifndef LZGPU_UNIFORM_EXIT
-#define LZGPU_UNIFORM_EXIT 1
-#endif
-// (write-combining needs the batch's wave-uniform exit)
-#if !LZGPU_UNIFORM_EXIT
-#undef LZGPU_LIT_WC
-#define LZGPU_LIT_WC 0
 #endif
 
 // Per-lane decoder state (CLzmaDec fields, LzmaDec.h:50-69).  lo = the LDS
@@ -374,11 +240,7 @@ struct Tab {
   // cell `off` of the global table (lane-interleaved under kIlvBit)
   __device__ __forceinline__ auto g(uint32_t off) const {
     if constexpr ((M & kIlvBit) != 0u)
-#if LZGPU_ILV_PAIR
-      return GS{gl, off};
-#else
       return GS{gl + kIlv * off};
-#endif
     else
       return gl + off;
   }
@@ -395,12 +257,19 @@ __device__ __forceinline__ uint64_t ring_back(uint64_t pos, uint32_t dist, uint6
   return pos - dist + (pos < dist ? cap : 0);
 }
 
+// LZGPU_SHADOW_OUT (attribution build, never the default): every output
+// store is repeated LZGPU_SHADOW_OUT bytes further on (the caller's buffer
+// extends that far), so the L2 -> memory write traffic the output causes shows
+// as the increase of WRITE_SIZE over the default build (traffic).
+#ifndef LZGPU_SHADOW_OUT
+#define LZGPU_SHADOW_OUT 0
+#endif
+
 // one decoded literal byte to the window
 __device__ __forceinline__ void lz_put(gbyte* p, uint32_t v) {
-#if LZGPU_OUT_NT && !defined(LZGPU_HOST_EMU)
-  __builtin_nontemporal_store(uint8_t(v), p);
-#else
   *p = uint8_t(v);
+#if LZGPU_SHADOW_OUT
+  p[LZGPU_SHADOW_OUT] = uint8_t(v);
 #endif
 }
 
@@ -413,59 +282,6 @@ alignas(16) static uint32_t g_lz_zero_word[4] = {0, 0, 0, 0};
 __device__ __attribute__((aligned(16))) uint32_t g_lz_zero_word[4] = {0, 0, 0, 0};
 #endif
 
-// Prefetching reader over a lane's compressed bytes in global memory.  Holds up
-// to 7 bytes in `win` plus one prefetched aligned word in `pend`; the word is
-// merged only when fewer than 4 bytes remain, one full word after its load
-// was issued.  The prefetch load is unconditional (an exhausted reader loads a
-// zero word from g_lz_zero_word instead), so the compiler can leave it in
-// flight until the merge instead of waiting on it at a control-flow join.
-// Never loads a word wholly outside [p, p+avail).
-struct GlobalReader {
-  const gu32* wp;  // next aligned word to prefetch
-  uint32_t left;   // words with a valid byte still to prefetch
-  uint32_t nb;     // valid bytes in win
-  uint64_t win;
-  uint32_t pend;
-  uint32_t idx;    // bytes consumed since init
-
-  __device__ __forceinline__ uint32_t fetch() {
-    const gu32* a = left ? wp : (const gu32*)g_lz_zero_word;
-    const uint32_t v = *a;
-    wp += left ? 1 : 0;
-    left -= left ? 1u : 0u;
-    return v;
-  }
-  __device__ __forceinline__ void init(const gbyte* p, uint64_t avail) {
-    const uintptr_t a = (uintptr_t)p;
-    const uintptr_t a0 = a & ~uintptr_t(3);
-    const uint32_t skip = uint32_t(a & 3);
-    const uint64_t words = avail ? (((a + avail + 3) & ~uintptr_t(3)) - a0) >> 2 : 0;
-    wp = (const gu32*)a0;
-    left = words > 0xFFFFFFF0ull ? 0xFFFFFFF0u : uint32_t(words);
-    idx = 0;
-    win = uint64_t(fetch() >> (8 * skip));
-    nb = avail ? 4 - skip : 0;
-    pend = fetch();
-  }
-  __device__ __forceinline__ uint32_t peek() const { return uint32_t(win) & 0xFFu; }
-  __device__ __forceinline__ uint32_t used() const { return idx; }
-  // consume the peeked byte when n is set
-  __device__ __forceinline__ void advance(bool n) {
-    win = n ? (win >> 8) : win;
-    nb -= n ? 1u : 0u;
-    idx += n ? 1u : 0u;
-    if (nb < 4) {
-      win |= uint64_t(pend) << (8 * nb);
-      nb += 4;
-      pend = fetch();
-    }
-  }
-  __device__ __forceinline__ uint32_t next() {
-    const uint32_t b = peek();
-    advance(true);
-    return b;
-  }
-};
 
 // Same contract, 16-byte refills: `win` holds up to 8 bytes; `nxt` is the
 // next 16-byte aligned block (its low half is taken when win empties, the high
@@ -486,12 +302,6 @@ struct GlobalReader16 {
 #ifdef LZGPU_HOST_EMU
     nlo = uint64_t(a[0]) | (uint64_t(a[1]) << 32);
     nhi = uint64_t(a[2]) | (uint64_t(a[3]) << 32);
-#elif LZGPU_READER_SPLIT
-    // two 8-byte loads straight into nlo / nhi: no 16-byte register tuple
-    // that has to be copied (and therefore waited for) at the refill
-    typedef __attribute__((address_space(1))) const uint64_t gu64c;
-    nlo = ((gu64c*)a)[0];
-    nhi = ((gu64c*)a)[1];
 #else
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
     const u32x4 v = *(const __attribute__((address_space(1))) u32x4*)a;
@@ -593,8 +403,6 @@ struct GlobalReaderQ {
     const gu32* a = left ? wp : (const gu32*)g_lz_zero_word;
 #ifdef LZGPU_HOST_EMU
     nx = u32x4{a[0], a[1], a[2], a[3]};
-#elif LZGPU_IN_NT
-    nx = __builtin_nontemporal_load((const __attribute__((address_space(1))) u32x4*)a);
 #else
     nx = *(const __attribute__((address_space(1))) u32x4*)a;
 #endif
@@ -661,11 +469,7 @@ struct GlobalReaderQ {
   }
 };
 
-#if LZGPU_READER16
 typedef GlobalReader16 PlainReader;
-#else
-typedef GlobalReader PlainReader;
-#endif
 // Reader of the bulk pass per placement: the checkpoint reader for the
 // throughput placement (many lanes per wave: a refill check in every
 // NORMALIZE fires in some lane almost every decision), the per-byte-checked
@@ -677,7 +481,6 @@ template <uint32_t M>
 struct BulkReaderFor {
   typedef PlainReader type;
 };
-#if LZGPU_READER_Q
 template <>
 struct BulkReaderFor<LZGPU_LDS_MASK> {
   typedef GlobalReaderQ type;
@@ -686,7 +489,6 @@ template <>
 struct BulkReaderFor<LZGPU_LDS_MASK | kIlvBit> {
   typedef GlobalReaderQ type;
 };
-#endif
 template <>
 struct BulkReaderFor<LZGPU_LDS_MASK_LAT | kCoopBit> {
   typedef GlobalReaderQ type;
@@ -700,7 +502,7 @@ struct BulkReaderFor<LZGPU_LDS_MASK_ALL | kCoopBit> {
   typedef GlobalReaderQ type;
 };
 
-// LZGPU_MB_PF per placement: the matched byte is prefetched at match end in
+// Matched-byte prefetch per placement: the byte at rep0 is loaded at match end in
 // the throughput and cooperative kernels; the one-stream-per-wave latency
 // kernel loads it when the literal needs it -- the register the prefetch holds
 // across the next IsMatch decision costs it scratch spills at 4 waves per SIMD
@@ -708,7 +510,7 @@ struct BulkReaderFor<LZGPU_LDS_MASK_ALL | kCoopBit> {
 // within noise either way: profiles/r02_ilv/mbpf_latency_ab.log)
 template <uint32_t M>
 __host__ __device__ constexpr bool mb_pf_on() {
-  return LZGPU_MB_PF && (((M & kCoopBit) != 0u) || ((M & ~kIlvBit) == LZGPU_LDS_MASK));
+  return ((M & kCoopBit) != 0u) || ((M & ~kIlvBit) == LZGPU_LDS_MASK);
 }
 
 // checkpoint hooks for readers without them: every NORMALIZE checks
@@ -737,68 +539,27 @@ struct LocalReader {
 
 // ------------------------------------------------------------------ range decoder
 
-// 32-bit view of a 16-bit cell pointer in the same address space
-#ifdef LZGPU_HOST_EMU
-__device__ __forceinline__ const uint32_t* wide(const uint16_t* p) { return (const uint32_t*)p; }
-__device__ __forceinline__ const uint32_t* wide(uint16_t* p) { return (const uint32_t*)p; }
-__device__ __forceinline__ uint64_t ld64(const uint16_t* p) {
-  return uint64_t(p[0]) | (uint64_t(p[1]) << 16) | (uint64_t(p[2]) << 32) |
-         (uint64_t(p[3]) << 48);
-}
-#else
-typedef __attribute__((address_space(3))) uint32_t lds_u32;
-typedef __attribute__((address_space(3))) uint64_t lds_u64;
-typedef __attribute__((address_space(1))) uint64_t gu64;
-__device__ __forceinline__ const lds_u32* wide(lds_u16* p) { return (const lds_u32*)p; }
-__device__ __forceinline__ const gu32* wide(gu16* p) { return (const gu32*)p; }
-// four cells (8-byte aligned) in one read
-__device__ __forceinline__ uint64_t ld64(lds_u16* p) { return *(const lds_u64*)p; }
-__device__ __forceinline__ uint64_t ld64(gu16* p) { return *(const gu64*)p; }
-#endif
-
 template <class Rd>
 struct Rc {
   uint32_t range, code;
   Rd* rd;
   // NORMALIZE (LzmaDec.c:17): shift in one input byte when range < 2^24
   __device__ __forceinline__ void norm() {
-#if LZGPU_NORM_BRANCHLESS
-    const bool n = range < kTop;
-    const uint32_t byte = rd->peek();
-    range = n ? (range << 8) : range;
-    code = n ? ((code << 8) | byte) : code;
-    rd->advance(n);
-#else
     if (range < kTop) {
       range <<= 8;
       code = (code << 8) | rd->next();
     }
-#endif
   }
   // NORMALIZE after a reader checkpoint: the byte is known to be in the window
   __device__ __forceinline__ void norm_u() {
-#if LZGPU_NORMU_BRANCHLESS
-    if constexpr (__is_same(Rd, GlobalReaderQ)) {
-      // selects instead of a branch: no exec-mask save/restore and no
-      // s_cbranch per decision (a wave issues one instruction per cycle
-      // window whatever its type)
-      const bool n = range < kTop;
-      code = n ? ((code << 8) | (uint32_t(rd->win) & 0xFFu)) : code;
-      range = n ? (range << 8) : range;
-      rd->win = n ? (rd->win >> 8) : rd->win;
-      rd->nb -= n ? 1u : 0u;
-      return;
-    }
-#endif
     if (range < kTop) {
       range <<= 8;
       code = (code << 8) | rd_take_u(*rd);
     }
   }
-  // decision with norm_u (the shared-form update of LZGPU_BIT_MASK 2)
+  // decision with norm_u (the shared-form update, see bit())
   template <class P>
   __device__ __forceinline__ uint32_t bit_u(P prob) {
-#if LZGPU_BIT_MASK == 2 && !LZGPU_NORM_BRANCHLESS
     const uint32_t p = *prob;
     norm_u();
     const uint32_t bound = (range >> 11) * p;
@@ -808,14 +569,10 @@ struct Rc {
     range = b ? range - bound : bound;
     code = b ? code - bound : code;
     return b ? 1u : 0u;
-#else
-    return bit(prob);
-#endif
   }
   // decision on a preloaded value p with norm_u
   template <class P>
   __device__ __forceinline__ uint32_t bit_vu(uint32_t p, P prob) {
-#if LZGPU_BIT_MASK == 2 && !LZGPU_NORM_BRANCHLESS
     norm_u();
     const uint32_t bound = (range >> 11) * p;
     const bool b = code >= bound;
@@ -824,28 +581,6 @@ struct Rc {
     range = b ? range - bound : bound;
     code = b ? code - bound : code;
     return b ? 1u : 0u;
-#else
-    return bit_v(p, prob);
-#endif
-  }
-  // The plain literal tree (8 levels from node 1) after an IsMatch
-  // checkpoint, with a second checkpoint before level 4; the next level's
-  // two cells are read (one 32-bit read) while the current decision resolves,
-  // so the tree's chain has no load latency in it.  probs 4-byte aligned.
-  template <class P>
-  __device__ __forceinline__ uint32_t lit8_pf(P probs) {
-    uint32_t m = 1;
-    uint32_t p = probs[1];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      uint32_t pair = 0;
-      if (k < 7) pair = *wide(probs + 2 * m);
-      if (k == 4) rd_topup(*rd);
-      const uint32_t b = bit_vu(p, probs + m);
-      m = (m << 1) | b;
-      if (k < 7) p = b ? (pair >> 16) : (pair & 0xFFFFu);
-    }
-    return m;
   }
   // BITS levels of an MSB-first tree from node m (no refill checks: at most
   // 5 levels after a checkpoint); returns the node reached
@@ -861,7 +596,6 @@ struct Rc {
     const uint32_t p = *prob;
     norm();
     const uint32_t bound = (range >> 11) * p;
-#if LZGPU_BIT_MASK == 2
     // selects only: with b = (code >= bound),
     //   UPDATE_0: p + ((2048 - p) >> 5) == p - ((p - 2017) >> 5)  (arithmetic >>)
     //   UPDATE_1: p - (p >> 5)          == p - ((p - 0) >> 5)
@@ -871,57 +605,15 @@ struct Rc {
     range = b ? range - bound : bound;
     code = b ? code - bound : code;
     return b ? 1u : 0u;
-#elif LZGPU_BIT_MASK
-    // mask arithmetic: lanes of a wave sit on different symbol paths, and the
-    // compiler otherwise turns the two updates into a divergent if/else
-    const uint32_t mask = 0u - uint32_t(code >= bound);
-    code -= bound & mask;
-    range = bound ^ ((bound ^ (range - bound)) & mask);
-    *prob = uint16_t(p + (((kProbOne - p) >> 5) & ~mask) - ((p >> 5) & mask));
-    return mask & 1u;
-#else
-    if (code < bound) {
-      range = bound;
-      *prob = uint16_t(p + ((kProbOne - p) >> 5));
-      return 0;
-    }
-    range -= bound;
-    code -= bound;
-    *prob = uint16_t(p - (p >> 5));
-    return 1;
-#endif
   }
   // decision on an already-loaded probability value p, update stored to *prob
   template <class P>
   __device__ __forceinline__ uint32_t bit_v(uint32_t p, P prob) {
     norm();
     const uint32_t bound = (range >> 11) * p;
-#if LZGPU_BIT_MASK == 2
     const bool b = code >= bound;
     const int32_t m = b ? 0 : int32_t(kProbOne - 31);
     *prob = uint16_t(int32_t(p) - ((int32_t(p) - m) >> 5));
-    range = b ? range - bound : bound;
-    code = b ? code - bound : code;
-    return b ? 1u : 0u;
-#endif
-    if (code < bound) {
-      range = bound;
-      *prob = uint16_t(p + ((kProbOne - p) >> 5));
-      return 0;
-    }
-    range -= bound;
-    code -= bound;
-    *prob = uint16_t(p - (p >> 5));
-    return 1;
-  }
-  // decision on probability value p; the updated value goes to np (the
-  // caller stores it) -- IF_BIT_0 / UPDATE_0 / UPDATE_1 in the shared form
-  __device__ __forceinline__ uint32_t bit_np(uint32_t p, uint32_t& np) {
-    norm();
-    const uint32_t bound = (range >> 11) * p;
-    const bool b = code >= bound;
-    const int32_t m = b ? 0 : int32_t(kProbOne - 31);
-    np = uint32_t(int32_t(p) - ((int32_t(p) - m) >> 5)) & 0xFFFFu;
     range = b ? range - bound : bound;
     code = b ? code - bound : code;
     return b ? 1u : 0u;
@@ -930,21 +622,8 @@ struct Rc {
   template <int BITS, class P>
   __device__ __forceinline__ uint32_t tree(P probs) {
     uint32_t m = 1;
-#if LZGPU_TREE_PF
-    // probs must be 4-byte aligned: children 2m, 2m+1 form one 32-bit word
-    uint32_t p = probs[1];
-#pragma unroll
-    for (int k = 0; k < BITS; ++k) {
-      uint32_t pair = 0;
-      if (k + 1 < BITS) pair = *wide(probs + 2 * m);
-      const uint32_t b = bit_v(p, probs + m);
-      m = (m << 1) | b;
-      if (k + 1 < BITS) p = b ? (pair >> 16) : (pair & 0xFFFFu);
-    }
-#else
 #pragma unroll
     for (int k = 0; k < BITS; ++k) m = (m << 1) | bit(probs + m);
-#endif
     return m - (1u << BITS);
   }
   // Three levels of a bit tree below node `root` (cells root, 2root + {0,1},
@@ -1021,42 +700,6 @@ struct Rc {
   template <class P>
   __device__ __forceinline__ uint32_t tree8_g(P probs) {
     return sub2(probs, sub3(probs, sub3(probs, 1)));
-  }
-  // 8-level MSB-first tree (a literal, TREE_DECODE of LzmaDec.c:174) in two
-  // memory round trips instead of eight: cells 0..15 (levels 0-3) in four
-  // 8-byte reads, then the 15 cells of the 4-level subtree under the node
-  // reached (m, 2m.., 4m.., 8m..) in one batch; each level's cell is picked
-  // from registers with selects.  probs must be 8-byte aligned.  Returns the
-  // node 0x100 | byte.
-  template <class P>
-  __device__ __forceinline__ uint32_t tree8_2rt(P probs) {
-    const uint64_t q0 = ld64(probs), q1 = ld64(probs + 4), q2 = ld64(probs + 8),
-                   q3 = ld64(probs + 12);
-    auto half = [](uint64_t q, uint32_t j) {  // cell j (0..3) of a 4-cell word
-      return uint32_t(q >> (16 * j)) & 0xFFFFu;
-    };
-    uint32_t b = bit_v(half(q0, 1), probs + 1);
-    uint32_t m = 2 + b;                                   // 2..3
-    b = bit_v(half(q0, m), probs + m);
-    m = 2 * m + b;                                        // 4..7
-    b = bit_v(half(q1, m - 4), probs + m);
-    m = 2 * m + b;                                        // 8..15
-    b = bit_v(half((m & 4) ? q3 : q2, m & 3), probs + m);
-    m = 2 * m + b;                                        // 16..31
-    const uint32_t c0 = probs[m];
-    const uint32_t c1 = *wide(probs + 2 * m);
-    const uint64_t c2 = ld64(probs + 4 * m), c3a = ld64(probs + 8 * m),
-                   c3b = ld64(probs + 8 * m + 4);
-    const uint32_t r = m;
-    b = bit_v(c0, probs + m);
-    m = 2 * m + b;                                        // 2r + j, j < 2
-    b = bit_v((c1 >> (16 * (m - 2 * r))) & 0xFFFFu, probs + m);
-    m = 2 * m + b;                                        // 4r + j, j < 4
-    b = bit_v(half(c2, m - 4 * r), probs + m);
-    m = 2 * m + b;                                        // 8r + j, j < 8
-    const uint32_t j = m - 8 * r;
-    b = bit_v(half((j & 4) ? c3b : c3a, j & 3), probs + m);
-    return 2 * m + b;
   }
   // fixed-probability bit in the reference's exact arithmetic (LzmaDec.c:325-334)
   __device__ __forceinline__ void direct(uint32_t& v) {
@@ -1173,17 +816,6 @@ __device__ __forceinline__ uint32_t lit8_coop(Rc<GlobalReaderQ>& rc, P probs) {
 // Copy n bytes of an LZ match: dic[pos..pos+n) = dic[from..], byte-serial
 // overlap semantics (rep0 < n replicates the period), ring wrap at cap.
 // Non-overlapping, non-wrapping spans go 8 bytes per round trip.
-#if LZGPU_COPY_V2
-// low min(rem, 8) bytes of v to d[0..)
-__device__ __forceinline__ void lz_store_upto8(gbyte* d, uint64_t v, uint32_t rem) {
-  if (rem >= 8) {
-#pragma unroll
-    for (int k = 0; k < 8; ++k) d[k] = uint8_t(v >> (8 * k));
-  } else {
-    for (uint32_t k = 0; k < rem; ++k) d[k] = uint8_t(v >> (8 * k));
-  }
-}
-#endif
 
 // Unaligned 8-byte global access (gfx950 runs global memory in unaligned
 // mode: one dwordx2 per 8 bytes instead of eight byte instructions -- the
@@ -1209,12 +841,21 @@ __device__ __forceinline__ uint64_t ldu64(const gbyte* p) {
 }
 __device__ __forceinline__ void stu64(gbyte* p, uint64_t v) {
   *(__attribute__((address_space(1))) lz_u64a1*)p = v;
+#if LZGPU_SHADOW_OUT
+  *(__attribute__((address_space(1))) lz_u64a1*)(p + LZGPU_SHADOW_OUT) = v;
+#endif
 }
 __device__ __forceinline__ void stu32(gbyte* p, uint32_t v) {
   *(__attribute__((address_space(1))) lz_u32a1*)p = v;
+#if LZGPU_SHADOW_OUT
+  *(__attribute__((address_space(1))) lz_u32a1*)(p + LZGPU_SHADOW_OUT) = v;
+#endif
 }
 __device__ __forceinline__ void stu16(gbyte* p, uint32_t v) {
   *(__attribute__((address_space(1))) lz_u16a1*)p = uint16_t(v);
+#if LZGPU_SHADOW_OUT
+  *(__attribute__((address_space(1))) lz_u16a1*)(p + LZGPU_SHADOW_OUT) = uint16_t(v);
+#endif
 }
 #endif
 // the low rem (1..7) bytes of v to d: at most three stores
@@ -1229,13 +870,12 @@ __device__ __forceinline__ void stu_tail(gbyte* d, uint64_t v, uint32_t rem) {
     v >>= 16;
     d += 2;
   }
-  if (rem & 1) *d = uint8_t(v);
+  if (rem & 1) lz_put(d, uint32_t(v));
 }
 
 __device__ __forceinline__ uint32_t lz_copy(gbyte* dic, uint64_t pos, uint64_t from, uint32_t n,
                                             uint32_t dist, uint64_t cap) {
   uint32_t last = 0;
-#if LZGPU_COPY_WIDE
   if (from + n <= cap && from < pos) {
     // source span does not wrap (always so for a flat LzmaDecode window)
     gbyte* d = dic + pos;
@@ -1282,70 +922,6 @@ __device__ __forceinline__ uint32_t lz_copy(gbyte* dic, uint64_t pos, uint64_t f
       v = (v >> (8 * t)) | (v << (8 * (dist - t)));
     }
   }
-#endif
-#if LZGPU_COPY_V2
-  if (from + n <= cap && from < pos) {
-    // source span [from, from+n) does not wrap; from < pos always holds here
-    // except for the ring case handled below
-    gbyte* d = dic + pos;
-    const gbyte* src = dic + from;
-    uint64_t v;
-    if (dist >= 8) {
-      // src[i..i+8) lies below d + i: written before this step reads it
-      uint32_t i = 0;
-      do {
-        v = 0;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) v |= uint64_t(src[i + k]) << (8 * k);
-        const uint32_t rem = n - i;
-        lz_store_upto8(d + i, v, rem);
-        if (rem <= 8) {
-          last = uint32_t(v >> (8 * (rem - 1))) & 0xFFu;
-          break;
-        }
-        i += 8;
-      } while (true);
-      return last;
-    }
-    // rep0 < 8: the output is src[0..dist) repeated; build 8 bytes of it
-    v = 0;
-    for (uint32_t k = 0; k < dist; ++k) v |= uint64_t(src[k]) << (8 * k);
-    v |= v << (8 * dist);
-    if (dist < 4) v |= v << (16 * dist);
-    if (dist < 2) v |= v << 32;
-    // next 8 bytes of the period: shift by t = 8 mod dist
-    const uint32_t t = 8u % dist;
-    uint32_t i = 0;
-    do {
-      const uint32_t rem = n - i;
-      lz_store_upto8(d + i, v, rem);
-      if (rem <= 8) {
-        last = uint32_t(v >> (8 * (rem - 1))) & 0xFFu;
-        break;
-      }
-      v = (v >> (8 * t)) | (v << (8 * (dist - t)));
-      i += 8;
-    } while (true);
-    return last;
-  }
-#endif
-#if LZGPU_COPY_SHORT
-  if (dist < 8 && dist < n && from + dist <= cap && from < pos) {
-    // overlapping: the output is the dist-byte period starting at `from`,
-    // repeated; load the period once, then stream it from registers
-    uint64_t per = 0;
-    for (uint32_t k = 0; k < dist; ++k) per |= uint64_t(dic[from + k]) << (8 * k);
-    gbyte* d = dic + pos;
-    uint32_t k = 0;
-    for (uint32_t i = 0; i < n; ++i) {
-      const uint32_t b = uint32_t(per >> (8 * k)) & 0xFFu;
-      d[i] = uint8_t(b);
-      last = b;
-      k = (k + 1 == dist) ? 0 : k + 1;
-    }
-    return last;
-  }
-#endif
   if (from + n <= cap) {
     gbyte* d = dic + pos;
     const gbyte* s = dic + from;
@@ -1399,47 +975,30 @@ __device__ __forceinline__ uint32_t lit_bit(Rc<Rd>& rc, const Tab<M, Lo>& T, uin
 
 // One literal (LzmaDec.c:161-196): plain tree for state < 7, matched tree
 // against the byte at rep0 otherwise; writes the byte, updates state.
-template <uint32_t M, bool St = true, class Lo, class Rd>
+template <uint32_t M, class Lo, class Rd>
 __device__ __forceinline__ void lz_literal(Rc<Rd>& rc, const Tab<M, Lo>& T, uint32_t& st,
                                            uint32_t& prev, uint32_t& total, uint32_t full,
                                            uint32_t lc, uint32_t lp_mask, gbyte* dic,
-                                           uint64_t& pos, uint64_t cap, uint32_t r0
-#if LZGPU_MB_PF
-                                           , uint32_t mb_pf
-#endif
-) {
+                                           uint64_t& pos, uint64_t cap, uint32_t r0,
+                                           uint32_t mb_pf) {
   uint32_t sym = 1;
   uint32_t ctx = 0;
   if (full != 0 || total != 0) ctx = ((total & lp_mask) << lc) + (prev >> (8 - lc));
   if (st < 7) {
     st = (st < 4) ? 0 : st - 3;
-#if LZGPU_LIT_2RT
-    sym = rc.tree8_2rt(T.template at<S_LITP>(ctx << 8));
-#elif LZGPU_READER_Q
     if constexpr (((M & kCoopBit) != 0u) && __is_same(Rd, GlobalReaderQ)) {
       sym = lit8_coop(rc, T.template at<S_LITP>(ctx << 8));
     } else {
       auto lp = T.template at<S_LITP>(ctx << 8);
-#if LZGPU_LIT_PF
-      sym = rc.lit8_pf(lp);
-#else
       const uint32_t m = rc.template tree_u<4>(lp, 1);
       rd_topup(*rc.rd);
       sym = rc.template tree_u<4>(lp, m);
-#endif
     }
-#else
-    sym = 0x100u | rc.template tree<8>(T.template at<S_LITP>(ctx << 8));
-#endif
   } else {
-#if LZGPU_MB_PF
     uint32_t mbyte = mb_pf_on<M>() ? mb_pf : uint32_t(dic[ring_back(pos, r0, cap)]);
-#else
-    uint32_t mbyte = dic[ring_back(pos, r0, cap)];
-#endif
     st = (st < 10) ? st - 3 : st - 6;
     constexpr bool p_lds = ((M >> S_LITP) & 1u) != 0u, m_lds = ((M >> S_LITM) & 1u) != 0u;
-    if constexpr (LZGPU_MLIT_PF && p_lds && !m_lds) {
+    if constexpr (p_lds && !m_lds) {
       // While the decoded bits equal the match byte's, the cell of bit k is
       // fixed by the match byte alone (offs stays 0x100, symbol = its top k
       // bits under a leading 1): load all eight matched-tree cells at once
@@ -1457,18 +1016,11 @@ __device__ __forceinline__ void lz_literal(Rc<Rd>& rc, const Tab<M, Lo>& T, uint
       for (int k = 0; k < 8; ++k) {
         const uint32_t mk = (mb >> (7 - k)) & 1u;
         uint32_t b;
-#if LZGPU_READER_Q
         if (k == 4) rd_topup(*rc.rd);
         if (matched)
           b = rc.bit_vu(pk[k], lm + ((mk << 8) + sym));
         else
           b = rc.bit_u(T.template at<S_LITP>((ctx << 8) + sym));
-#else
-        if (matched)
-          b = rc.bit_v(pk[k], lm + ((mk << 8) + sym));
-        else
-          b = rc.bit(T.template at<S_LITP>((ctx << 8) + sym));
-#endif
         matched = matched && (b == mk);
         sym = (sym << 1) | b;
       }
@@ -1485,7 +1037,7 @@ __device__ __forceinline__ void lz_literal(Rc<Rd>& rc, const Tab<M, Lo>& T, uint
     }
   }
   prev = sym & 0xFFu;
-  if constexpr (St) lz_put(dic + pos, prev);
+  lz_put(dic + pos, prev);
   pos++;
   total++;
 }
@@ -1513,55 +1065,6 @@ __device__ __forceinline__ bool lz_any(bool v) {
 #endif
 }
 
-// One literal (LzmaDec.c:161-196) with plain and matched literals on ONE
-// instruction path (LZGPU_LIT_UNIFIED; plain tree in LDS, matched cells in
-// global memory).  Lanes of a wave decode plain and matched literals side by
-// side in the same batch iteration; as two code paths the wave would run both
-// nearly every iteration.  Per level: the plain cell is read from LDS by
-// every lane; a lane still on the all-match path uses its preloaded matched
-// cell instead, writes the plain cell back unchanged and stores the update to
-// its matched cell (a predicated store, no else-path).  Once a decoded bit
-// differs from the match byte's the lane continues in the plain tree, as the
-// reference's offs = 0 does; a plain literal is that walk from the start.
-template <uint32_t M, class Lo, class Rd>
-__device__ __forceinline__ void lz_literal_unified(Rc<Rd>& rc, const Tab<M, Lo>& T, uint32_t& st,
-                                                   uint32_t& prev, uint32_t& total,
-                                                   uint32_t full, uint32_t lc, uint32_t lp_mask,
-                                                   gbyte* dic, uint64_t& pos, uint32_t mbyte) {
-  uint32_t ctx = 0;
-  if (full != 0 || total != 0) ctx = ((total & lp_mask) << lc) + (prev >> (8 - lc));
-  const bool mlit = st >= 7;
-  st = (st < 4) ? 0 : ((st < 10) ? st - 3 : st - 6);
-  const uint32_t mb = mlit ? (mbyte & 0xFFu) : 0u;
-  auto lp = T.template at<S_LITP>(ctx << 8);
-  auto lm = T.template at<S_LITM>(ctx << 9);
-  uint32_t pk[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) pk[k] = 0;
-  if (lz_any(mlit)) {
-    if (mlit) {
-#pragma unroll
-      for (int k = 0; k < 8; ++k)
-        pk[k] = lm[(((mb >> (7 - k)) & 1u) << 8) + ((1u << k) | (mb >> (8 - k)))];
-    }
-  }
-  bool matching = mlit;
-  uint32_t sym = 1;
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    const uint32_t mk = (mb >> (7 - k)) & 1u;
-    const uint32_t pl = lp[sym];
-    uint32_t np;
-    const uint32_t b = rc.bit_np(matching ? pk[k] : pl, np);
-    lp[sym] = uint16_t(matching ? pl : np);
-    if (matching) lm[(mk << 8) + sym] = uint16_t(np);
-    matching = matching && (b == mk);
-    sym = (sym << 1) | b;
-  }
-  prev = sym & 0xFFu;
-  dic[pos++] = uint8_t(prev);
-  total++;
-}
 
 // Decode symbols until pos reaches `limit` or the reader index reaches
 // `in_limit` (checked after each whole symbol; the first is always decoded).
@@ -1585,40 +1088,25 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
   // previous byte (literal context), kept in a register
   uint32_t prev = 0;
   if (full != 0 || total != 0) prev = dic[(pos == 0 ? cap : pos) - 1];
-#if LZGPU_MB_PF
   // byte at distance rep0, needed by a matched literal (state >= 7)
   uint32_t mb_pf = 0;
   if constexpr (mb_pf_on<M>()) mb_pf = (st >= 7) ? uint32_t(dic[ring_back(pos, r0, cap)]) : 0u;
-#endif
 
   uint32_t ps = 0;
 #if LZGPU_PROF && !defined(LZGPU_HOST_EMU)
   uint64_t t_prof = lz_clock();
 #endif
-  // LZGPU_TAIL_LIT: the symbol after a match was started at the end of the
-  // previous pass (its IsMatch bit said "match"): skip straight to the match
-  // path, the symbol must complete whatever the limits say now
-  bool pend_match = false;
   do {
     uint32_t lcoder_is_rep;
     // Up to LZGPU_LIT_BATCH symbols per pass of this loop while they are
     // literals: a lane's symbol sequence is unchanged, but lanes of a wave
     // that sit in literal runs keep decoding together instead of idling
     // behind a neighbour's match path on every symbol.
-    bool is_match = pend_match, stop = false;
-    pend_match = false;
-#if LZGPU_UNIFORM_EXIT
+    bool is_match = false, stop = false;
     // lanes leave the batch by clearing lit_on, the loop itself exits only
     // when the whole wave is done: no divergent exit, so no per-iteration
     // copies of the lane state into exit registers
     bool lit_on = !is_match;
-#if LZGPU_LIT_WC
-    // the batch's literals are consecutive output bytes: collected in a
-    // register and written with at most three stores after the batch
-    static_assert(LZGPU_LIT_BATCH <= 8, "literal write-combining holds 8 bytes");
-    uint64_t lit_buf = 0;
-    uint32_t lit_n = 0;
-#endif
 #pragma unroll 1
     for (int lit = 0; lit < LZGPU_LIT_BATCH; ++lit) {
 #if LZGPU_PROF && !defined(LZGPU_HOST_EMU)
@@ -1642,12 +1130,8 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
 #endif
       if (lit_on) {
         ps = total & pb_mask;
-#if LZGPU_READER_Q
         rd_topup(rd);
         const uint32_t ism = rc.bit_u(T.template at<S_MATCH>((st << pb) + ps));
-#else
-        const uint32_t ism = rc.bit(T.template at<S_MATCH>((st << pb) + ps));
-#endif
         if (ism) {
           is_match = true;
           lit_on = false;
@@ -1656,22 +1140,7 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
           tB = lz_clock();
           did_lit = true;
 #endif
-#if LZGPU_LIT_UNIFIED && LZGPU_MB_PF
-          if constexpr (((M >> S_LITP) & 1u) != 0u && ((M >> S_LITM) & 1u) == 0u)
-            lz_literal_unified<M>(rc, T, st, prev, total, full, lc, lp_mask, dic, pos,
-                                  mb_pf_on<M>() ? mb_pf : uint32_t(dic[ring_back(pos, r0, cap)]));
-          else
-#endif
-          lz_literal<M, !LZGPU_LIT_WC>(rc, T, st, prev, total, full, lc, lp_mask, dic, pos,
-                                         cap, r0
-#if LZGPU_MB_PF
-                                         , mb_pf
-#endif
-          );
-#if LZGPU_LIT_WC
-          lit_buf |= uint64_t(prev) << (8 * lit_n);
-          ++lit_n;
-#endif
+          lz_literal<M>(rc, T, st, prev, total, full, lc, lp_mask, dic, pos, cap, r0, mb_pf);
 #if LZGPU_PROF && !defined(LZGPU_HOST_EMU)
           tC = lz_clock();
 #endif
@@ -1695,51 +1164,10 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
         s.prof[17] += lz_clock() - t_it;  // the whole iteration, every live lane
         if (!more) break;
       }
-#elif LZGPU_LIT_THR
-      {
-        // leave the batch once fewer than LZGPU_LIT_THR % of the wave's live
-        // lanes are still on literals (the others wait for the match path)
-#ifdef LZGPU_HOST_EMU
-        if (!lit_on) break;
-#else
-        const uint32_t on = uint32_t(__builtin_popcountll(__builtin_amdgcn_ballot_w64(lit_on)));
-        const uint32_t live = uint32_t(__builtin_popcountll(__builtin_amdgcn_ballot_w64(true)));
-        if (on == 0 || on * 100u < live * uint32_t(LZGPU_LIT_THR)) break;
-#endif
-      }
 #else
       if (!lz_any(lit_on)) break;
 #endif
     }
-#else
-#pragma unroll 1
-    for (int lit = 0; lit < LZGPU_LIT_BATCH && !is_match; ++lit) {
-      ps = total & pb_mask;
-      rd_topup(rd);  // checkpoint: IsMatch + the literal tree's first half
-      if (rc.bit_u(T.template at<S_MATCH>((st << pb) + ps))) {
-        is_match = true;
-        break;
-      }
-      lz_literal<M>(rc, T, st, prev, total, full, lc, lp_mask, dic, pos, cap, r0
-#if LZGPU_MB_PF
-                    , mb_pf
-#endif
-      );
-      if (!(pos < limit && rd.used() < in_limit)) {
-        stop = true;
-        break;
-      }
-    }
-#endif
-#if LZGPU_UNIFORM_EXIT && LZGPU_LIT_WC
-    if (lit_n != 0) {
-      gbyte* d = dic + (pos - lit_n);
-      if (lit_n == 8)
-        stu64(d, lit_buf);
-      else
-        stu_tail(d, lit_buf, lit_n);
-    }
-#endif
     LZ_PROF_MARK(s, 0, t_prof);
 #if LZGPU_PROF >= 2 && !defined(LZGPU_HOST_EMU)
     {
@@ -1773,9 +1201,7 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
           lz_put(dic + pos++, prev);
           total++;
           st = (st < 7) ? 9 : 11;
-#if LZGPU_MB_PF
           if constexpr (mb_pf_on<M>()) mb_pf = dic[ring_back(pos, r0, cap)];
-#endif
           continue;
         }
       } else {
@@ -1809,10 +1235,10 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
       auto lbase = [&]() {
         if constexpr (len_lds) return T.lo + lsec_o; else return T.g(lsec_o);
       }();
-      if constexpr (!len_lds && LZGPU_TREE_GPF) {
+      if constexpr (!len_lds) {
         // global length coder: the choice bits and the low tree load together,
         // the mid tree only behind choice = 1
-        if constexpr (LZGPU_MATCH_FAT && (M & ~kIlvBit) != LZGPU_LDS_MASK) {
+        if constexpr ((M & ~kIlvBit) != LZGPU_LDS_MASK) {
         // choice, choice2 and both 3-level trees of this posState in ONE load
         // batch; only lengths >= 18 go back to memory (LenHigh, 3 batches)
         auto lo_t = lbase + 2 + (ps << 3);
@@ -1854,7 +1280,7 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
     if (st >= 12) {
       const uint32_t lstate = len < 4 ? len : 3;
       uint32_t dist;
-      if constexpr (((M >> S_SLOT) & 1u) == 0u && LZGPU_TREE_GPF) {
+      if constexpr (((M >> S_SLOT) & 1u) == 0u) {
         auto sl_t = T.template at<S_SLOT>(lstate << 6);
 #if LZGPU_PROF == 1 && !defined(LZGPU_HOST_EMU)
         // one global round trip + 3 decisions, timed (profiling builds)
@@ -1879,7 +1305,7 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
           dist <<= nbits;
           uint32_t mask = 1, node = 1;
           const uint32_t sp = dist - slot - 1;
-          if constexpr (((M >> S_SPEC) & 1u) == 0u && LZGPU_TREE_GPF) {
+          if constexpr (((M >> S_SPEC) & 1u) == 0u) {
             if (nbits >= 3) {
               // first three reverse-tree bits in one load batch
               node = rc.sub3(T.template at<S_SPEC>(sp), 1);
@@ -1887,7 +1313,7 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
               mask = 8;
               nbits -= 3;
             }
-            if constexpr (LZGPU_MATCH_FAT && (M & ~kIlvBit) != LZGPU_LDS_MASK) if (nbits == 2) {
+            if constexpr ((M & ~kIlvBit) != LZGPU_LDS_MASK) if (nbits == 2) {
               // the last two bits in one batch as well
               const uint32_t n2 = rc.sub2(T.template at<S_SPEC>(sp), node);
               dist |= (((n2 >> 1) & 1u) ? mask : 0u) | ((n2 & 1u) ? (mask << 1) : 0u);
@@ -1906,8 +1332,8 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
           do rc.direct(dist); while (--nbits != 0);
           dist <<= 4;
           uint32_t node = 1;
-          if constexpr (((M >> S_ALIGN) & 1u) == 0u && LZGPU_TREE_GPF) {
-            if constexpr (LZGPU_MATCH_FAT && (M & ~kIlvBit) != LZGPU_LDS_MASK) {
+          if constexpr (((M >> S_ALIGN) & 1u) == 0u) {
+            if constexpr ((M & ~kIlvBit) != LZGPU_LDS_MASK) {
               // all four reverse bits from one batch of the 15 cells
               node = rc.sub4(T.template at<S_ALIGN>(0), 1);
               dist |= ((node >> 3) & 1u) | (((node >> 2) & 1u) << 1) |
@@ -1959,32 +1385,10 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
       len -= n;
       prev = lz_copy(dic, pos, from, n, r0, cap);
       pos += n;
-#if LZGPU_MB_PF
       if constexpr (mb_pf_on<M>()) mb_pf = dic[ring_back(pos, r0, cap)];
-#endif
     }
     LZ_PROF_MARK(s, 2, t_prof);
-#if LZGPU_TAIL_LIT
-    // The symbol after a match, decoded here while only the lanes that
-    // matched are active: if it is a literal it is a matched one (state >= 7),
-    // which would otherwise diverge from the plain literals of the batch.
-    if (pos < limit && rd.used() < in_limit) {
-      ps = total & pb_mask;
-      rd_topup(rd);  // checkpoint: IsMatch + the literal tree's first half
-      if (rc.bit_u(T.template at<S_MATCH>((st << pb) + ps))) {
-        pend_match = true;
-      } else {
-        lz_literal<M>(rc, T, st, prev, total, full, lc, lp_mask, dic, pos, cap, r0
-#if LZGPU_MB_PF
-                      , mb_pf
-#endif
-        );
-      }
-    }
-  } while ((pos < limit && rd.used() < in_limit) || pend_match);
-#else
   } while (pos < limit && rd.used() < in_limit);
-#endif
 
   rc.norm();
   s.range = rc.range;
@@ -2222,12 +1626,7 @@ __device__ __forceinline__ void lz_init_state_real(LzStateT<Lo>& s) {
     if constexpr ((M & kIlvBit) != 0u) {
       // the lane's column: one cell per row (the lanes of a group that start
       // together store whole 64-byte rows)
-#if LZGPU_ILV_PAIR
-      for (uint32_t i = 0; i < L.glb_cells; i += 2)
-        *(gu32*)(s.gl + ilv_cell(i)) = kProbInit | (kProbInit << 16);
-#else
       for (uint32_t i = 0; i < L.glb_cells; ++i) s.gl[kIlv * i] = uint16_t(kProbInit);
-#endif
     } else {
       fill_prob_init(s.gl, L.glb_cells);
     }
@@ -2306,7 +1705,7 @@ __device__ __forceinline__ int lz_decode_to_dic(LzStateT<Lo>& s, uint64_t dic_li
       }
       typename BulkReaderFor<M>::type rd;
       rd.init(src, avail);
-#if LZGPU_PROF && !defined(LZGPU_HOST_EMU) && LZGPU_READER16
+#if LZGPU_PROF && !defined(LZGPU_HOST_EMU)
       const int rr = lz_run_split<M>(s, dic_limit, rd, in_limit);
       s.prof[4] += rd.prof;
       if (rr != kOk) return kErrData;
