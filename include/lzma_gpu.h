@@ -156,6 +156,13 @@ SRes LzmaDecode(Byte *dest, SizeT *destLen, const Byte *src, SizeT *srcLen,
  * or probs), so the next call starts from the host copy.  Mirrors beyond
  * 256 decoders or 16 GiB are evicted least recently used first. */
 void LzmaGpu_DecoderRelease(const CLzmaDec *p);
+/* Host<->device bytes moved by the drop-in decode entry points (LzmaDecode,
+ * LzmaUncompress, Lzma2Decode, LzmaDec_DecodeToDic / DecodeToBuf and the LZMA2
+ * streaming calls built on them) since start or the last reset, and the number
+ * of decode calls that reached the device; reset != 0 zeroes them.  Any
+ * argument may be NULL.  Process-wide. */
+void LzmaGpu_DropinTransferStats(uint64_t *h2d_bytes, uint64_t *d2h_bytes, uint64_t *calls,
+                                 int reset);
 
 /* ---------------------------------------------------------------- drop-in LzmaLib.h */
 

@@ -31,6 +31,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstddef>
 #include <cstdio>
 #include <cstdlib>
@@ -53,6 +54,17 @@ using lzgpu_host::set_error;
 namespace {
 
 uint32_t probs_for(uint32_t lc, uint32_t lp) { return lzgpu::num_probs(lc, lp); }
+
+// PCIe bytes moved by the drop-in entry points (LzmaGpu_DropinTransferStats):
+// the evidence that the dictionary interface uploads its input, not its
+// dictionary, per call
+std::atomic<uint64_t> g_h2d{0}, g_d2h{0}, g_calls{0};
+
+hipError_t xfer(void* dst, const void* src, size_t n, hipMemcpyKind kind, hipStream_t st) {
+  if (kind == hipMemcpyHostToDevice) g_h2d += n;
+  if (kind == hipMemcpyDeviceToHost) g_d2h += n;
+  return hipMemcpyAsync(dst, src, n, kind, st);
+}
 
 // RAII borrow of a pooled call scratch (buffers + its own stream)
 struct ScratchLease {
@@ -78,6 +90,7 @@ SRes gpu_one_call(uint8_t kind, Byte* dest, SizeT* destLen, const Byte* src, Siz
   *srcLen = 0;
   *destLen = 0;
   if (!ensure_device()) return SZ_ERROR_FAIL;
+  ++g_calls;
   struct Meta {  // one upload: the descriptor and its lane order
     LzmaGpuStreamDesc d;
     uint32_t order;
@@ -111,16 +124,16 @@ SRes gpu_one_call(uint8_t kind, Byte* dest, SizeT* destLen, const Byte* src, Siz
   }
   const hipStream_t st = S.stream;
   LzmaGpuResult r;
-  if (in_size && !hip_ok(hipMemcpyAsync(d_io, src, in_size, hipMemcpyHostToDevice, st), "upload src"))
+  if (in_size && !hip_ok(xfer(d_io, src, in_size, hipMemcpyHostToDevice, st), "upload src"))
     return SZ_ERROR_FAIL;
-  if (!hip_ok(hipMemcpyAsync(d_meta, &m, sizeof m, hipMemcpyHostToDevice, st), "upload desc"))
+  if (!hip_ok(xfer(d_meta, &m, sizeof m, hipMemcpyHostToDevice, st), "upload desc"))
     return SZ_ERROR_FAIL;
   LzmaGpuResult* d_res = reinterpret_cast<LzmaGpuResult*>(d_meta + sizeof(Meta));
   if (LzmaGpu_DecodeBatchEx(&plan, reinterpret_cast<LzmaGpuStreamDesc*>(d_meta),
                             reinterpret_cast<uint32_t*>(d_meta + offsetof(Meta, order)), d_io,
                             d_io + in_pad, d_ws, d_res, st) != SZ_OK)
     return SZ_ERROR_FAIL;
-  if (!hip_ok(hipMemcpyAsync(&r, d_res, sizeof r, hipMemcpyDeviceToHost, st), "download result") ||
+  if (!hip_ok(xfer(&r, d_res, sizeof r, hipMemcpyDeviceToHost, st), "download result") ||
       !hip_ok(hipStreamSynchronize(st), "decode kernel"))
     return SZ_ERROR_FAIL;
   if (r.dest_len > out_size) {
@@ -128,7 +141,7 @@ SRes gpu_one_call(uint8_t kind, Byte* dest, SizeT* destLen, const Byte* src, Siz
     return SZ_ERROR_FAIL;
   }
   if (r.dest_len &&
-      (!hip_ok(hipMemcpyAsync(dest, d_io + in_pad, r.dest_len, hipMemcpyDeviceToHost, st),
+      (!hip_ok(xfer(dest, d_io + in_pad, r.dest_len, hipMemcpyDeviceToHost, st),
                "download output") ||
        !hip_ok(hipStreamSynchronize(st), "download output")))
     return SZ_ERROR_FAIL;
@@ -248,7 +261,7 @@ bool mirror_host_wrote(const CLzmaDec* p, SizeT off, SizeT n) {
   ScratchLease L;
   uint8_t* d_dic = static_cast<uint8_t*>(m->block.p) + kSessBytes + probs_area(m->num_probs);
   if (!L.s ||
-      !hip_ok(hipMemcpyAsync(d_dic + off, p->dic + off, n, hipMemcpyHostToDevice, L.s->stream),
+      !hip_ok(xfer(d_dic + off, p->dic + off, n, hipMemcpyHostToDevice, L.s->stream),
               "dictionary write-through") ||
       !hip_ok(hipStreamSynchronize(L.s->stream), "dictionary write-through")) {
     m->history = false;
@@ -264,6 +277,7 @@ SRes gpu_session_call(CLzmaDec* p, int mode, SizeT dicLimit, const Byte* src, Si
                       ELzmaStatus* status) {
   int dev = 0;
   if (!hip_ok(hipGetDevice(&dev), "current device")) return SZ_ERROR_FAIL;
+  ++g_calls;
   const uint32_t cells = lzgpu::table_cells(p->prop.lc, p->prop.lp, p->prop.pb);
   if (p->probs == nullptr || cells > p->numProbs) {
     set_error("LzmaDec: probabilities not allocated for the current props");
@@ -304,16 +318,16 @@ SRes gpu_session_call(CLzmaDec* p, int mode, SizeT dicLimit, const Byte* src, Si
   };
   // the table: the device copy is current after every successful call
   if (!m->probs_dev &&
-      hipMemcpyAsync(d_probs, p->probs, size_t(cells) * 2, hipMemcpyHostToDevice, st) != hipSuccess)
+      xfer(d_probs, p->probs, size_t(cells) * 2, hipMemcpyHostToDevice, st) != hipSuccess)
     return fail("LzmaDec: upload probs");
   // history: only a decoder continuing a dictionary reads bytes it did not
   // write in this call (LzmaDec.c:165-166,176,216,376-408 read dic only when
   // processedPos or checkDicSize is non-zero); uploaded once per mirror
   const bool need_hist = p->processedPos != 0 || p->checkDicSize != 0;
   if (need_hist && !m->history && p->dicBufSize &&
-      hipMemcpyAsync(d_dic, p->dic, p->dicBufSize, hipMemcpyHostToDevice, st) != hipSuccess)
+      xfer(d_dic, p->dic, p->dicBufSize, hipMemcpyHostToDevice, st) != hipSuccess)
     return fail("LzmaDec: upload dictionary");
-  if (in_size && hipMemcpyAsync(d_io, src, in_size, hipMemcpyHostToDevice, st) != hipSuccess)
+  if (in_size && xfer(d_io, src, in_size, hipMemcpyHostToDevice, st) != hipSuccess)
     return fail("LzmaDec: upload src");
 
   LzgpuSession q;
@@ -345,7 +359,7 @@ SRes gpu_session_call(CLzmaDec* p, int mode, SizeT dicLimit, const Byte* src, Si
   q.out = d_io + in_pad;
   q.out_len = out_room;
   const SizeT pos0 = p->dicPos;
-  if (hipMemcpyAsync(d_sess, &q, sizeof q, hipMemcpyHostToDevice, st) != hipSuccess)
+  if (xfer(d_sess, &q, sizeof q, hipMemcpyHostToDevice, st) != hipSuccess)
     return fail("LzmaDec: upload session");
   const int lr = cells <= kSessCoopMaxCells ? lzgpu_launch_session_coop(d_sess, 1, cells, 1, st)
                                             : lzgpu_launch_session(d_sess, 1, st);
@@ -360,7 +374,7 @@ SRes gpu_session_call(CLzmaDec* p, int mode, SizeT dicLimit, const Byte* src, Si
     set_error("LzmaDec: host allocation failed");
     return SZ_ERROR_MEM;
   }
-  if (hipMemcpyAsync(back.data(), blk, back.size(), hipMemcpyDeviceToHost, st) != hipSuccess ||
+  if (xfer(back.data(), blk, back.size(), hipMemcpyDeviceToHost, st) != hipSuccess ||
       hipStreamSynchronize(st) != hipSuccess)
     return fail("LzmaDec: session kernel");
   memcpy(&q, back.data(), sizeof q);
@@ -368,14 +382,14 @@ SRes gpu_session_call(CLzmaDec* p, int mode, SizeT dicLimit, const Byte* src, Si
   if (mode == 0) {
     if (q.dic_pos < pos0 || q.dic_pos > p->dicBufSize) return fail("LzmaDec: bad session state");
     if (q.dic_pos > pos0 &&
-        (hipMemcpyAsync(p->dic + pos0, d_dic + pos0, q.dic_pos - pos0, hipMemcpyDeviceToHost, st) !=
+        (xfer(p->dic + pos0, d_dic + pos0, q.dic_pos - pos0, hipMemcpyDeviceToHost, st) !=
              hipSuccess ||
          hipStreamSynchronize(st) != hipSuccess))
       return fail("LzmaDec: download dictionary");
   } else {
     if (q.out_len > out_room || q.dic_pos > p->dicBufSize) return fail("LzmaDec: bad session state");
     if (q.out_len &&
-        (hipMemcpyAsync(dest, d_io + in_pad, q.out_len, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        (xfer(dest, d_io + in_pad, q.out_len, hipMemcpyDeviceToHost, st) != hipSuccess ||
          hipStreamSynchronize(st) != hipSuccess))
       return fail("LzmaDec: download output");
     // the host ring gets the same bytes the device ring got (LzmaDec.c:849-866:
@@ -507,6 +521,13 @@ void LzmaDec_Init(CLzmaDec* p) {
 }
 
 void LzmaGpu_DecoderRelease(const CLzmaDec* p) { mirror_drop(p); }
+
+void LzmaGpu_DropinTransferStats(uint64_t* h2d_bytes, uint64_t* d2h_bytes, uint64_t* calls,
+                                 int reset) {
+  if (h2d_bytes) *h2d_bytes = reset ? g_h2d.exchange(0) : g_h2d.load();
+  if (d2h_bytes) *d2h_bytes = reset ? g_d2h.exchange(0) : g_d2h.load();
+  if (calls) *calls = reset ? g_calls.exchange(0) : g_calls.load();
+}
 
 // ------------------------------------------------------------------ decode entry points
 

@@ -188,6 +188,7 @@ _sig = {
     "LzmaDec_DecodeToDic": (ctypes.c_int, [ctypes.POINTER(CLzmaDec), ctypes.c_size_t, _P, _sp, ctypes.c_int, _ip]),
     "LzmaDec_DecodeToBuf": (ctypes.c_int, [ctypes.POINTER(CLzmaDec), _P, _sp, _P, _sp, ctypes.c_int, _ip]),
     "LzmaGpu_DecoderRelease": (None, [ctypes.POINTER(CLzmaDec)]),
+    "LzmaGpu_DropinTransferStats": (None, [ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]),
     "LzmaDecode": (ctypes.c_int, [_P, _sp, _P, _sp, ctypes.c_char_p, ctypes.c_uint, ctypes.c_int, _ip, ctypes.POINTER(ISzAlloc)]),
     "LzmaUncompress": (ctypes.c_int, [_P, _sp, _P, _sp, ctypes.c_char_p, ctypes.c_size_t]),
     "Lzma2Dec_AllocateProbs": (ctypes.c_int, [ctypes.POINTER(CLzma2Dec), ctypes.c_ubyte, ctypes.POINTER(ISzAlloc)]),
@@ -265,6 +266,15 @@ def _py_free(_p, a):
 
 
 g_alloc = ISzAlloc(_py_alloc, _py_free)
+
+
+def transfer_stats(reset=False):
+    """(h2d_bytes, d2h_bytes, calls) of the drop-in entry points
+    (LzmaGpu_DropinTransferStats); reset zeroes the counters after reading."""
+    h, d, c = ctypes.c_uint64(0), ctypes.c_uint64(0), ctypes.c_uint64(0)
+    _lib.LzmaGpu_DropinTransferStats(ctypes.byref(h), ctypes.byref(d), ctypes.byref(c),
+                                     1 if reset else 0)
+    return h.value, d.value, c.value
 
 
 def last_error():
@@ -354,14 +364,15 @@ def stream_decode(src, props, out_total, in_chunk, out_chunk, finish, max_calls=
     return len(trace), trace, out.raw[:out_pos], in_pos
 
 
-def dic_decode(src, props, out_total, win, max_calls=100000, out=None):
+def dic_decode(src, props, out_total, win, max_calls=100000, out=None, between=None):
     """The 7zDec.c:127-171 (SzDecodeLzma) loop over LzmaDec_DecodeToDic:
     LzmaDec_AllocateProbs, dic = the whole output buffer (dicBufSize =
     out_total), LzmaDec_Init, then DecodeToDic(out_total, FINISH_END) over look
     windows of at most `win` input bytes -- the same contract as the oracle's
     orc_lzma_dic_decode.  `out` (optional): a ctypes buffer of >= out_total bytes
-    to decode into.  Returns (calls, trace[(res, status, srcLen, dicPos)],
-    out bytes, in_used)."""
+    to decode into.  `between` (optional): called with (call index, the
+    CLzmaDec) after every call.  Returns (calls, trace[(res, status, srcLen,
+    dicPos)], out bytes, in_used)."""
     dec = CLzmaDec()
     dec.dic = None
     dec.probs = None
@@ -390,6 +401,8 @@ def dic_decode(src, props, out_total, win, max_calls=100000, out=None):
                 break
             if dec.dicPos == out_total or (sl.value == 0 and dec.dicPos == pos0):
                 break
+            if between is not None:
+                between(len(trace) - 1, dec)
     finally:
         _lib.LzmaDec_FreeProbs(ctypes.byref(dec), ctypes.byref(g_alloc))
     return len(trace), trace, out.raw[:dec.dicPos], in_pos

@@ -8,7 +8,7 @@ shift
 mkdir -p "$OUT"
 for spec in "$@"; do
   cfg=${spec%%:*}; rest=${spec#*:}; streams=${rest%%:*}; v=${rest#*:}
-  tag=$(echo "${cfg}_${streams}_${v}" | tr ' =' '_-')
+  tag=$(echo "${cfg}_${streams}_${v}" | sed 's#[^ =]*/##g' | tr ' =' '_-')
   sarg=""; [ -n "$streams" ] && sarg="--streams $streams"
   env $v timeout -k 10 300 python -u bench.py --config $cfg $sarg --steps 5 --warmup 1 \
     --no-secondary --no-e2e --no-crc --no-cpu-baseline > "$OUT/$tag.json" 2> "$OUT/$tag.err"
