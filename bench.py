@@ -466,11 +466,29 @@ def run_cfg1(args):
                                          "compressed_bytes": len(comp),
                                          "note": "device dictionary mirror: each call uploads "
                                                  "its input window + the 192-byte state"}
+    # the 7zDec pattern over a dictionary far larger than the stream: a 64 MiB
+    # dic (a whole folder's output buffer) decoded through 16 KiB windows --
+    # round 2 uploaded dicBufSize on every call (quadratic); the mirror uploads
+    # the windows.  Per-call parity against the oracle's identical loop.
+    import native
+    big = 64 << 20
+    L.transfer_stats(reset=True)
+    t0 = time.perf_counter()
+    calls, trace, out, used = L.dic_decode(comp, props, big, 1 << 14)
+    dt = time.perf_counter() - t0
+    h2d, d2h, _ = L.transfer_stats(reset=True)
+    w = native.dic_decode(native.oracle(), "orc", comp, props, big, 1 << 14)
+    ok = ok and [tuple(t) for t in trace] == [tuple(t) for t in w[1]] and out == w[2] \
+        and sha(out) == want_sha
+    dropin["DecodeToDic_16K_windows_64MiB_dic"] = {
+        "MBps": round(len(out) / dt / 1e6, 3), "calls": calls, "h2d_bytes": h2d,
+        "d2h_bytes": d2h, "round2_h2d_bytes_would_be": calls * big,
+        "note": "dicBufSize 64 MiB, the 1 MiB stream decoded into its start; trace equal "
+                "to the oracle's loop"}
     ok = D.all_true(ok, dev)
 
     cpu = None
     if rank == 0 and not args.no_cpu_baseline:
-        import native
         if native.have_ref():
             lib, pre, kind = native.ref(), "ref", "reference"
         else:

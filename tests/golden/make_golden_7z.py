@@ -95,6 +95,12 @@ def archives():
     A.append(("256 small files in one LZMA folder", W.archive(
         [W.Folder([(f"s/{i}", native.gen("text", 720 + i, 50 + 37 * i)) for i in range(256)])])))
 
+    # unnamed stream files (no kName): the reader takes their count and sizes
+    # from the substreams alone (7zIn.c:986-1104), however many there are
+    A.append(("3000 unnamed files in one LZMA folder (no kName property)", W.archive(
+        [W.Folder([("", native.gen("text", 760 + (i % 7), 1 + (i * 13) % 97)) for i in range(3000)])],
+        names=False)))
+
     from make_golden_bra import branchy
     ad = branchy("ARM", 730, 70001)
     A.append(("ARM + LZMA, folder CRC", W.archive(

@@ -203,9 +203,11 @@ def streams_info(folders, pack_pos, substreams=True):
     return out + bytes([END])
 
 
-def header(folders, empty=(), pack_pos=0):
+def header(folders, empty=(), pack_pos=0, names=True):
     """The plain header; `empty` lists (name, is_dir) entries without data,
-    written after the folders' files."""
+    written after the folders' files; names=False leaves out the kName
+    property (files known only by their substream sizes)."""
+    want_names = names
     names = [n for f in folders for n, _ in f.files] + [n for n, _ in empty]
     nfiles = len(names)
     out = bytes([HEADER, MAIN_STREAMS]) + streams_info(folders, pack_pos)
@@ -216,16 +218,17 @@ def header(folders, empty=(), pack_pos=0):
         out += bytes([EMPTY_STREAM]) + number(len(v)) + v
         v = bools([not d for _, d in empty])
         out += bytes([EMPTY_FILE]) + number(len(v)) + v
-    nb = b"".join(n.encode("utf-16-le") + b"\0\0" for n in names)
-    out += bytes([NAME]) + number(len(nb) + 1) + b"\0" + nb
+    if want_names:
+        nb = b"".join(n.encode("utf-16-le") + b"\0\0" for n in names)
+        out += bytes([NAME]) + number(len(nb) + 1) + b"\0" + nb
     return out + bytes([END, END])
 
 
-def archive(folders, empty=(), encode_header=False, header_method=M_LZMA):
+def archive(folders, empty=(), encode_header=False, header_method=M_LZMA, names=True):
     """A whole .7z archive: signature header, the folders' packed streams,
     the (optionally LZMA-encoded) header."""
     body = b"".join(f.packed for f in folders)
-    hdr = header(folders, empty)
+    hdr = header(folders, empty, names=names)
     if encode_header:
         hf = Folder([("", hdr)], method=header_method, crc=True)
         pos = len(body)

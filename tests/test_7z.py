@@ -95,6 +95,12 @@ def test_open_structure(L):
     c = notes["unsupported coder (PPMd id)"]
     r, folders, files, _, _ = L.sz_open(arc_of(d, c))
     assert r == 0 and [f.supported for f in folders] == [4, 0]
+    # no kName: 3000 files from the substream sizes alone (the
+    # file-count bound counts substreams, 7zIn.c:986-1104 accepts this)
+    c = notes["3000 unnamed files in one LZMA folder (no kName property)"]
+    r, folders, files, names, _ = L.sz_open(arc_of(d, c))
+    assert r == 0 and len(folders) == 1 and len(files) == 3000 and folders[0].num_files == 3000
+    assert c["names_len"] == len(names)
 
 
 def test_open_rejects_malformed(L):
