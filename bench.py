@@ -893,6 +893,15 @@ def run_cfg5(args):
                                  d_chunks.data_ptr(), d_crc.data_ptr(), sh) == 0
     got = np.frombuffer(d_crc.cpu().numpy().tobytes(), dtype="<u4")
     ok = D.all_true(ok and bool(np.array_equal(got, crcs)), dev)
+    sliced = None
+    if args.sliced:
+        def check(rr):
+            return bool((rr["res"] == 0).all() and (rr["status"] == want_status[0]).all() and
+                        (rr["dest_len"] == nout).all() and
+                        (rr["src_len"][fin == 1] == lens[fin == 1]).all())
+        sliced = measure_sliced(L, torch, descs, count, d_src, d_dst, dev, args.sliced,
+                                min(args.steps, 3), dec_ms, check)
+        ok = D.all_true(ok and sliced["verified"], dev)
     value = world * total_out * args.steps / elapsed / 1e6
     alg = int(lens.sum()) + 5 * count + total_out
     achieved = alg / (dec_ms * 1e-3) / 1e9
@@ -925,7 +934,7 @@ def run_cfg5(args):
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
                          "traffic": None, "kernel": plan_kernels(plan),
                          "kernel_avg_ms": round(dec_ms, 4), "alg_bytes_per_launch": alg},
-            "cpu_baseline": cpu, "verified": ok}), flush=True)
+            "sliced": sliced, "cpu_baseline": cpu, "verified": ok}), flush=True)
     if world > 1:
         dist.destroy_process_group()
     if not ok:
@@ -1473,6 +1482,64 @@ def measure_e2e_pipelined(L, torch, plan, d_desc, d_order, d_ws, d_res, comp, pl
                     "(H2D + D2H) hide under the next batch's decode"}
 
 
+def measure_sliced(L, torch, descs, count, d_src, d_dst, dev, slice_bytes, steps, one_shot_ms,
+                   check):
+    """The same batch decoded time-sliced (LzmaGpu_DecodeBatchSliced): rounds of
+    at most slice_bytes per stream, the decoder state spilled between rounds.
+    Every step starts from a poisoned output and results array; its results
+    must pass check(results) and its output equal the one-shot decode's
+    (d_dst as the caller's verified timed steps left it, compared on the GPU)."""
+    import ctypes
+    sd = (L.StreamDesc * count)()
+    ctypes.memmove(sd, descs, ctypes.sizeof(sd))
+    plan, order = L.plan_sliced(sd, slice_bytes)
+    ref = d_dst.clone()
+    d_desc = torch.frombuffer(bytearray(bytes(sd)), dtype=torch.uint8).to(dev)
+    d_order = torch.frombuffer(bytearray(bytes(order)[:4 * count]), dtype=torch.uint8).to(dev)
+    d_ws = torch.empty(int(plan.workspace_bytes), dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    sh = stream.cuda_stream
+
+    def run(res):
+        r = L.decode_batch_sliced_device(plan, d_desc.data_ptr(), d_order.data_ptr(),
+                                         d_src.data_ptr(), d_dst.data_ptr(), d_ws.data_ptr(),
+                                         res.data_ptr(), 0, 0, sh)
+        if r != 0:
+            raise RuntimeError("LzmaGpu_DecodeBatchSliced failed: " + L.last_error())
+
+    warm = torch.empty(count * 24, dtype=torch.uint8, device=dev)
+    run(warm)
+    torch.cuda.synchronize()
+    ms, ok = [], True
+    for _ in range(steps):
+        d_dst.fill_(0xA5)
+        res = torch.full((count * 24,), 0xFF, dtype=torch.uint8, device=dev)
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        a.record(stream)
+        run(res)
+        b.record(stream)
+        torch.cuda.synchronize()
+        ms.append(a.elapsed_time(b))
+        ok = ok and check(np.frombuffer(res.cpu().numpy().tobytes(), dtype=RES_DT))
+        ok = ok and bool(torch.equal(d_dst, ref))
+    del ref
+    avg = float(np.mean(ms))
+    left = L.sliced_active(plan, d_ws.data_ptr(), plan.rounds, sh)
+    kern = {1: "lzgpu_sliced_lane_kernel", 2: "lzgpu_sliced_coop_kernel",
+            3: "lzgpu_sliced_global_kernel"}[plan.kernel]
+    out_bytes = int(np.frombuffer(bytes(sd), dtype=np.uint8).reshape(count, 48)[:, 24:32]
+                    .copy().view(np.uint64).sum())
+    return {"slice_bytes": slice_bytes, "rounds": int(plan.rounds), "kernel": kern,
+            "placement": hex(plan.lds_mask), "groups_per_cu": int(plan.groups_per_cu),
+            "streams_in_place": int(plan.n_inplace), "ms": round(avg, 3),
+            "MBps": round(out_bytes / (avg * 1e-3) / 1e6, 2),
+            "vs_one_shot": round(one_shot_ms / avg, 3), "unfinished_after_last_round": int(left),
+            "workspace_bytes": int(plan.workspace_bytes), "verified": ok and left == 0,
+            "note": "the same streams in rounds of at most slice_bytes per stream, decoder "
+                    "state spilled to device memory between rounds; no host round trip"}
+
+
 def run_secondary(cfgs, steps=5, warmup=1, timeout=420):
     """The other BASELINE configs, each a short run of this script in a child
     process (started, not exec'd: this process has touched the GPU), so the
@@ -1482,6 +1549,8 @@ def run_secondary(cfgs, steps=5, warmup=1, timeout=420):
         cmd = [sys.executable, os.path.abspath(__file__), "--config", c, "--steps", str(steps),
                "--warmup", str(warmup), "--no-cpu-baseline", "--no-e2e", "--no-crc",
                "--no-secondary"]
+        if c == "cfg2":
+            cmd += ["--sliced", "16384"]  # the time-sliced form of the same batch beside it
         t0 = time.perf_counter()
         try:
             r = subprocess.run(cmd, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
@@ -1498,6 +1567,7 @@ def run_secondary(cfgs, steps=5, warmup=1, timeout=420):
                   (cfg_d.get("kernel_ms") or {}).get("lzma2_batch"),
                   "workload": cfg_d.get("workload"), "kernel_plan": cfg_d.get("kernel_plan"),
                   "verified": bool(d.get("verified")) and (r is not None and r.returncode == 0),
+                  "sliced": d.get("sliced"),
                   "wall_s": round(time.perf_counter() - t0, 1)}
         log(f"[secondary] {c}: {out[c]['value']} MB/s verified={out[c]['verified']}")
     return out
@@ -1565,6 +1635,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-crc", action="store_true", help="skip the CRC-32 (8(f) row 1) leg")
     ap.add_argument("--no-e2e", action="store_true", help="skip the H2D + decode + D2H leg")
+    ap.add_argument("--sliced", type=int, default=0,
+                    help="cfg2 / cfg3 / cfg5: also time the batch as a time-sliced decode "
+                         "(LzmaGpu_DecodeBatchSliced) with this many output bytes per stream "
+                         "and round (SURVEY 8(f) row 2)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launcher, sharding and reductions on CPU (gloo), no decode")
     ap.add_argument("--no-secondary", action="store_true",
@@ -1687,6 +1761,15 @@ def main():
                                                  comp, plain, count, n, dev, 12)
         ok = D.all_true(ok and e2e["pipelined"]["verified"], dev)
 
+    sliced = None
+    if args.sliced:
+        def check(rr):
+            return bool((rr["res"] == 0).all() and (rr["status"] == 1).all() and
+                        (rr["dest_len"] == n).all() and (rr["src_len"] == lens).all())
+        sliced = measure_sliced(L, torch, descs, count, d_src, d_dst, dev, args.sliced,
+                                min(args.steps, 5), float(np.mean(kern_ms)), check)
+        ok = D.all_true(ok and sliced["verified"], dev)
+
     total_streams = int(D.reduce_sum(float(count), dev))
     total_bytes = total_streams * n * args.steps
     value = total_bytes / elapsed / 1e6
@@ -1769,6 +1852,7 @@ def main():
                                 "decisions per stream: the kernel is bound by issue latency "
                                 "(waves parked on s_waitcnt), not by HBM bytes"},
             "e2e": e2e,
+            "sliced": sliced,
             "cpu_baseline": cpu_base,
             "crc32": crc,
             "secondary": secondary,

@@ -426,6 +426,68 @@ SRes LzmaGpu_SessionInit(LzmaGpuSession *s, const Byte *props, unsigned propsSiz
  * written back into each d_sessions[i].  Asynchronous on `stream`. */
 SRes LzmaGpu_SessionDecodeBatch(LzmaGpuSession *d_sessions, size_t n, void *stream);
 
+/* ---------------------------------------------------------------- time-sliced batches */
+
+/* A batch of LZMA streams decoded in rounds.  Each round is one launch in
+ * which every unfinished stream makes one LzmaDec_DecodeToDic call
+ * (LzmaDec.c:719-838) on its device-resident decoder (an LzmaGpuSession in the
+ * workspace) with dicLimit = dicPos + slice_bytes and LZMA_FINISH_ANY -- the
+ * call that reaches dst_cap takes the stream's own finish mode -- and its
+ * state is spilled back for the next round (the CLzmaDec checkpoint,
+ * LzmaDec.h:50-69).  Streams that finish drop out; the next round deals the
+ * unfinished ones over every CU again.  Results (output bytes and
+ * LzmaGpuResult) equal LzmaGpu_DecodeBatchEx's, i.e. LzmaDecode's per stream.
+ * A round's launch is bounded by slice_bytes of output per stream, so work of
+ * other streams or tenants queued on the device waits at most one round
+ * behind a long stream, and a caller can stop after any round and resume.
+ * LZMA items only (an LZMA2 item: SZ_ERROR_PARAM at plan time). */
+#define LZMA_GPU_SLICED_AUTO 0u
+#define LZMA_GPU_SLICED_LANE 1u   /* one stream per wave, its table staged in LDS per round */
+#define LZMA_GPU_SLICED_COOP 2u   /* one stream per 32-lane wave (literal trees by lane speculation) */
+#define LZMA_GPU_SLICED_GLOBAL 3u /* one stream per lane, table in the workspace (any lc/lp) */
+typedef struct LzmaGpuSlicedPlan {
+  uint64_t workspace_bytes;
+  uint64_t n;
+  uint64_t slice_bytes;
+  uint32_t rounds;          /* launches that take every stream to its end: ceil(max dst_cap / slice) */
+  uint32_t kernel;          /* LZMA_GPU_SLICED_* that runs */
+  uint32_t table_cells;     /* LDS cells staged per stream (the widest, <= 32768) */
+  uint32_t groups_per_cu;   /* resident workgroups per CU (persistent grid) */
+  uint32_t max_groups;      /* grid of every round launch */
+  uint32_t lds_mask;        /* LANE: sections staged in LDS (0x7FF all; 0x200001BF the
+                               latency kernel's, the others used in place) */
+  uint64_t sess_off, list_off, ctr_off; /* workspace sections (bytes) */
+  uint64_t n_inplace;       /* streams whose table is wider than the staged slot: decoded
+                               in place by the global kernel each round */
+} LzmaGpuSlicedPlan;
+/* Plan a sliced batch: fills descs[i].probs_off (the stream's table, in cells
+ * into the workspace, 16-byte aligned), order (if not NULL: longest work
+ * first, uploaded by the caller as DecodeBatchSliced's d_order) and *plan.
+ * kernel = LZMA_GPU_SLICED_*; AUTO picks COOP for at most 8 streams per CU,
+ * else LANE, and GLOBAL when no table fits LDS; streams whose table does not
+ * fit the LDS kernel's slot (over 64 KiB) run in place on the global kernel
+ * in the same rounds (plan->n_inplace).  SZ_ERROR_PARAM: slice_bytes == 0,
+ * an LZMA2 item, more than 2^24 rounds. */
+SRes LzmaGpu_PlanSliced(LzmaGpuStreamDesc *descs, size_t n, uint64_t slice_bytes, unsigned kernel,
+                        uint32_t *order, LzmaGpuSlicedPlan *plan);
+/* Enqueue rounds [first_round, first_round + n_rounds) of a planned batch on
+ * `stream` (n_rounds 0 = every remaining round).  first_round 0 also resets
+ * the workspace's counters and spills every stream's initial state.  Device
+ * pointers as for DecodeBatchEx; d_order may be NULL (identity). */
+SRes LzmaGpu_DecodeBatchSliced(const LzmaGpuSlicedPlan *plan, const LzmaGpuStreamDesc *d_descs,
+                               const uint32_t *d_order, const Byte *d_src, Byte *d_dst,
+                               void *d_workspace, LzmaGpuResult *d_results, unsigned first_round,
+                               unsigned n_rounds, void *stream);
+/* Streams still unfinished when round `round` starts (round = plan->rounds:
+ * after the last; 0 once every stream is done).  Synchronises `stream`. */
+SRes LzmaGpu_SlicedActive(const LzmaGpuSlicedPlan *plan, const void *d_workspace, unsigned round,
+                          size_t *active, void *stream);
+/* Host-buffer form (uploads, every round, downloads); rounds_out may be NULL. */
+SRes LzmaGpu_DecodeBatchSlicedHost(const LzmaGpuStreamDesc *descs, size_t n, const Byte *src,
+                                   size_t src_bytes, Byte *dst, size_t dst_bytes,
+                                   LzmaGpuResult *results, uint64_t slice_bytes, unsigned kernel,
+                                   LzmaGpuSlicedPlan *plan_out);
+
 /* ---------------------------------------------------------------- CRC-32 */
 
 /* Drop-ins for 7zCrc.h (poly 0xEDB88320, 7zCrc.c:7):

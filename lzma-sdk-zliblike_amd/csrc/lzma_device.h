@@ -117,6 +117,23 @@ __host__ __device__ __forceinline__ Layout make_layout(uint32_t lc, uint32_t lp,
   L.glb_cells = b;
   return L;
 }
+// Bit 29 of a placement mask (kSessHybBit, the time-sliced lane kernel): the
+// mask's sections live in LDS, packed as usual, and the others stay at their
+// offsets in the session's whole all-global table -- a round stages only the
+// LDS sections in and out of the spilled table.
+constexpr uint32_t kSessHybBit = 0x20000000u;
+__host__ __device__ __forceinline__ Layout make_layout_m(uint32_t lc, uint32_t lp, uint32_t pb,
+                                                         uint32_t m) {
+  Layout L = make_layout(lc, lp, pb, m);
+  if (m & kSessHybBit) {
+    const Layout F = make_layout(lc, lp, pb, 0u);
+    for (uint32_t k = 0; k < S_NSEC; ++k)
+      if (!((m >> k) & 1u)) L.o[k] = F.o[k];
+    L.glb_cells = F.glb_cells;
+  }
+  return L;
+}
+
 // whole table (all sections): 56P + 950 + 0x300 << (lc+lp) cells
 __host__ __device__ __forceinline__ uint32_t table_cells(uint32_t lc, uint32_t lp, uint32_t pb) {
   return (56u << pb) + 950u + (768u << (lc + lp));
@@ -236,7 +253,7 @@ struct Tab {
   gu16* gl;
   Layout L;
   __device__ __forceinline__ Tab(const LzStateT<Lo>& s)
-      : lo(s.lo), gl(s.gl), L(make_layout(s.lc, s.lp, s.pb, M)) {}
+      : lo(s.lo), gl(s.gl), L(make_layout_m(s.lc, s.lp, s.pb, M)) {}
   // cell `off` of the global table (lane-interleaved under kIlvBit)
   __device__ __forceinline__ auto g(uint32_t off) const {
     if constexpr ((M & kIlvBit) != 0u)
@@ -1612,7 +1629,17 @@ __device__ __forceinline__ void fill_prob_init(lds_u16* p, uint32_t n) {
 
 template <uint32_t M, class Lo>
 __device__ __forceinline__ void lz_init_state_real(LzStateT<Lo>& s) {
-  const Layout L = make_layout(s.lc, s.lp, s.pb, M);
+  const Layout L = make_layout_m(s.lc, s.lp, s.pb, M);
+  if constexpr ((M & kSessHybBit) != 0u) {
+    // LDS sections packed, the others in place in the whole table
+    fill_prob_init(s.lo, L.lds_cells);
+    for (uint32_t k = 0; k < S_NSEC; ++k)
+      if (!((M >> k) & 1u)) fill_prob_init(s.gl + L.o[k], sec_cells(k, s.lc, s.lp, s.pb));
+    s.rep0 = s.rep1 = s.rep2 = s.rep3 = 1;
+    s.st = 0;
+    s.need_state_init = 0;
+    return;
+  }
 #ifndef LZGPU_HOST_EMU
   if constexpr ((M & kCoopBit) != 0u) {
     // cooperative kernel: the lanes share the stream's tables, each fills a

@@ -19,6 +19,9 @@ extern "C" int lzgpu_launch_session(LzgpuSession* d_sess, uint32_t n, hipStream_
 // lds_cells cells staged in LDS for the call; max_groups 0 = one per session
 extern "C" int lzgpu_launch_session_coop(LzgpuSession* d_sess, uint32_t n, uint32_t lds_cells,
                                          uint32_t max_groups, hipStream_t stream);
+// lets a kernel launch with up to 160 KiB of dynamic LDS (once per kernel and
+// device, thread-safe); 0 on success
+int lzgpu_allow_full_lds(const void* kfn);
 // largest table (cells) the cooperative session kernel stages in LDS: lc+lp <= 4
 // at any pb (LZMA2's bound, 28 KiB) and wider LZMA tables up to 64 KiB
 constexpr uint32_t kSessCoopMaxCells = 32768;

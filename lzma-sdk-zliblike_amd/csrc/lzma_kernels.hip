@@ -41,6 +41,8 @@ static int allow_full_lds(const void* kfn) {
   return 0;
 }
 
+int lzgpu_allow_full_lds(const void* kfn) { return allow_full_lds(kfn); }
+
 
 __global__ void __launch_bounds__(64) lzgpu_decode_batch_kernel(
     const LzmaGpuStreamDesc* __restrict__ descs, const uint32_t* __restrict__ order, uint32_t n,

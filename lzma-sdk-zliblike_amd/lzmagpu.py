@@ -111,6 +111,20 @@ def plan_options(kernel="auto", **kw):
     return o
 
 
+class SlicedPlan(ctypes.Structure):
+    """LzmaGpuSlicedPlan (include/lzma_gpu.h): a time-sliced batch."""
+    _fields_ = [("workspace_bytes", ctypes.c_uint64), ("n", ctypes.c_uint64),
+                ("slice_bytes", ctypes.c_uint64), ("rounds", ctypes.c_uint32),
+                ("kernel", ctypes.c_uint32), ("table_cells", ctypes.c_uint32),
+                ("groups_per_cu", ctypes.c_uint32), ("max_groups", ctypes.c_uint32),
+                ("lds_mask", ctypes.c_uint32), ("sess_off", ctypes.c_uint64),
+                ("list_off", ctypes.c_uint64), ("ctr_off", ctypes.c_uint64),
+                ("n_inplace", ctypes.c_uint64)]
+
+
+SLICED_KERNELS = {"auto": 0, "lane": 1, "coop": 2, "global": 3}
+
+
 class Session(ctypes.Structure):
     """LzmaGpuSession: a device-resident decoder (include/lzma_gpu.h)."""
     _fields_ = [("lc", ctypes.c_uint32), ("lp", ctypes.c_uint32), ("pb", ctypes.c_uint32),
@@ -208,6 +222,10 @@ _sig = {
     "LzmaGpu_SessionProbsBytes": (ctypes.c_size_t, [ctypes.c_char_p, ctypes.c_uint]),
     "LzmaGpu_SessionInit": (ctypes.c_int, [ctypes.POINTER(Session), ctypes.c_char_p, ctypes.c_uint, _P, _P, ctypes.c_size_t]),
     "LzmaGpu_SessionDecodeBatch": (ctypes.c_int, [_P, ctypes.c_size_t, _P]),
+    "LzmaGpu_PlanSliced": (ctypes.c_int, [ctypes.POINTER(StreamDesc), ctypes.c_size_t, ctypes.c_uint64, ctypes.c_uint, _P, ctypes.POINTER(SlicedPlan)]),
+    "LzmaGpu_DecodeBatchSliced": (ctypes.c_int, [ctypes.POINTER(SlicedPlan), _P, _P, _P, _P, _P, _P, ctypes.c_uint, ctypes.c_uint, _P]),
+    "LzmaGpu_SlicedActive": (ctypes.c_int, [ctypes.POINTER(SlicedPlan), _P, ctypes.c_uint, _sp, _P]),
+    "LzmaGpu_DecodeBatchSlicedHost": (ctypes.c_int, [ctypes.POINTER(StreamDesc), ctypes.c_size_t, _P, ctypes.c_size_t, _P, ctypes.c_size_t, ctypes.POINTER(Result), ctypes.c_uint64, ctypes.c_uint, ctypes.POINTER(SlicedPlan)]),
     "CrcGenerateTable": (None, []),
     "CrcUpdate": (ctypes.c_uint32, [ctypes.c_uint32, _P, ctypes.c_size_t]),
     "CrcCalc": (ctypes.c_uint32, [_P, ctypes.c_size_t]),
@@ -475,6 +493,46 @@ def decode_batch_device(d_descs, d_order, n, d_src, d_dst, d_ws, ws_bytes, d_res
     """All arguments are raw device pointers (ints); stream is a hipStream_t (int)."""
     return _lib.LzmaGpu_DecodeBatch(d_descs, d_order, n, d_src, d_dst, d_ws, ws_bytes, d_results,
                                     stream or None)
+
+
+def plan_sliced(descs, slice_bytes, kernel="auto"):
+    """LzmaGpu_PlanSliced: fills descs' probs_off; returns (SlicedPlan, order)."""
+    n = len(descs)
+    order = (ctypes.c_uint32 * max(n, 1))()
+    p = SlicedPlan()
+    r = _lib.LzmaGpu_PlanSliced(descs, n, slice_bytes, SLICED_KERNELS[kernel], order,
+                                ctypes.byref(p))
+    if r != SZ_OK:
+        raise RuntimeError(f"LzmaGpu_PlanSliced failed: {r}")
+    return p, order
+
+
+def decode_batch_sliced_device(plan, d_descs, d_order, d_src, d_dst, d_ws, d_results,
+                               first_round=0, n_rounds=0, stream=0):
+    """LzmaGpu_DecodeBatchSliced over raw device pointers (ints)."""
+    return _lib.LzmaGpu_DecodeBatchSliced(ctypes.byref(plan), d_descs, d_order, d_src, d_dst,
+                                          d_ws, d_results, first_round, n_rounds, stream or None)
+
+
+def sliced_active(plan, d_ws, round_, stream=0):
+    """Streams still unfinished entering round `round_` (synchronises `stream`)."""
+    v = ctypes.c_size_t(0)
+    r = _lib.LzmaGpu_SlicedActive(ctypes.byref(plan), d_ws, round_, ctypes.byref(v), stream or None)
+    if r != SZ_OK:
+        raise RuntimeError(f"LzmaGpu_SlicedActive failed: {r}")
+    return v.value
+
+
+def decode_batch_sliced_host(descs, src, dst_bytes, slice_bytes, kernel="auto", plan_out=None):
+    """Time-sliced batch from host buffers: (res, results[ctypes], dst bytes)."""
+    n = len(descs)
+    res = (Result * max(n, 1))()
+    s = _buf(src)
+    d = ctypes.create_string_buffer(max(dst_bytes, 1))
+    r = _lib.LzmaGpu_DecodeBatchSlicedHost(descs, n, s, len(src), d, dst_bytes, res, slice_bytes,
+                                           SLICED_KERNELS[kernel],
+                                           ctypes.byref(plan_out) if plan_out is not None else None)
+    return r, res, d.raw[:dst_bytes]
 
 
 def split_lzma2_blocks(src):
