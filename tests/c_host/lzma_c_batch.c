@@ -3,10 +3,12 @@
  * launch, (a) from host buffers with LzmaGpu_DecodeBatchHost, (b) device-
  * resident with LzmaGpu_PlanBatchEx + LzmaGpu_DecodeBatchEx on buffers the
  * program allocates itself through the HIP runtime's C API (caller-owned
- * device memory, no allocation inside the decode call).
+ * device memory, no allocation inside the decode call), (c) the same buffers
+ * decoded time-sliced (LzmaGpu_PlanSliced + LzmaGpu_DecodeBatchSliced, one
+ * round per call, LzmaGpu_SlicedActive between rounds).
  * TEST INFRASTRUCTURE: tests/test_c_host.py builds and runs it.
  *
- *   lzma_c_batch host|device SRC_FILE LENS_FILE PROPS_FILE CAP FINISH
+ *   lzma_c_batch host|device|sliced SRC_FILE LENS_FILE PROPS_FILE CAP FINISH
  *
  * SRC_FILE: the streams back to back; LENS_FILE: n little-endian uint64
  * lengths; PROPS_FILE: n x 5 props bytes; every stream gets CAP output bytes.
@@ -50,10 +52,10 @@ int main(int argc, char **argv) {
   LzmaGpuResult *res;
   int device;
   if (argc != 7) {
-    fprintf(stderr, "usage: %s host|device SRC LENS PROPS CAP FINISH\n", argv[0]);
+    fprintf(stderr, "usage: %s host|device|sliced SRC LENS PROPS CAP FINISH\n", argv[0]);
     return 2;
   }
-  device = strcmp(argv[1], "device") == 0;
+  device = strcmp(argv[1], "device") == 0 ? 1 : strcmp(argv[1], "sliced") == 0 ? 2 : 0;
   src = read_file(argv[2], &ns);
   lens_b = read_file(argv[3], &nl);
   props = read_file(argv[4], &np);
@@ -84,6 +86,48 @@ int main(int argc, char **argv) {
       fprintf(stderr, "LzmaGpu_DecodeBatchHost: %d %s\n", (int)r, LzmaGpu_LastError());
       return 4;
     }
+  } else if (device == 2) {
+    /* time-sliced: 4 KiB of output per stream and round, rounds enqueued one
+       at a time, the unfinished count read back between them */
+    LzmaGpuSlicedPlan sp;
+    uint32_t *order = (uint32_t *)malloc((n ? n : 1) * sizeof(uint32_t));
+    void *d_src, *d_dst, *d_ws, *d_desc, *d_order, *d_res;
+    unsigned r;
+    size_t active, prev = n;
+    hipStream_t stream;
+    if (LzmaGpu_PlanSliced(descs, n, 4096, LZMA_GPU_SLICED_AUTO, order, &sp) != SZ_OK) return 4;
+    HIP_OK(hipMalloc(&d_src, ns + 16));
+    HIP_OK(hipMalloc(&d_dst, dst_bytes + 16));
+    HIP_OK(hipMalloc(&d_ws, sp.workspace_bytes + 16));
+    HIP_OK(hipMalloc(&d_desc, n * sizeof *descs + 16));
+    HIP_OK(hipMalloc(&d_order, n * sizeof(uint32_t) + 16));
+    HIP_OK(hipMalloc(&d_res, n * sizeof *res + 16));
+    HIP_OK(hipStreamCreate(&stream));
+    HIP_OK(hipMemcpy(d_src, src, ns, hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(d_desc, descs, n * sizeof *descs, hipMemcpyHostToDevice));
+    HIP_OK(hipMemcpy(d_order, order, n * sizeof(uint32_t), hipMemcpyHostToDevice));
+    for (r = 0; r < sp.rounds; ++r) {
+      if (LzmaGpu_DecodeBatchSliced(&sp, (const LzmaGpuStreamDesc *)d_desc,
+                                    (const uint32_t *)d_order, (const Byte *)d_src, (Byte *)d_dst,
+                                    d_ws, (LzmaGpuResult *)d_res, r, 1, (void *)stream) != SZ_OK ||
+          LzmaGpu_SlicedActive(&sp, d_ws, r + 1, &active, (void *)stream) != SZ_OK) {
+        fprintf(stderr, "sliced round %u: %s\n", r, LzmaGpu_LastError());
+        return 4;
+      }
+      if (active > prev) return 5; /* the unfinished count never rises */
+      prev = active;
+    }
+    if (prev != 0) return 6;
+    HIP_OK(hipMemcpy(res, d_res, n * sizeof *res, hipMemcpyDeviceToHost));
+    HIP_OK(hipMemcpy(dst, d_dst, dst_bytes, hipMemcpyDeviceToHost));
+    HIP_OK(hipStreamDestroy(stream));
+    HIP_OK(hipFree(d_src));
+    HIP_OK(hipFree(d_dst));
+    HIP_OK(hipFree(d_ws));
+    HIP_OK(hipFree(d_desc));
+    HIP_OK(hipFree(d_order));
+    HIP_OK(hipFree(d_res));
+    free(order);
   } else {
     LzmaGpuPlan plan;
     uint32_t *order = (uint32_t *)malloc((n ? n : 1) * sizeof(uint32_t));

@@ -123,9 +123,10 @@ def test_gpu_c_host_matches_oracle(tmp_path):
 @pytest.mark.gpu
 def test_gpu_c_batch_host_and_device_match_oracle(tmp_path):
     """300 streams (mixed lc/lp/pb and dictionaries, corrupt and truncated ones)
-    through LzmaGpu_DecodeBatchHost and through PlanBatchEx + DecodeBatchEx on
-    the C program's own hipMalloc'd buffers: per-stream results and output CRCs
-    equal the oracle's LzmaDecode."""
+    through LzmaGpu_DecodeBatchHost, through PlanBatchEx + DecodeBatchEx on the
+    C program's own hipMalloc'd buffers, and time-sliced (PlanSliced, rounds of
+    4 KiB enqueued one at a time): per-stream results and output CRCs equal the
+    oracle's LzmaDecode."""
     import lzma
     import random
     import struct
@@ -160,7 +161,7 @@ def test_gpu_c_batch_host_and_device_match_oracle(tmp_path):
     open(files["src"], "wb").write(b"".join(srcs))
     open(files["lens"], "wb").write(b"".join(struct.pack("<Q", x) for x in lens))
     open(files["props"], "wb").write(b"".join(props_all))
-    for mode in ("host", "device"):
+    for mode in ("host", "device", "sliced"):
         r = subprocess.run([BATCH_BIN, mode, files["src"], files["lens"], files["props"],
                             str(cap), "0"], stdout=subprocess.PIPE, stderr=subprocess.PIPE,
                            text=True, timeout=120)
