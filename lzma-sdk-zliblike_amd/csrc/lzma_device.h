@@ -556,6 +556,43 @@ struct LocalReader {
 
 // ------------------------------------------------------------------ range decoder
 
+// Deferred probability stores (Rc::sub3d): three pending (cell, value) pairs,
+// always three stores per flush (unused slots write a cell no decision reads,
+// the Align tree's cell 0), so the number of vector-memory operations between
+// a batch's loads and their use is the same on every path and the compiler's
+// vmcnt waits stay exact.
+__device__ __forceinline__ gu16* cell_addr(gu16* p) { return p; }
+__device__ __forceinline__ gu16* cell_addr(GS p) { return p.p; }
+struct Pend3 {
+  gu16* a0;
+  gu16* a1;
+  gu16* a2;
+  uint32_t v0, v1, v2;
+  __device__ __forceinline__ void clear(gu16* dummy) {
+    a0 = a1 = a2 = dummy;
+    v0 = v1 = v2 = 0;
+  }
+  __device__ __forceinline__ void set(gu16* x0, uint32_t w0, gu16* x1, uint32_t w1, gu16* x2,
+                                      uint32_t w2) {
+    a0 = x0; v0 = w0;
+    a1 = x1; v1 = w1;
+    a2 = x2; v2 = w2;
+  }
+  __device__ __forceinline__ void flush() {
+    *a0 = uint16_t(v0);
+    *a1 = uint16_t(v1);
+    *a2 = uint16_t(v2);
+  }
+};
+#ifndef LZGPU_DEFER
+#define LZGPU_DEFER 0
+#endif
+// deferred stores in the throughput placement's global match path
+template <uint32_t M>
+__host__ __device__ constexpr bool defer_on() {
+  return LZGPU_DEFER != 0 && (M & ~kIlvBit) == LZGPU_LDS_MASK;
+}
+
 template <class Rd>
 struct Rc {
   uint32_t range, code;
@@ -711,6 +748,39 @@ struct Rc {
     const uint32_t p2 = b0 ? (b1 ? c[6] : c[5]) : (b1 ? c[4] : c[3]);
     const uint32_t b2 = bit_v(p2, probs + m);
     return 2 * m + b2;
+  }
+  // decision on a preloaded value; the update is returned in np, not stored
+  __device__ __forceinline__ uint32_t bit_vn(uint32_t p, uint32_t& np) {
+    norm();
+    const uint32_t bound = (range >> 11) * p;
+    const bool b = code >= bound;
+    const int32_t m = b ? 0 : int32_t(kProbOne - 31);
+    np = uint32_t(int32_t(p) - ((int32_t(p) - m) >> 5));
+    range = b ? range - bound : bound;
+    code = b ? code - bound : code;
+    return b ? 1u : 0u;
+  }
+  // sub3 with deferred stores (global trees of the throughput kernel): the
+  // seven loads issue first, then (Flush) the previous batch's three pending
+  // updates are stored, and this batch's three updates become pending -- so
+  // the next batch's loads do not wait behind them in the in-order vmcnt
+  // queue.  The caller keeps every pending cell out of the next batch.
+  template <bool Flush, class P>
+  __device__ __forceinline__ uint32_t sub3d(P probs, uint32_t root, Pend3& pd) {
+    const uint32_t r2 = root * 2, r4 = root * 4;
+    const uint32_t c0 = probs[root], c10 = probs[r2], c11 = probs[r2 + 1];
+    const uint32_t c20 = probs[r4], c21 = probs[r4 + 1], c22 = probs[r4 + 2],
+                   c23 = probs[r4 + 3];
+    if constexpr (Flush) pd.flush();
+    uint32_t n0, n1, n2;
+    const uint32_t b0 = bit_vn(c0, n0);
+    uint32_t m = r2 + b0;
+    const uint32_t b1 = bit_vn(b0 ? c11 : c10, n1);
+    const uint32_t m1 = 2 * m + b1;
+    const uint32_t p2 = b0 ? (b1 ? c23 : c22) : (b1 ? c21 : c20);
+    const uint32_t b2 = bit_vn(p2, n2);
+    pd.set(cell_addr(probs + root), n0, cell_addr(probs + m), n1, cell_addr(probs + m1), n2);
+    return 2 * m1 + b2;
   }
   // 8-level tree in global memory in three load batches (3 + 3 + 2 levels)
   // instead of eight dependent round trips; returns the node (256..511).
@@ -890,15 +960,53 @@ __device__ __forceinline__ void stu_tail(gbyte* d, uint64_t v, uint32_t rem) {
   if (rem & 1) lz_put(d, uint32_t(v));
 }
 
+// WantMb (the kernels that keep the next matched byte in a register): `mb`
+// gets the byte at distance dist from pos + n -- the next matched literal's
+// -- where the copy's own loads already hold it (mb_ok), so the caller does
+// not reload it behind the copy's stores (a load's data waits for every
+// older store in the in-order vmcnt queue: ~600-950 cycles against ~200 for
+// an L2 hit).  Short non-overlapping matches (dist > n, n <= 15: most of
+// them) load both 8-byte halves before either store.
+// `mid` runs after the copy's loads and before its stores on the short path
+// (before everything on the others): the deferred probability stores of the
+// match path go there.
+struct LzNoop {
+  __device__ __forceinline__ void operator()() const {}
+};
+template <bool WantMb = false, class Mid = LzNoop>
 __device__ __forceinline__ uint32_t lz_copy(gbyte* dic, uint64_t pos, uint64_t from, uint32_t n,
-                                            uint32_t dist, uint64_t cap) {
+                                            uint32_t dist, uint64_t cap, uint32_t* mb = nullptr,
+                                            bool* mb_ok = nullptr, Mid mid = Mid()) {
   uint32_t last = 0;
+  if constexpr (WantMb) *mb_ok = false;
   if (from + n <= cap && from < pos) {
     // source span does not wrap (always so for a flat LzmaDecode window)
     gbyte* d = dic + pos;
     const gbyte* src = dic + from;
     uint64_t v = 0;
     uint32_t i = 0;
+    if constexpr (WantMb) {
+      if (dist > n && n <= 15 && from + 16 <= cap) {
+        // bytes 0..n of the source lie below pos (n < dist): the words may
+        // also cover bytes at or past pos, which are never used
+        const uint64_t c0 = ldu64(src);
+        const uint64_t c1 = ldu64(src + 8);  // unconditional: no branch around a load
+        mid();
+        if (n >= 8) {
+          stu64(d, c0);
+          if (n > 8) stu_tail(d + 8, c1, n - 8);
+        } else {
+          stu_tail(d, c0, n);
+        }
+        auto byte_at = [&](uint32_t k) -> uint32_t {
+          return uint32_t((k < 8 ? c0 >> (8 * k) : c1 >> (8 * (k - 8)))) & 0xFFu;
+        };
+        *mb = byte_at(n);
+        *mb_ok = true;
+        return byte_at(n - 1);
+      }
+    }
+    mid();
     if (dist >= 8) {
       // src[i..i+8) lies below d + i: written before this step reads it
       for (; i + 8 <= n; i += 8) {
@@ -933,12 +1041,18 @@ __device__ __forceinline__ uint32_t lz_copy(gbyte* dic, uint64_t pos, uint64_t f
           stu64(d + i, v);
         else
           stu_tail(d + i, v, rem);
+        if constexpr (WantMb) {
+          // v byte k = pattern byte i + k; pattern byte i + 8 = v byte t
+          *mb = uint32_t(v >> (8 * (rem == 8 ? t : rem))) & 0xFFu;
+          *mb_ok = true;
+        }
         return uint32_t(v >> (8 * (rem - 1))) & 0xFFu;
       }
       stu64(d + i, v);
       v = (v >> (8 * t)) | (v << (8 * (dist - t)));
     }
   }
+  mid();  // (the paths above all return)
   if (from + n <= cap) {
     gbyte* d = dic + pos;
     const gbyte* s = dic + from;
@@ -966,6 +1080,73 @@ __device__ __forceinline__ uint32_t lz_copy(gbyte* dic, uint64_t pos, uint64_t f
     } while (--n != 0);
   }
   return last;
+}
+
+// j mod d for j < 2^16, d >= 1, from the float reciprocal rd = 1/d: the
+// quotient is exact or one off, corrected by one compare each way.
+__device__ __forceinline__ uint32_t lz_mod_small(uint32_t j, uint32_t d, float rd) {
+  const int32_t q = int32_t(float(j) * rd);
+  int32_t r = int32_t(j) - q * int32_t(d);
+  r += (r < 0) ? int32_t(d) : 0;
+  r -= (r >= int32_t(d)) ? int32_t(d) : 0;
+  return uint32_t(r);
+}
+
+// LZ copy of the wave-cooperative kernel (every lane holds the same state).
+// Byte j of the match (j < n) is the window byte at from + (j mod dist) --
+// written before this match, by byte-serial overlap semantics -- and the byte
+// the next matched literal reads (the one at distance dist from pos + n) is
+// the j = n term of the same formula.  So all of them are loaded in one batch,
+// lane l taking j = l, l + 32, ...: one global round trip per 32 bytes instead
+// of one per 8 bytes, and no reload of the matched byte behind the copy's own
+// stores (a load waits for every earlier store in the in-order vmcnt queue).
+// Lanes of one wave see each other's global stores in order (one vector L1).
+// Returns the last byte copied; `mb` gets the next matched byte.
+constexpr uint32_t kCoopLanes = 32u;
+__device__ __forceinline__ uint32_t lz_copy_coop(gbyte* dic, uint64_t pos, uint64_t from,
+                                                 uint32_t n, uint32_t dist, uint64_t cap,
+                                                 uint32_t& mb) {
+  const bool per = dist <= n;  // the match overlaps itself: period dist
+#ifdef LZGPU_HOST_EMU
+  // one lane plays every lane: all loads (sources lie before pos), then stores
+  uint8_t v[kLenDone];  // n <= 273
+  for (uint32_t j = 0; j <= n; ++j) {
+    uint64_t a = from + (per ? j % dist : j);
+    v[j] = dic[a >= cap ? a - cap : a];
+  }
+  for (uint32_t j = 0; j < n; ++j) dic[pos + j] = v[j];
+  mb = v[n];
+  return v[n - 1];
+#else
+  const float rd = per ? __builtin_amdgcn_rcpf(float(dist)) : 0.f;
+  const uint32_t lane = lz_lane_id() & (kCoopLanes - 1u);
+  // window index of byte j (j <= n); j > n: a harmless in-window address
+  auto src_of = [&](uint32_t j) -> uint64_t {
+    const uint32_t k = j > n ? 0u : (per ? lz_mod_small(j, dist, rd) : j);
+    const uint64_t a = from + k;
+    return a >= cap ? a - cap : a;
+  };
+  uint32_t my_last = 0, my_mb = 0;
+  // the first 64 bytes (almost every match): both loads before any store
+  const uint32_t j0 = lane, j1 = lane + kCoopLanes;
+  const uint32_t v0 = dic[src_of(j0)];
+  uint32_t v1 = 0;
+  if (n >= kCoopLanes) v1 = dic[src_of(j1)];
+  if (j0 < n) dic[pos + j0] = uint8_t(v0);
+  if (j1 < n) dic[pos + j1] = uint8_t(v1);
+  my_last = (j0 + 1 == n) ? v0 : ((j1 + 1 == n) ? v1 : 0u);
+  my_mb = (j0 == n) ? v0 : ((j1 == n) ? v1 : 0u);
+  // longer matches: 32 bytes per round trip
+  for (uint32_t b = 2 * kCoopLanes; b <= n; b += kCoopLanes) {
+    const uint32_t j = b + lane;
+    const uint32_t v = dic[src_of(j)];
+    if (j < n) dic[pos + j] = uint8_t(v);
+    my_last = (j + 1 == n) ? v : my_last;
+    my_mb = (j == n) ? v : my_mb;
+  }
+  mb = uint32_t(__builtin_amdgcn_readlane(int(my_mb), int(n & (kCoopLanes - 1u))));
+  return uint32_t(__builtin_amdgcn_readlane(int(my_last), int((n - 1) & (kCoopLanes - 1u))));
+#endif
 }
 
 // ------------------------------------------------------------------ symbol loop
@@ -1207,6 +1388,8 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
 #endif
     const uint64_t tm0 = lz_clock();
 #endif
+    [[maybe_unused]] Pend3 pd;
+    if constexpr (defer_on<M>()) pd.clear(cell_addr(T.template at<S_ALIGN>(0)));
     if (!rc.bit(T.template at<S_REP>(st))) {
       st += 12;
       lcoder_is_rep = 0;
@@ -1214,11 +1397,25 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
       if (full == 0 && total == 0) return kErrData;
       if (!rc.bit(T.template at<S_REP>(12 + st))) {
         if (!rc.bit(T.template at<S_REP0L>((st << pb) + ps))) {
-          prev = dic[ring_back(pos, r0, cap)];
-          lz_put(dic + pos++, prev);
+          if constexpr ((M & kCoopBit) != 0u) {
+            // short rep = a one-byte copy: the byte and the next matched byte
+            // in one load batch
+            prev = lz_copy_coop(dic, pos, ring_back(pos, r0, cap), 1, r0, cap, mb_pf);
+            pos++;
+          } else if constexpr (mb_pf_on<M>()) {
+            // the byte and the next matched byte (at pos + 1 - rep0: the byte
+            // after it, or for rep0 = 1 the byte itself) loaded before the store
+            const uint64_t f = ring_back(pos, r0, cap);
+            prev = dic[f];
+            const uint32_t nxt = dic[f + 1 == cap ? 0 : f + 1];
+            lz_put(dic + pos++, prev);
+            mb_pf = r0 > 1 ? nxt : prev;
+          } else {
+            prev = dic[ring_back(pos, r0, cap)];
+            lz_put(dic + pos++, prev);
+          }
           total++;
           st = (st < 7) ? 9 : 11;
-          if constexpr (mb_pf_on<M>()) mb_pf = dic[ring_back(pos, r0, cap)];
           continue;
         }
       } else {
@@ -1273,12 +1470,21 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
         } else {
         const uint32_t ch = lbase[0];
         auto lo_t = lbase + 2 + (ps << 3);
+        if constexpr (defer_on<M>()) {
+          if (!rc.bit_v(ch, lbase))
+            len = rc.template sub3d<false>(lo_t, 1, pd) - 8;
+          else if (!rc.bit(lbase + 1))
+            len = 8 + rc.template sub3d<false>(lbase + 2 + (8u << pb) + (ps << 3), 1, pd) - 8;
+          else
+            len = 16 + rc.template tree<8>(T.template at<S_LENHI>(lcoder_is_rep << 8));
+        } else {
         if (!rc.bit_v(ch, lbase))
           len = rc.sub3(lo_t, 1) - 8;
         else if (!rc.bit(lbase + 1))
           len = 8 + rc.sub3(lbase + 2 + (8u << pb) + (ps << 3), 1) - 8;
         else
           len = 16 + rc.template tree<8>(T.template at<S_LENHI>(lcoder_is_rep << 8));
+        }
         }
       } else {
         if (!rc.bit(lbase))
@@ -1299,6 +1505,9 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
       uint32_t dist;
       if constexpr (((M >> S_SLOT) & 1u) == 0u) {
         auto sl_t = T.template at<S_SLOT>(lstate << 6);
+        if constexpr (defer_on<M>()) {
+          dist = rc.template sub3d<true>(sl_t, rc.template sub3d<true>(sl_t, 1, pd), pd) - 64;
+        } else {
 #if LZGPU_PROF == 1 && !defined(LZGPU_HOST_EMU)
         // one global round trip + 3 decisions, timed (profiling builds)
         const uint64_t t0 = lz_clock();
@@ -1311,6 +1520,7 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
 #else
         dist = rc.sub3(sl_t, rc.sub3(sl_t, 1)) - 64;
 #endif
+        }
       } else {
         dist = rc.template tree<6>(T.template at<S_SLOT>(lstate << 6));
       }
@@ -1325,7 +1535,10 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
           if constexpr (((M >> S_SPEC) & 1u) == 0u) {
             if (nbits >= 3) {
               // first three reverse-tree bits in one load batch
-              node = rc.sub3(T.template at<S_SPEC>(sp), 1);
+              if constexpr (defer_on<M>())
+                node = rc.template sub3d<true>(T.template at<S_SPEC>(sp), 1, pd);
+              else
+                node = rc.sub3(T.template at<S_SPEC>(sp), 1);
               dist |= ((node >> 2) & 1u) | (((node >> 1) & 1u) << 1) | ((node & 1u) << 2);
               mask = 8;
               nbits -= 3;
@@ -1356,7 +1569,10 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
               dist |= ((node >> 3) & 1u) | (((node >> 2) & 1u) << 1) |
                       (((node >> 1) & 1u) << 2) | ((node & 1u) << 3);
             } else {
-              node = rc.sub3(T.template at<S_ALIGN>(0), 1);
+              if constexpr (defer_on<M>())
+                node = rc.template sub3d<true>(T.template at<S_ALIGN>(0), 1, pd);
+              else
+                node = rc.sub3(T.template at<S_ALIGN>(0), 1);
               dist |= ((node >> 2) & 1u) | (((node >> 1) & 1u) << 1) | ((node & 1u) << 2);
               const uint32_t b = rc.bit(T.template at<S_ALIGN>(node));
               dist |= b << 3;
@@ -1370,6 +1586,7 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
             }
           }
           if (dist == 0xFFFFFFFFu) {
+            if constexpr (defer_on<M>()) pd.flush();
             len += kLenDone;
             st -= 12;
             break;
@@ -1380,9 +1597,8 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
       r2 = r1;
       r1 = r0;
       r0 = dist + 1;
-      if (full == 0) {
-        if (dist >= total) return kErrData;
-      } else if (dist >= full) {
+      if (full == 0 ? dist >= total : dist >= full) {
+        if constexpr (defer_on<M>()) pd.flush();
         return kErrData;
       }
       st = (st < 19) ? 7 : 10;
@@ -1393,16 +1609,31 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
     }
     len += 2;
     LZ_PROF_MARK(s, 1, t_prof);
-    if (limit == pos) return kErrData;
+    if (limit == pos) {
+      if constexpr (defer_on<M>()) pd.flush();
+      return kErrData;
+    }
     {
       const uint64_t room = limit - pos;
       const uint32_t n = (room < len) ? uint32_t(room) : len;
       const uint64_t from = ring_back(pos, r0, cap);
       total += n;
       len -= n;
-      prev = lz_copy(dic, pos, from, n, r0, cap);
-      pos += n;
-      if constexpr (mb_pf_on<M>()) mb_pf = dic[ring_back(pos, r0, cap)];
+      if constexpr ((M & kCoopBit) != 0u) {
+        prev = lz_copy_coop(dic, pos, from, n, r0, cap, mb_pf);
+        pos += n;
+      } else if constexpr (mb_pf_on<M>()) {
+        bool mb_ok;
+        if constexpr (defer_on<M>())
+          prev = lz_copy<true>(dic, pos, from, n, r0, cap, &mb_pf, &mb_ok, [&]() { pd.flush(); });
+        else
+          prev = lz_copy<true>(dic, pos, from, n, r0, cap, &mb_pf, &mb_ok);
+        pos += n;
+        if (!mb_ok) mb_pf = dic[ring_back(pos, r0, cap)];
+      } else {
+        prev = lz_copy(dic, pos, from, n, r0, cap);
+        pos += n;
+      }
     }
     LZ_PROF_MARK(s, 2, t_prof);
   } while (pos < limit && rd.used() < in_limit);

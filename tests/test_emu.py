@@ -38,6 +38,9 @@ EMU_VARIANTS = {
     "interleaved_global_instantiation": "-DEMU_ILV",
     "coop_instantiation": "-DEMU_COOP",
     "coop_all_lds_instantiation": "-DEMU_COOP_ALL",
+    # deferred probability stores of the throughput placement's match path
+    "deferred_stores": "-DLZGPU_DEFER=1",
+    "deferred_stores_interleaved": "-DLZGPU_DEFER=1 -DEMU_ILV",
 }
 
 
