@@ -215,6 +215,11 @@ constexpr uint32_t kIlvLaneCells = 1u;
 #ifndef LZGPU_PROF
 #define LZGPU_PROF 0
 #endif
+// LZGPU_SPEC_UST (A/B): the cooperative literal stage's probability updates
+// stored by every lane (uniform cells and values) instead of by the winner lane
+#ifndef LZGPU_SPEC_UST
+#define LZGPU_SPEC_UST 0
+#endif
 
 // Per-lane decoder state (CLzmaDec fields, LzmaDec.h:50-69).  lo = the LDS
 // table (pointer type Lo: lds_u16*; or gu16* aliasing gl when everything is
@@ -396,7 +401,22 @@ struct GlobalReader16 {
 // is already loaded (nlo:nhi) when the current one runs out, and only then is
 // the one after requested.  Same contract as GlobalReader16 otherwise:
 // used() = bytes consumed, never loads a block wholly outside [p, p+avail).
-struct GlobalReaderQ {
+// Uni (the wave-cooperative kernel, LZGPU_COOP_UNI): every lane holds the same
+// reader, so its branch conditions are taken wave-uniform (a ballot: the
+// compiler then branches on SCC instead of saving and restoring EXEC).
+template <bool Uni>
+__device__ __forceinline__ bool lz_uc(bool c) {
+#ifdef LZGPU_HOST_EMU
+  return c;
+#else
+  if constexpr (Uni)
+    return __builtin_amdgcn_ballot_w64(c) != 0;
+  else
+    return c;
+#endif
+}
+template <bool Uni>
+struct GlobalReaderQT {
 #ifdef LZGPU_HOST_EMU
   struct u32x4 { uint32_t x, y, z, w; };
 #else
@@ -430,7 +450,8 @@ struct GlobalReaderQ {
   __device__ __forceinline__ void pop_word() {
     blo = (blo >> 32) | (bhi << 32);
     bhi >>= 32;
-    if (--bw == 0) {
+    --bw;
+    if (lz_uc<Uni>(bw == 0)) {
       blo = uint64_t(nx.x) | (uint64_t(nx.y) << 32);
       bhi = uint64_t(nx.z) | (uint64_t(nx.w) << 32);
       bw = 4;
@@ -458,7 +479,7 @@ struct GlobalReaderQ {
   }
   __device__ __forceinline__ uint32_t used() const { return taken - nb; }
   __device__ __forceinline__ void topup() {
-    if (nb <= 4) {
+    if (lz_uc<Uni>(nb <= 4)) {
       win |= uint64_t(uint32_t(blo)) << (8 * nb);
       nb += 4;
       taken += 4;
@@ -474,17 +495,31 @@ struct GlobalReaderQ {
     return b;
   }
   __device__ __forceinline__ uint32_t next() {
-    if (nb == 0) topup();
+    if (lz_uc<Uni>(nb == 0)) topup();
     return take_u();
   }
   __device__ __forceinline__ void advance(bool n) {
-    if (n) {
+    if (lz_uc<Uni>(n)) {
       win >>= 8;
       --nb;
-      if (nb == 0) topup();
+      if (lz_uc<Uni>(nb == 0)) topup();
     }
   }
 };
+typedef GlobalReaderQT<false> GlobalReaderQ;
+typedef GlobalReaderQT<true> GlobalReaderQU;
+template <class Rd>
+constexpr bool kIsQ = __is_same(Rd, GlobalReaderQ) || __is_same(Rd, GlobalReaderQU);
+template <class Rd>
+constexpr bool kUniRd = __is_same(Rd, GlobalReaderQU);
+#ifndef LZGPU_COOP_UNI
+#define LZGPU_COOP_UNI 0
+#endif
+#if LZGPU_COOP_UNI
+typedef GlobalReaderQU CoopReader;
+#else
+typedef GlobalReaderQ CoopReader;
+#endif
 
 typedef GlobalReader16 PlainReader;
 // Reader of the bulk pass per placement: the checkpoint reader for the
@@ -508,7 +543,7 @@ struct BulkReaderFor<LZGPU_LDS_MASK | kIlvBit> {
 };
 template <>
 struct BulkReaderFor<LZGPU_LDS_MASK_LAT | kCoopBit> {
-  typedef GlobalReaderQ type;
+  typedef CoopReader type;
 };
 // every section in LDS (cooperative classes with few streams per CU)
 #ifndef LZGPU_LDS_MASK_ALL
@@ -516,7 +551,7 @@ struct BulkReaderFor<LZGPU_LDS_MASK_LAT | kCoopBit> {
 #endif
 template <>
 struct BulkReaderFor<LZGPU_LDS_MASK_ALL | kCoopBit> {
-  typedef GlobalReaderQ type;
+  typedef CoopReader type;
 };
 
 // Matched-byte prefetch per placement: the byte at rep0 is loaded at match end in
@@ -533,11 +568,11 @@ __host__ __device__ constexpr bool mb_pf_on() {
 // checkpoint hooks for readers without them: every NORMALIZE checks
 template <class Rd>
 __device__ __forceinline__ void rd_topup(Rd& rd) {
-  if constexpr (__is_same(Rd, GlobalReaderQ)) rd.topup();
+  if constexpr (kIsQ<Rd>) rd.topup();
 }
 template <class Rd>
 __device__ __forceinline__ uint32_t rd_take_u(Rd& rd) {
-  if constexpr (__is_same(Rd, GlobalReaderQ))
+  if constexpr (kIsQ<Rd>)
     return rd.take_u();
   else
     return rd.next();
@@ -599,14 +634,14 @@ struct Rc {
   Rd* rd;
   // NORMALIZE (LzmaDec.c:17): shift in one input byte when range < 2^24
   __device__ __forceinline__ void norm() {
-    if (range < kTop) {
+    if (lz_uc<kUniRd<Rd>>(range < kTop)) {
       range <<= 8;
       code = (code << 8) | rd->next();
     }
   }
   // NORMALIZE after a reader checkpoint: the byte is known to be in the window
   __device__ __forceinline__ void norm_u() {
-    if (range < kTop) {
+    if (lz_uc<kUniRd<Rd>>(range < kTop)) {
       range <<= 8;
       code = (code << 8) | rd_take_u(*rd);
     }
@@ -622,7 +657,7 @@ struct Rc {
     *prob = uint16_t(int32_t(p) - ((int32_t(p) - m) >> 5));
     range = b ? range - bound : bound;
     code = b ? code - bound : code;
-    return b ? 1u : 0u;
+    return lz_uc<kUniRd<Rd>>(b) ? 1u : 0u;
   }
   // decision on a preloaded value p with norm_u
   template <class P>
@@ -634,7 +669,7 @@ struct Rc {
     *prob = uint16_t(int32_t(p) - ((int32_t(p) - m) >> 5));
     range = b ? range - bound : bound;
     code = b ? code - bound : code;
-    return b ? 1u : 0u;
+    return lz_uc<kUniRd<Rd>>(b) ? 1u : 0u;
   }
   // BITS levels of an MSB-first tree from node m (no refill checks: at most
   // 5 levels after a checkpoint); returns the node reached
@@ -658,7 +693,7 @@ struct Rc {
     *prob = uint16_t(int32_t(p) - ((int32_t(p) - m) >> 5));
     range = b ? range - bound : bound;
     code = b ? code - bound : code;
-    return b ? 1u : 0u;
+    return lz_uc<kUniRd<Rd>>(b) ? 1u : 0u;
   }
   // decision on an already-loaded probability value p, update stored to *prob
   template <class P>
@@ -670,7 +705,7 @@ struct Rc {
     *prob = uint16_t(int32_t(p) - ((int32_t(p) - m) >> 5));
     range = b ? range - bound : bound;
     code = b ? code - bound : code;
-    return b ? 1u : 0u;
+    return lz_uc<kUniRd<Rd>>(b) ? 1u : 0u;
   }
   // MSB-first bit tree of BITS levels (TREE_DECODE); returns [0, 1 << BITS)
   template <int BITS, class P>
@@ -758,7 +793,7 @@ struct Rc {
     np = uint32_t(int32_t(p) - ((int32_t(p) - m) >> 5));
     range = b ? range - bound : bound;
     code = b ? code - bound : code;
-    return b ? 1u : 0u;
+    return lz_uc<kUniRd<Rd>>(b) ? 1u : 0u;
   }
   // sub3 with deferred stores (global trees of the throughput kernel): the
   // seven loads issue first, then (Flush) the previous batch's three pending
@@ -854,8 +889,8 @@ __device__ __forceinline__ void spec_path(uint32_t j, uint32_t m0, P probs, uint
   o.ok = ok;
 }
 
-template <int L, class P>
-__device__ __forceinline__ uint32_t spec_stage(Rc<GlobalReaderQ>& rc, P probs, uint32_t m0) {
+template <int L, class Rd, class P>
+__device__ __forceinline__ uint32_t spec_stage(Rc<Rd>& rc, P probs, uint32_t m0) {
   constexpr uint32_t kPaths = 1u << L;
   SpecPath<L> o;
   uint32_t w;
@@ -877,7 +912,18 @@ __device__ __forceinline__ uint32_t spec_stage(Rc<GlobalReaderQ>& rc, P probs, u
   const uint32_t wlo = uint32_t(__builtin_amdgcn_readlane(int(uint32_t(o.win)), int(wl)));
   const uint32_t whi = uint32_t(__builtin_amdgcn_readlane(int(uint32_t(o.win >> 32)), int(wl)));
   o.win = uint64_t(wlo) | (uint64_t(whi) << 32);
+#if LZGPU_SPEC_UST
+  // every lane stores the winner's updates (wave-uniform cells and values):
+  // no exec-mask region around the stores
+  (void)mine;
+#pragma unroll
+  for (int k = 0; k < L; ++k)
+    probs[(m0 << k) | (w >> (L - k))] =
+        uint16_t(__builtin_amdgcn_readlane(int(o.np[k]), int(wl)));
+  if (false)
+#else
   if (mine)
+#endif
 #endif
   {
 #pragma unroll
@@ -892,8 +938,8 @@ __device__ __forceinline__ uint32_t spec_stage(Rc<GlobalReaderQ>& rc, P probs, u
 
 // the plain literal tree in two cooperative stages (5 + 3 levels); the caller's
 // IsMatch checkpoint is followed by one here, and one between the stages
-template <class P>
-__device__ __forceinline__ uint32_t lit8_coop(Rc<GlobalReaderQ>& rc, P probs) {
+template <class Rd, class P>
+__device__ __forceinline__ uint32_t lit8_coop(Rc<Rd>& rc, P probs) {
   rc.rd->topup();
   const uint32_t m = spec_stage<5>(rc, probs, 1u);
   rc.rd->topup();
@@ -1184,7 +1230,7 @@ __device__ __forceinline__ void lz_literal(Rc<Rd>& rc, const Tab<M, Lo>& T, uint
   if (full != 0 || total != 0) ctx = ((total & lp_mask) << lc) + (prev >> (8 - lc));
   if (st < 7) {
     st = (st < 4) ? 0 : st - 3;
-    if constexpr (((M & kCoopBit) != 0u) && __is_same(Rd, GlobalReaderQ)) {
+    if constexpr (((M & kCoopBit) != 0u) && kIsQ<Rd>) {
       sym = lit8_coop(rc, T.template at<S_LITP>(ctx << 8));
     } else {
       auto lp = T.template at<S_LITP>(ctx << 8);

@@ -16,7 +16,7 @@ for spec in "$@"; do
   python3 -c "
 import json
 d=json.load(open('$OUT/$tag.json'))
-r=d['roofline']; p=d['config'].get('kernel_plan')
-print('$cfg', '$streams', '[$v]', d['value'], 'MB/s', r['kernel_avg_ms'], 'ms', p, d['verified'])" || echo "$tag exit $s"
+r=d.get('roofline') or {}; p=d.get('config', {}).get('kernel_plan')
+print('$cfg', '$streams', '[$v]', d['value'], 'MB/s', r.get('kernel_avg_ms', d.get('ms_per_step')), 'ms', p, d['verified'])" || echo "$tag exit $s"
   [ $s -eq 0 ] || [ $s -eq 3 ] || exit $s
 done

@@ -41,6 +41,8 @@ EMU_VARIANTS = {
     # deferred probability stores of the throughput placement's match path
     "deferred_stores": "-DLZGPU_DEFER=1",
     "deferred_stores_interleaved": "-DLZGPU_DEFER=1 -DEMU_ILV",
+    # the cooperative kernel's reader and decisions with wave-uniform branches
+    "coop_uniform_branches": "-DLZGPU_COOP_UNI=1 -DEMU_COOP_ALL",
 }
 
 

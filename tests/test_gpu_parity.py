@@ -98,6 +98,51 @@ def test_golden_streaming_decode_to_buf(L):
     assert not bad, bad[:5]
 
 
+def test_streaming_ring_wrap_cooperative_copy(L):
+    """The drop-in DecodeToBuf (cooperative session kernel: lz_copy_coop) over
+    streams 5-30x longer than a 4 KiB dictionary ring, so match sources and the
+    next matched byte wrap the ring end; runs give periodic copies (dist < 32),
+    repeated blocks long matches (> 64 bytes: the 32-byte-per-round loop).  Every
+    call's {res, status, srcLen, destLen} and the output against the oracle's
+    DecodeToBuf loop on the same input (encoder: liblzma, FORMAT_ALONE)."""
+    orc = native.oracle()
+    rng = random.Random(20261017)
+    bad = []
+    for k in range(16):
+        n = rng.choice([20000, 60000, 120000])
+        parts, size = [], 0
+        while size < n:
+            kind = rng.choice(["text", "runs", "random", "repeat"])
+            m = rng.randrange(64, 6000)
+            if kind == "repeat" and parts:
+                src = b"".join(parts)
+                a = rng.randrange(max(1, len(src) - 300))
+                p = src[a:a + rng.randrange(65, 300)]
+            else:
+                p = native.gen("text" if kind == "repeat" else kind, rng.randrange(1 << 30), m)
+            parts.append(p)
+            size += len(p)
+        data = b"".join(parts)[:n]
+        lc, lp, pb = rng.choice([(3, 0, 2), (0, 0, 0), (1, 1, 1), (4, 0, 0), (0, 2, 2)])
+        enc = lzma.compress(data, format=lzma.FORMAT_ALONE,
+                            filters=[{"id": lzma.FILTER_LZMA1, "dict_size": 4096,
+                                      "lc": lc, "lp": lp, "pb": pb}])
+        props, src = enc[:5], enc[13:]
+        in_chunk = rng.choice([1 << 20, 4096, 333])
+        out_chunk = rng.choice([1 << 20, 5000, 777])
+        # FINISH_END only where one call may reach the end: with smaller output
+        # chunks it applies at every chunk end (LzmaDec.c:857-861) and stops
+        # the loop at the first match that crosses one
+        fin = rng.randrange(2) if out_chunk >= n else 0
+        want = native.stream_decode(orc, "orc", src, props, n, in_chunk, out_chunk, fin)
+        got = L.stream_decode(src, props, n, in_chunk, out_chunk, fin)
+        assert want[2] == data, (k, want[1][-1])
+        if got != want:
+            bad.append((k, (lc, lp, pb), in_chunk, out_chunk, got[0], want[0], got[1][:2],
+                        want[1][:2], got[2] == want[2]))
+    assert not bad, bad[:4]
+
+
 def test_golden_lzma2_one_call(L):
     d = G.load()
     bad = []
