@@ -215,11 +215,6 @@ constexpr uint32_t kIlvLaneCells = 1u;
 #ifndef LZGPU_PROF
 #define LZGPU_PROF 0
 #endif
-// LZGPU_SPEC_UST (A/B): the cooperative literal stage's probability updates
-// stored by every lane (uniform cells and values) instead of by the winner lane
-#ifndef LZGPU_SPEC_UST
-#define LZGPU_SPEC_UST 0
-#endif
 
 // Per-lane decoder state (CLzmaDec fields, LzmaDec.h:50-69).  lo = the LDS
 // table (pointer type Lo: lds_u16*; or gu16* aliasing gl when everything is
@@ -305,11 +300,29 @@ __device__ __attribute__((aligned(16))) uint32_t g_lz_zero_word[4] = {0, 0, 0, 0
 #endif
 
 
+// Wave-uniform branch conditions (readers with Uni = true): every active lane
+// of the wave holds the same reader -- the wave-cooperative kernel
+// (LZGPU_COOP_UNI) or a one-lane wave (LZGPU_ONE_UNI) -- so a condition is
+// taken as a ballot and the compiler branches on it (s_cbranch_vccz) instead of
+// saving, masking and restoring EXEC around the branch.
+template <bool Uni>
+__device__ __forceinline__ bool lz_uc(bool c) {
+#ifdef LZGPU_HOST_EMU
+  return c;
+#else
+  if constexpr (Uni)
+    return __builtin_amdgcn_ballot_w64(c) != 0;
+  else
+    return c;
+#endif
+}
+
 // Same contract, 16-byte refills: `win` holds up to 8 bytes; `nxt` is the
 // next 16-byte aligned block (its low half is taken when win empties, the high
 // half 8 bytes later, and only then is the following block requested), so one
 // load and one drain per 16 input bytes.
-struct GlobalReader16 {
+template <bool Uni>
+struct GlobalReader16T {
   const gu32* wp;  // next 16-byte block to prefetch (as words)
   uint32_t left;   // 16-byte blocks with a valid byte still to prefetch
   uint32_t nb;     // valid bytes in win
@@ -363,7 +376,7 @@ struct GlobalReader16 {
 #if LZGPU_PROF && !defined(LZGPU_HOST_EMU)
     const uint64_t t0 = __builtin_amdgcn_s_memtime();
 #endif
-    if (half == 0) {
+    if (lz_uc<Uni>(half == 0)) {
       win = nlo;
       half = 1;
     } else {
@@ -378,20 +391,22 @@ struct GlobalReader16 {
 #endif
   }
   __device__ __forceinline__ void advance(bool n) {
-    if (n) {
+    if (lz_uc<Uni>(n)) {
       win >>= 8;
       --nb;
-      if (nb == 0) refill();
+      if (lz_uc<Uni>(nb == 0)) refill();
     }
   }
   __device__ __forceinline__ uint32_t next() {
     const uint32_t b = peek();
     win >>= 8;
     --nb;
-    if (nb == 0) refill();
+    if (lz_uc<Uni>(nb == 0)) refill();
     return b;
   }
 };
+typedef GlobalReader16T<false> GlobalReader16;
+typedef GlobalReader16T<true> GlobalReader16U;
 
 // Checkpoint reader: NORMALIZE takes its byte from `win` without a refill
 // check (take_u), and the decoder tops the window up at checkpoints where a
@@ -401,20 +416,6 @@ struct GlobalReader16 {
 // is already loaded (nlo:nhi) when the current one runs out, and only then is
 // the one after requested.  Same contract as GlobalReader16 otherwise:
 // used() = bytes consumed, never loads a block wholly outside [p, p+avail).
-// Uni (the wave-cooperative kernel, LZGPU_COOP_UNI): every lane holds the same
-// reader, so its branch conditions are taken wave-uniform (a ballot: the
-// compiler then branches on SCC instead of saving and restoring EXEC).
-template <bool Uni>
-__device__ __forceinline__ bool lz_uc(bool c) {
-#ifdef LZGPU_HOST_EMU
-  return c;
-#else
-  if constexpr (Uni)
-    return __builtin_amdgcn_ballot_w64(c) != 0;
-  else
-    return c;
-#endif
-}
 template <bool Uni>
 struct GlobalReaderQT {
 #ifdef LZGPU_HOST_EMU
@@ -511,7 +512,7 @@ typedef GlobalReaderQT<true> GlobalReaderQU;
 template <class Rd>
 constexpr bool kIsQ = __is_same(Rd, GlobalReaderQ) || __is_same(Rd, GlobalReaderQU);
 template <class Rd>
-constexpr bool kUniRd = __is_same(Rd, GlobalReaderQU);
+constexpr bool kUniRd = __is_same(Rd, GlobalReaderQU) || __is_same(Rd, GlobalReader16U);
 #ifndef LZGPU_COOP_UNI
 #define LZGPU_COOP_UNI 0
 #endif
@@ -544,6 +545,13 @@ struct BulkReaderFor<LZGPU_LDS_MASK | kIlvBit> {
 template <>
 struct BulkReaderFor<LZGPU_LDS_MASK_LAT | kCoopBit> {
   typedef CoopReader type;
+};
+// Bit 28: the latency placement's one-lane-wave instantiation (LZGPU_ONE_UNI):
+// the wave has one active lane, so its reader branches wave-uniform.
+constexpr uint32_t kOneBit = 0x10000000u;
+template <>
+struct BulkReaderFor<LZGPU_LDS_MASK_LAT | kOneBit> {
+  typedef GlobalReader16U type;
 };
 // every section in LDS (cooperative classes with few streams per CU)
 #ifndef LZGPU_LDS_MASK_ALL
@@ -905,30 +913,23 @@ __device__ __forceinline__ uint32_t spec_stage(Rc<Rd>& rc, P probs, uint32_t m0)
   const uint64_t hits = __builtin_amdgcn_ballot_w64(o.ok);
   const uint32_t wl = uint32_t(__builtin_ctzll(hits));  // wave-uniform winner lane
   w = wl & (kPaths - 1u);
-  const bool mine = lz_lane_id() == wl;
   o.range = uint32_t(__builtin_amdgcn_readlane(int(o.range), int(wl)));
   o.code = uint32_t(__builtin_amdgcn_readlane(int(o.code), int(wl)));
   o.nb = uint32_t(__builtin_amdgcn_readlane(int(o.nb), int(wl)));
   const uint32_t wlo = uint32_t(__builtin_amdgcn_readlane(int(uint32_t(o.win)), int(wl)));
   const uint32_t whi = uint32_t(__builtin_amdgcn_readlane(int(uint32_t(o.win >> 32)), int(wl)));
   o.win = uint64_t(wlo) | (uint64_t(whi) << 32);
-#if LZGPU_SPEC_UST
   // every lane stores the winner's updates (wave-uniform cells and values):
-  // no exec-mask region around the stores
-  (void)mine;
+  // no exec-mask region around the stores (round 3: config 4 -2.2 % time
+  // against the winner lane storing alone)
 #pragma unroll
   for (int k = 0; k < L; ++k)
     probs[(m0 << k) | (w >> (L - k))] =
         uint16_t(__builtin_amdgcn_readlane(int(o.np[k]), int(wl)));
-  if (false)
-#else
-  if (mine)
 #endif
+#ifdef LZGPU_HOST_EMU
+  for (int k = 0; k < L; ++k) probs[(m0 << k) | (w >> (L - k))] = uint16_t(o.np[k]);
 #endif
-  {
-#pragma unroll
-    for (int k = 0; k < L; ++k) probs[(m0 << k) | (w >> (L - k))] = uint16_t(o.np[k]);
-  }
   rc.range = o.range;
   rc.code = o.code;
   rc.rd->win = o.win;
@@ -1006,52 +1007,21 @@ __device__ __forceinline__ void stu_tail(gbyte* d, uint64_t v, uint32_t rem) {
   if (rem & 1) lz_put(d, uint32_t(v));
 }
 
-// WantMb (the kernels that keep the next matched byte in a register): `mb`
-// gets the byte at distance dist from pos + n -- the next matched literal's
-// -- where the copy's own loads already hold it (mb_ok), so the caller does
-// not reload it behind the copy's stores (a load's data waits for every
-// older store in the in-order vmcnt queue: ~600-950 cycles against ~200 for
-// an L2 hit).  Short non-overlapping matches (dist > n, n <= 15: most of
-// them) load both 8-byte halves before either store.
-// `mid` runs after the copy's loads and before its stores on the short path
-// (before everything on the others): the deferred probability stores of the
-// match path go there.
+// `mid` runs before the copy's first store: the deferred probability stores
+// of the match path (LZGPU_DEFER) go there.
 struct LzNoop {
   __device__ __forceinline__ void operator()() const {}
 };
-template <bool WantMb = false, class Mid = LzNoop>
+template <class Mid = LzNoop>
 __device__ __forceinline__ uint32_t lz_copy(gbyte* dic, uint64_t pos, uint64_t from, uint32_t n,
-                                            uint32_t dist, uint64_t cap, uint32_t* mb = nullptr,
-                                            bool* mb_ok = nullptr, Mid mid = Mid()) {
+                                            uint32_t dist, uint64_t cap, Mid mid = Mid()) {
   uint32_t last = 0;
-  if constexpr (WantMb) *mb_ok = false;
   if (from + n <= cap && from < pos) {
     // source span does not wrap (always so for a flat LzmaDecode window)
     gbyte* d = dic + pos;
     const gbyte* src = dic + from;
     uint64_t v = 0;
     uint32_t i = 0;
-    if constexpr (WantMb) {
-      if (dist > n && n <= 15 && from + 16 <= cap) {
-        // bytes 0..n of the source lie below pos (n < dist): the words may
-        // also cover bytes at or past pos, which are never used
-        const uint64_t c0 = ldu64(src);
-        const uint64_t c1 = ldu64(src + 8);  // unconditional: no branch around a load
-        mid();
-        if (n >= 8) {
-          stu64(d, c0);
-          if (n > 8) stu_tail(d + 8, c1, n - 8);
-        } else {
-          stu_tail(d, c0, n);
-        }
-        auto byte_at = [&](uint32_t k) -> uint32_t {
-          return uint32_t((k < 8 ? c0 >> (8 * k) : c1 >> (8 * (k - 8)))) & 0xFFu;
-        };
-        *mb = byte_at(n);
-        *mb_ok = true;
-        return byte_at(n - 1);
-      }
-    }
     mid();
     if (dist >= 8) {
       // src[i..i+8) lies below d + i: written before this step reads it
@@ -1087,11 +1057,6 @@ __device__ __forceinline__ uint32_t lz_copy(gbyte* dic, uint64_t pos, uint64_t f
           stu64(d + i, v);
         else
           stu_tail(d + i, v, rem);
-        if constexpr (WantMb) {
-          // v byte k = pattern byte i + k; pattern byte i + 8 = v byte t
-          *mb = uint32_t(v >> (8 * (rem == 8 ? t : rem))) & 0xFFu;
-          *mb_ok = true;
-        }
         return uint32_t(v >> (8 * (rem - 1))) & 0xFFu;
       }
       stu64(d + i, v);
@@ -1448,17 +1413,10 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
             // in one load batch
             prev = lz_copy_coop(dic, pos, ring_back(pos, r0, cap), 1, r0, cap, mb_pf);
             pos++;
-          } else if constexpr (mb_pf_on<M>()) {
-            // the byte and the next matched byte (at pos + 1 - rep0: the byte
-            // after it, or for rep0 = 1 the byte itself) loaded before the store
-            const uint64_t f = ring_back(pos, r0, cap);
-            prev = dic[f];
-            const uint32_t nxt = dic[f + 1 == cap ? 0 : f + 1];
-            lz_put(dic + pos++, prev);
-            mb_pf = r0 > 1 ? nxt : prev;
           } else {
             prev = dic[ring_back(pos, r0, cap)];
             lz_put(dic + pos++, prev);
+            if constexpr (mb_pf_on<M>()) mb_pf = dic[ring_back(pos, r0, cap)];
           }
           total++;
           st = (st < 7) ? 9 : 11;
@@ -1668,17 +1626,13 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
       if constexpr ((M & kCoopBit) != 0u) {
         prev = lz_copy_coop(dic, pos, from, n, r0, cap, mb_pf);
         pos += n;
-      } else if constexpr (mb_pf_on<M>()) {
-        bool mb_ok;
-        if constexpr (defer_on<M>())
-          prev = lz_copy<true>(dic, pos, from, n, r0, cap, &mb_pf, &mb_ok, [&]() { pd.flush(); });
-        else
-          prev = lz_copy<true>(dic, pos, from, n, r0, cap, &mb_pf, &mb_ok);
-        pos += n;
-        if (!mb_ok) mb_pf = dic[ring_back(pos, r0, cap)];
       } else {
-        prev = lz_copy(dic, pos, from, n, r0, cap);
+        if constexpr (defer_on<M>())
+          prev = lz_copy(dic, pos, from, n, r0, cap, [&]() { pd.flush(); });
+        else
+          prev = lz_copy(dic, pos, from, n, r0, cap);
         pos += n;
+        if constexpr (mb_pf_on<M>()) mb_pf = dic[ring_back(pos, r0, cap)];
       }
     }
     LZ_PROF_MARK(s, 2, t_prof);

@@ -43,6 +43,8 @@ EMU_VARIANTS = {
     "deferred_stores_interleaved": "-DLZGPU_DEFER=1 -DEMU_ILV",
     # the cooperative kernel's reader and decisions with wave-uniform branches
     "coop_uniform_branches": "-DLZGPU_COOP_UNI=1 -DEMU_COOP_ALL",
+    # the latency placement's one-lane-wave instantiation (LZGPU_ONE_UNI)
+    "one_lane_uniform_branches": "-DEMU_ONE_LANE",
 }
 
 
