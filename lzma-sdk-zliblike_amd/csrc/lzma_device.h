@@ -201,7 +201,11 @@ constexpr uint32_t kIlvLaneCells = 1u;
 // matched literals, literal write-combining, byte-wise and batched-tail copies,
 // threshold / divergent batch exits, nontemporal input / output, pair-
 // interleaved rows, ...) were removed in round 3; their A/B evidence stays in
-// DESIGN.md §4 and profiles/.  The kept shapes are unconditional: decision and
+// DESIGN.md §4 and profiles/.  So were round 3's own rejects: the throughput
+// copy taking the next matched byte from its own loads, deferred probability
+// stores in the throughput match path, wave-uniform (ballot) branches in the
+// cooperative and one-lane kernels (profiles/r03_storeack/).  The kept shapes
+// are unconditional: decision and
 // update as selects in the shared form, the checkpoint reader in the bulk pass
 // of the throughput and cooperative placements (the 16-byte per-byte-checked
 // reader elsewhere), the matched byte prefetched at match end (throughput and
@@ -300,29 +304,11 @@ __device__ __attribute__((aligned(16))) uint32_t g_lz_zero_word[4] = {0, 0, 0, 0
 #endif
 
 
-// Wave-uniform branch conditions (readers with Uni = true): every active lane
-// of the wave holds the same reader -- the wave-cooperative kernel
-// (LZGPU_COOP_UNI) or a one-lane wave (LZGPU_ONE_UNI) -- so a condition is
-// taken as a ballot and the compiler branches on it (s_cbranch_vccz) instead of
-// saving, masking and restoring EXEC around the branch.
-template <bool Uni>
-__device__ __forceinline__ bool lz_uc(bool c) {
-#ifdef LZGPU_HOST_EMU
-  return c;
-#else
-  if constexpr (Uni)
-    return __builtin_amdgcn_ballot_w64(c) != 0;
-  else
-    return c;
-#endif
-}
-
 // Same contract, 16-byte refills: `win` holds up to 8 bytes; `nxt` is the
 // next 16-byte aligned block (its low half is taken when win empties, the high
 // half 8 bytes later, and only then is the following block requested), so one
 // load and one drain per 16 input bytes.
-template <bool Uni>
-struct GlobalReader16T {
+struct GlobalReader16 {
   const gu32* wp;  // next 16-byte block to prefetch (as words)
   uint32_t left;   // 16-byte blocks with a valid byte still to prefetch
   uint32_t nb;     // valid bytes in win
@@ -376,7 +362,7 @@ struct GlobalReader16T {
 #if LZGPU_PROF && !defined(LZGPU_HOST_EMU)
     const uint64_t t0 = __builtin_amdgcn_s_memtime();
 #endif
-    if (lz_uc<Uni>(half == 0)) {
+    if (half == 0) {
       win = nlo;
       half = 1;
     } else {
@@ -391,22 +377,20 @@ struct GlobalReader16T {
 #endif
   }
   __device__ __forceinline__ void advance(bool n) {
-    if (lz_uc<Uni>(n)) {
+    if (n) {
       win >>= 8;
       --nb;
-      if (lz_uc<Uni>(nb == 0)) refill();
+      if (nb == 0) refill();
     }
   }
   __device__ __forceinline__ uint32_t next() {
     const uint32_t b = peek();
     win >>= 8;
     --nb;
-    if (lz_uc<Uni>(nb == 0)) refill();
+    if (nb == 0) refill();
     return b;
   }
 };
-typedef GlobalReader16T<false> GlobalReader16;
-typedef GlobalReader16T<true> GlobalReader16U;
 
 // Checkpoint reader: NORMALIZE takes its byte from `win` without a refill
 // check (take_u), and the decoder tops the window up at checkpoints where a
@@ -416,8 +400,7 @@ typedef GlobalReader16T<true> GlobalReader16U;
 // is already loaded (nlo:nhi) when the current one runs out, and only then is
 // the one after requested.  Same contract as GlobalReader16 otherwise:
 // used() = bytes consumed, never loads a block wholly outside [p, p+avail).
-template <bool Uni>
-struct GlobalReaderQT {
+struct GlobalReaderQ {
 #ifdef LZGPU_HOST_EMU
   struct u32x4 { uint32_t x, y, z, w; };
 #else
@@ -451,8 +434,7 @@ struct GlobalReaderQT {
   __device__ __forceinline__ void pop_word() {
     blo = (blo >> 32) | (bhi << 32);
     bhi >>= 32;
-    --bw;
-    if (lz_uc<Uni>(bw == 0)) {
+    if (--bw == 0) {
       blo = uint64_t(nx.x) | (uint64_t(nx.y) << 32);
       bhi = uint64_t(nx.z) | (uint64_t(nx.w) << 32);
       bw = 4;
@@ -480,7 +462,7 @@ struct GlobalReaderQT {
   }
   __device__ __forceinline__ uint32_t used() const { return taken - nb; }
   __device__ __forceinline__ void topup() {
-    if (lz_uc<Uni>(nb <= 4)) {
+    if (nb <= 4) {
       win |= uint64_t(uint32_t(blo)) << (8 * nb);
       nb += 4;
       taken += 4;
@@ -496,31 +478,19 @@ struct GlobalReaderQT {
     return b;
   }
   __device__ __forceinline__ uint32_t next() {
-    if (lz_uc<Uni>(nb == 0)) topup();
+    if (nb == 0) topup();
     return take_u();
   }
   __device__ __forceinline__ void advance(bool n) {
-    if (lz_uc<Uni>(n)) {
+    if (n) {
       win >>= 8;
       --nb;
-      if (lz_uc<Uni>(nb == 0)) topup();
+      if (nb == 0) topup();
     }
   }
 };
-typedef GlobalReaderQT<false> GlobalReaderQ;
-typedef GlobalReaderQT<true> GlobalReaderQU;
 template <class Rd>
-constexpr bool kIsQ = __is_same(Rd, GlobalReaderQ) || __is_same(Rd, GlobalReaderQU);
-template <class Rd>
-constexpr bool kUniRd = __is_same(Rd, GlobalReaderQU) || __is_same(Rd, GlobalReader16U);
-#ifndef LZGPU_COOP_UNI
-#define LZGPU_COOP_UNI 0
-#endif
-#if LZGPU_COOP_UNI
-typedef GlobalReaderQU CoopReader;
-#else
-typedef GlobalReaderQ CoopReader;
-#endif
+constexpr bool kIsQ = __is_same(Rd, GlobalReaderQ);
 
 typedef GlobalReader16 PlainReader;
 // Reader of the bulk pass per placement: the checkpoint reader for the
@@ -544,14 +514,7 @@ struct BulkReaderFor<LZGPU_LDS_MASK | kIlvBit> {
 };
 template <>
 struct BulkReaderFor<LZGPU_LDS_MASK_LAT | kCoopBit> {
-  typedef CoopReader type;
-};
-// Bit 28: the latency placement's one-lane-wave instantiation (LZGPU_ONE_UNI):
-// the wave has one active lane, so its reader branches wave-uniform.
-constexpr uint32_t kOneBit = 0x10000000u;
-template <>
-struct BulkReaderFor<LZGPU_LDS_MASK_LAT | kOneBit> {
-  typedef GlobalReader16U type;
+  typedef GlobalReaderQ type;
 };
 // every section in LDS (cooperative classes with few streams per CU)
 #ifndef LZGPU_LDS_MASK_ALL
@@ -559,7 +522,7 @@ struct BulkReaderFor<LZGPU_LDS_MASK_LAT | kOneBit> {
 #endif
 template <>
 struct BulkReaderFor<LZGPU_LDS_MASK_ALL | kCoopBit> {
-  typedef CoopReader type;
+  typedef GlobalReaderQ type;
 };
 
 // Matched-byte prefetch per placement: the byte at rep0 is loaded at match end in
@@ -599,57 +562,20 @@ struct LocalReader {
 
 // ------------------------------------------------------------------ range decoder
 
-// Deferred probability stores (Rc::sub3d): three pending (cell, value) pairs,
-// always three stores per flush (unused slots write a cell no decision reads,
-// the Align tree's cell 0), so the number of vector-memory operations between
-// a batch's loads and their use is the same on every path and the compiler's
-// vmcnt waits stay exact.
-__device__ __forceinline__ gu16* cell_addr(gu16* p) { return p; }
-__device__ __forceinline__ gu16* cell_addr(GS p) { return p.p; }
-struct Pend3 {
-  gu16* a0;
-  gu16* a1;
-  gu16* a2;
-  uint32_t v0, v1, v2;
-  __device__ __forceinline__ void clear(gu16* dummy) {
-    a0 = a1 = a2 = dummy;
-    v0 = v1 = v2 = 0;
-  }
-  __device__ __forceinline__ void set(gu16* x0, uint32_t w0, gu16* x1, uint32_t w1, gu16* x2,
-                                      uint32_t w2) {
-    a0 = x0; v0 = w0;
-    a1 = x1; v1 = w1;
-    a2 = x2; v2 = w2;
-  }
-  __device__ __forceinline__ void flush() {
-    *a0 = uint16_t(v0);
-    *a1 = uint16_t(v1);
-    *a2 = uint16_t(v2);
-  }
-};
-#ifndef LZGPU_DEFER
-#define LZGPU_DEFER 0
-#endif
-// deferred stores in the throughput placement's global match path
-template <uint32_t M>
-__host__ __device__ constexpr bool defer_on() {
-  return LZGPU_DEFER != 0 && (M & ~kIlvBit) == LZGPU_LDS_MASK;
-}
-
 template <class Rd>
 struct Rc {
   uint32_t range, code;
   Rd* rd;
   // NORMALIZE (LzmaDec.c:17): shift in one input byte when range < 2^24
   __device__ __forceinline__ void norm() {
-    if (lz_uc<kUniRd<Rd>>(range < kTop)) {
+    if (range < kTop) {
       range <<= 8;
       code = (code << 8) | rd->next();
     }
   }
   // NORMALIZE after a reader checkpoint: the byte is known to be in the window
   __device__ __forceinline__ void norm_u() {
-    if (lz_uc<kUniRd<Rd>>(range < kTop)) {
+    if (range < kTop) {
       range <<= 8;
       code = (code << 8) | rd_take_u(*rd);
     }
@@ -665,7 +591,7 @@ struct Rc {
     *prob = uint16_t(int32_t(p) - ((int32_t(p) - m) >> 5));
     range = b ? range - bound : bound;
     code = b ? code - bound : code;
-    return lz_uc<kUniRd<Rd>>(b) ? 1u : 0u;
+    return b ? 1u : 0u;
   }
   // decision on a preloaded value p with norm_u
   template <class P>
@@ -677,7 +603,7 @@ struct Rc {
     *prob = uint16_t(int32_t(p) - ((int32_t(p) - m) >> 5));
     range = b ? range - bound : bound;
     code = b ? code - bound : code;
-    return lz_uc<kUniRd<Rd>>(b) ? 1u : 0u;
+    return b ? 1u : 0u;
   }
   // BITS levels of an MSB-first tree from node m (no refill checks: at most
   // 5 levels after a checkpoint); returns the node reached
@@ -701,7 +627,7 @@ struct Rc {
     *prob = uint16_t(int32_t(p) - ((int32_t(p) - m) >> 5));
     range = b ? range - bound : bound;
     code = b ? code - bound : code;
-    return lz_uc<kUniRd<Rd>>(b) ? 1u : 0u;
+    return b ? 1u : 0u;
   }
   // decision on an already-loaded probability value p, update stored to *prob
   template <class P>
@@ -713,7 +639,7 @@ struct Rc {
     *prob = uint16_t(int32_t(p) - ((int32_t(p) - m) >> 5));
     range = b ? range - bound : bound;
     code = b ? code - bound : code;
-    return lz_uc<kUniRd<Rd>>(b) ? 1u : 0u;
+    return b ? 1u : 0u;
   }
   // MSB-first bit tree of BITS levels (TREE_DECODE); returns [0, 1 << BITS)
   template <int BITS, class P>
@@ -791,39 +717,6 @@ struct Rc {
     const uint32_t p2 = b0 ? (b1 ? c[6] : c[5]) : (b1 ? c[4] : c[3]);
     const uint32_t b2 = bit_v(p2, probs + m);
     return 2 * m + b2;
-  }
-  // decision on a preloaded value; the update is returned in np, not stored
-  __device__ __forceinline__ uint32_t bit_vn(uint32_t p, uint32_t& np) {
-    norm();
-    const uint32_t bound = (range >> 11) * p;
-    const bool b = code >= bound;
-    const int32_t m = b ? 0 : int32_t(kProbOne - 31);
-    np = uint32_t(int32_t(p) - ((int32_t(p) - m) >> 5));
-    range = b ? range - bound : bound;
-    code = b ? code - bound : code;
-    return lz_uc<kUniRd<Rd>>(b) ? 1u : 0u;
-  }
-  // sub3 with deferred stores (global trees of the throughput kernel): the
-  // seven loads issue first, then (Flush) the previous batch's three pending
-  // updates are stored, and this batch's three updates become pending -- so
-  // the next batch's loads do not wait behind them in the in-order vmcnt
-  // queue.  The caller keeps every pending cell out of the next batch.
-  template <bool Flush, class P>
-  __device__ __forceinline__ uint32_t sub3d(P probs, uint32_t root, Pend3& pd) {
-    const uint32_t r2 = root * 2, r4 = root * 4;
-    const uint32_t c0 = probs[root], c10 = probs[r2], c11 = probs[r2 + 1];
-    const uint32_t c20 = probs[r4], c21 = probs[r4 + 1], c22 = probs[r4 + 2],
-                   c23 = probs[r4 + 3];
-    if constexpr (Flush) pd.flush();
-    uint32_t n0, n1, n2;
-    const uint32_t b0 = bit_vn(c0, n0);
-    uint32_t m = r2 + b0;
-    const uint32_t b1 = bit_vn(b0 ? c11 : c10, n1);
-    const uint32_t m1 = 2 * m + b1;
-    const uint32_t p2 = b0 ? (b1 ? c23 : c22) : (b1 ? c21 : c20);
-    const uint32_t b2 = bit_vn(p2, n2);
-    pd.set(cell_addr(probs + root), n0, cell_addr(probs + m), n1, cell_addr(probs + m1), n2);
-    return 2 * m1 + b2;
   }
   // 8-level tree in global memory in three load batches (3 + 3 + 2 levels)
   // instead of eight dependent round trips; returns the node (256..511).
@@ -1007,14 +900,8 @@ __device__ __forceinline__ void stu_tail(gbyte* d, uint64_t v, uint32_t rem) {
   if (rem & 1) lz_put(d, uint32_t(v));
 }
 
-// `mid` runs before the copy's first store: the deferred probability stores
-// of the match path (LZGPU_DEFER) go there.
-struct LzNoop {
-  __device__ __forceinline__ void operator()() const {}
-};
-template <class Mid = LzNoop>
 __device__ __forceinline__ uint32_t lz_copy(gbyte* dic, uint64_t pos, uint64_t from, uint32_t n,
-                                            uint32_t dist, uint64_t cap, Mid mid = Mid()) {
+                                            uint32_t dist, uint64_t cap) {
   uint32_t last = 0;
   if (from + n <= cap && from < pos) {
     // source span does not wrap (always so for a flat LzmaDecode window)
@@ -1022,7 +909,6 @@ __device__ __forceinline__ uint32_t lz_copy(gbyte* dic, uint64_t pos, uint64_t f
     const gbyte* src = dic + from;
     uint64_t v = 0;
     uint32_t i = 0;
-    mid();
     if (dist >= 8) {
       // src[i..i+8) lies below d + i: written before this step reads it
       for (; i + 8 <= n; i += 8) {
@@ -1063,7 +949,6 @@ __device__ __forceinline__ uint32_t lz_copy(gbyte* dic, uint64_t pos, uint64_t f
       v = (v >> (8 * t)) | (v << (8 * (dist - t)));
     }
   }
-  mid();  // (the paths above all return)
   if (from + n <= cap) {
     gbyte* d = dic + pos;
     const gbyte* s = dic + from;
@@ -1399,8 +1284,6 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
 #endif
     const uint64_t tm0 = lz_clock();
 #endif
-    [[maybe_unused]] Pend3 pd;
-    if constexpr (defer_on<M>()) pd.clear(cell_addr(T.template at<S_ALIGN>(0)));
     if (!rc.bit(T.template at<S_REP>(st))) {
       st += 12;
       lcoder_is_rep = 0;
@@ -1474,21 +1357,12 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
         } else {
         const uint32_t ch = lbase[0];
         auto lo_t = lbase + 2 + (ps << 3);
-        if constexpr (defer_on<M>()) {
-          if (!rc.bit_v(ch, lbase))
-            len = rc.template sub3d<false>(lo_t, 1, pd) - 8;
-          else if (!rc.bit(lbase + 1))
-            len = 8 + rc.template sub3d<false>(lbase + 2 + (8u << pb) + (ps << 3), 1, pd) - 8;
-          else
-            len = 16 + rc.template tree<8>(T.template at<S_LENHI>(lcoder_is_rep << 8));
-        } else {
         if (!rc.bit_v(ch, lbase))
           len = rc.sub3(lo_t, 1) - 8;
         else if (!rc.bit(lbase + 1))
           len = 8 + rc.sub3(lbase + 2 + (8u << pb) + (ps << 3), 1) - 8;
         else
           len = 16 + rc.template tree<8>(T.template at<S_LENHI>(lcoder_is_rep << 8));
-        }
         }
       } else {
         if (!rc.bit(lbase))
@@ -1509,9 +1383,6 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
       uint32_t dist;
       if constexpr (((M >> S_SLOT) & 1u) == 0u) {
         auto sl_t = T.template at<S_SLOT>(lstate << 6);
-        if constexpr (defer_on<M>()) {
-          dist = rc.template sub3d<true>(sl_t, rc.template sub3d<true>(sl_t, 1, pd), pd) - 64;
-        } else {
 #if LZGPU_PROF == 1 && !defined(LZGPU_HOST_EMU)
         // one global round trip + 3 decisions, timed (profiling builds)
         const uint64_t t0 = lz_clock();
@@ -1524,7 +1395,6 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
 #else
         dist = rc.sub3(sl_t, rc.sub3(sl_t, 1)) - 64;
 #endif
-        }
       } else {
         dist = rc.template tree<6>(T.template at<S_SLOT>(lstate << 6));
       }
@@ -1539,10 +1409,7 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
           if constexpr (((M >> S_SPEC) & 1u) == 0u) {
             if (nbits >= 3) {
               // first three reverse-tree bits in one load batch
-              if constexpr (defer_on<M>())
-                node = rc.template sub3d<true>(T.template at<S_SPEC>(sp), 1, pd);
-              else
-                node = rc.sub3(T.template at<S_SPEC>(sp), 1);
+              node = rc.sub3(T.template at<S_SPEC>(sp), 1);
               dist |= ((node >> 2) & 1u) | (((node >> 1) & 1u) << 1) | ((node & 1u) << 2);
               mask = 8;
               nbits -= 3;
@@ -1573,10 +1440,7 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
               dist |= ((node >> 3) & 1u) | (((node >> 2) & 1u) << 1) |
                       (((node >> 1) & 1u) << 2) | ((node & 1u) << 3);
             } else {
-              if constexpr (defer_on<M>())
-                node = rc.template sub3d<true>(T.template at<S_ALIGN>(0), 1, pd);
-              else
-                node = rc.sub3(T.template at<S_ALIGN>(0), 1);
+              node = rc.sub3(T.template at<S_ALIGN>(0), 1);
               dist |= ((node >> 2) & 1u) | (((node >> 1) & 1u) << 1) | ((node & 1u) << 2);
               const uint32_t b = rc.bit(T.template at<S_ALIGN>(node));
               dist |= b << 3;
@@ -1590,7 +1454,6 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
             }
           }
           if (dist == 0xFFFFFFFFu) {
-            if constexpr (defer_on<M>()) pd.flush();
             len += kLenDone;
             st -= 12;
             break;
@@ -1601,10 +1464,7 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
       r2 = r1;
       r1 = r0;
       r0 = dist + 1;
-      if (full == 0 ? dist >= total : dist >= full) {
-        if constexpr (defer_on<M>()) pd.flush();
-        return kErrData;
-      }
+      if (full == 0 ? dist >= total : dist >= full) return kErrData;
       st = (st < 19) ? 7 : 10;
 #if LZGPU_PROF == 1 && !defined(LZGPU_HOST_EMU)
       s.prof[10] += lz_clock() - tm2;
@@ -1613,10 +1473,7 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
     }
     len += 2;
     LZ_PROF_MARK(s, 1, t_prof);
-    if (limit == pos) {
-      if constexpr (defer_on<M>()) pd.flush();
-      return kErrData;
-    }
+    if (limit == pos) return kErrData;
     {
       const uint64_t room = limit - pos;
       const uint32_t n = (room < len) ? uint32_t(room) : len;
@@ -1627,10 +1484,7 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
         prev = lz_copy_coop(dic, pos, from, n, r0, cap, mb_pf);
         pos += n;
       } else {
-        if constexpr (defer_on<M>())
-          prev = lz_copy(dic, pos, from, n, r0, cap, [&]() { pd.flush(); });
-        else
-          prev = lz_copy(dic, pos, from, n, r0, cap);
+        prev = lz_copy(dic, pos, from, n, r0, cap);
         pos += n;
         if constexpr (mb_pf_on<M>()) mb_pf = dic[ring_back(pos, r0, cap)];
       }

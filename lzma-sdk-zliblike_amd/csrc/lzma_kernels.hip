@@ -297,17 +297,6 @@ static int launch_class(const LzmaGpuStreamDesc* d_descs, const uint32_t* d_orde
     return launch_coop<4, MC, K2>(d_descs, d_order, n, d_src, d_dst, d_ws, d_results, stride,
                                   groups_per_cu, max_groups, d_queue, stream);
   }
-#ifndef LZGPU_ONE_UNI
-#define LZGPU_ONE_UNI 0
-#endif
-#if LZGPU_ONE_UNI
-  // one-lane waves: the instantiation whose reader branches wave-uniform
-  if (lds_mask == LZGPU_LDS_MASK_LAT && lanes == 1)
-    return launch_lds_w<LZGPU_LDS_MASK_LAT | kOneBit, K2>(d_descs, d_order, n, d_src, d_dst,
-                                                          d_ws, d_results, lanes, stride,
-                                                          waves_per_simd, groups_per_cu,
-                                                          max_groups, d_queue, sl, stream);
-#endif
   if (lds_mask == LZGPU_LDS_MASK_LAT)
     return launch_lds_w<LZGPU_LDS_MASK_LAT, K2>(d_descs, d_order, n, d_src, d_dst, d_ws,
                                                 d_results, lanes, stride, waves_per_simd,

@@ -17,6 +17,6 @@ for spec in "$@"; do
 import json
 d=json.load(open('$OUT/$tag.json'))
 r=d.get('roofline') or {}; p=d.get('config', {}).get('kernel_plan')
-print('$cfg', '$streams', '[$v]', d['value'], 'MB/s', r.get('kernel_avg_ms', d.get('ms_per_step')), 'ms', p, d['verified'])" || echo "$tag exit $s"
+print('$cfg', '$streams', '[$v]', d['value'], 'MB/s', r.get('kernel_avg_ms', d.get('ms_per_step')), 'ms', p, d['verified'])" | tee -a "$OUT/summary.log" || echo "$tag exit $s"
   [ $s -eq 0 ] || [ $s -eq 3 ] || exit $s
 done

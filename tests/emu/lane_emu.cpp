@@ -52,10 +52,6 @@ void emu_decode_batch_lds(const LzmaGpuStreamDesc* descs, size_t n, const uint8_
     // their paths one after another here)
     results[i] = lane_decode_lds<LZGPU_LDS_MASK_LAT | kCoopBit>(descs[i], src, dst, ws, slab,
                                                                 stride);
-#elif defined(EMU_ONE_LANE)
-    // the latency placement's one-lane-wave instantiation (uniform reader)
-    results[i] = lane_decode_lds<LZGPU_LDS_MASK_LAT | kOneBit>(descs[i], src, dst, ws, slab,
-                                                               stride);
 #elif defined(EMU_LAT_MASK)
     // the latency-placement instantiation (the kernels' second LDS variant)
     results[i] = lane_decode_lds<LZGPU_LDS_MASK_LAT>(descs[i], src, dst, ws, slab, stride);

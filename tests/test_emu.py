@@ -38,13 +38,6 @@ EMU_VARIANTS = {
     "interleaved_global_instantiation": "-DEMU_ILV",
     "coop_instantiation": "-DEMU_COOP",
     "coop_all_lds_instantiation": "-DEMU_COOP_ALL",
-    # deferred probability stores of the throughput placement's match path
-    "deferred_stores": "-DLZGPU_DEFER=1",
-    "deferred_stores_interleaved": "-DLZGPU_DEFER=1 -DEMU_ILV",
-    # the cooperative kernel's reader and decisions with wave-uniform branches
-    "coop_uniform_branches": "-DLZGPU_COOP_UNI=1 -DEMU_COOP_ALL",
-    # the latency placement's one-lane-wave instantiation (LZGPU_ONE_UNI)
-    "one_lane_uniform_branches": "-DEMU_ONE_LANE",
 }
 
 
