@@ -150,11 +150,17 @@ SRes LzmaDecode(Byte *dest, SizeT *destLen, const Byte *src, SizeT *srcLen,
  * dicBufSize and probs allocation, and the current device): a call uploads
  * its input only -- plus, once per mirror, the dictionary history a
  * continuing decoder needs -- and downloads the bytes it decoded, the state
- * and the table.  Bytes of dic the CALLER writes between calls are not seen
- * by the decoder while the mirror lives; LzmaGpu_DecoderRelease(p) drops it
- * (as do LzmaDec_FreeProbs / LzmaDec_Free and any change of dic, dicBufSize
- * or probs), so the next call starts from the host copy.  Mirrors beyond
- * 256 decoders or 16 GiB are evicted least recently used first. */
+ * and the table.  Bytes of dic the CALLER writes between calls are seen when
+ * it moves dicPos / processedPos over them as the reference's LZMA2 walker
+ * does (Lzma2Dec.c:159-166: the call uploads exactly that span); any other
+ * change of the positions, or of the host table, makes the call start from
+ * the host copies.  A caller rewriting bytes it already handed to the decoder
+ * without moving the positions is not detected: LzmaGpu_DecoderRelease(p)
+ * drops the mirror (as do LzmaDec_FreeProbs / LzmaDec_Free and any change of
+ * dic, dicBufSize or probs), so the next call starts from the host copy.  A
+ * decoder used on another device drops its mirrors on the others.  Mirrors
+ * beyond 256 decoders or 16 GiB (LZGPU_MIRROR_BUDGET_MB) are evicted least
+ * recently used first. */
 void LzmaGpu_DecoderRelease(const CLzmaDec *p);
 /* Host<->device bytes moved by the drop-in decode entry points (LzmaDecode,
  * LzmaUncompress, Lzma2Decode, LzmaDec_DecodeToDic / DecodeToBuf and the LZMA2

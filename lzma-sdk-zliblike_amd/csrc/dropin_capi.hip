@@ -22,12 +22,22 @@
 // whole ring loop (LzmaDec.c:840-878) in ONE launch on the device ring and
 // downloads the caller's output once; the host ring is rebuilt from it.
 //
-// The mirror's contract: bytes of `dic` the caller writes between calls (other
-// than through this library) are not seen by the decoder unless `dic`,
-// `dicBufSize` or the probs allocation change, or LzmaGpu_DecoderRelease(p) is
-// called -- the reference reads them (its dictionary IS the caller's buffer).
-// No caller in the reference does that; every decoder-written byte is
-// downloaded, so host and device copies agree.
+// Coherence with a caller that writes `dic` itself (round 4): the reference's
+// dictionary IS the caller's buffer, and its own LZMA2 walker copies stored
+// chunks into it and advances dicPos / processedPos between decoder calls
+// (Lzma2Dec.c:159-166, 234).  Every call therefore compares the decoder's
+// positions on entry with the ones the previous call left behind: equal (or
+// dicPos wrapped from dicBufSize to 0, LzmaDec.c:849) -- nothing to do; both
+// advanced by the same amount -- the host wrote exactly those bytes, which are
+// uploaded (ring-wrapped spans in two pieces); anything else -- the mirror's
+// history is dropped and the whole dictionary is uploaded again when the call
+// reads history.  The table is checked the same way (a 64-bit hash of the host
+// cells against the one recorded after the previous call).  What stays out of
+// reach is a caller rewriting bytes it already handed to the decoder without
+// moving the positions; no caller in the reference does that
+// (INTEGRATION.md §2).  A decoder used on another device drops its mirrors on
+// every other device, so switching devices back and forth never decodes on a
+// stale table or dictionary.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -164,6 +174,12 @@ struct Mirror {
   DevBuf io;     // this call's input (+ DecodeToBuf output)
   bool history = false;    // device dic holds every byte the decoder wrote since its dic init
   bool probs_dev = false;  // device table == host table (downloaded after every call)
+  // what the last successful call left in the host object: positions and a
+  // hash of the table (the coherence check on entry)
+  SizeT end_pos = 0;
+  uint32_t end_total = 0;
+  uint32_t probs_cells = 0;
+  uint64_t probs_hash = 0;
   uint64_t tick = 0;
   std::mutex busy;  // one call at a time per decoder object (the reference's contract)
 };
@@ -186,18 +202,35 @@ size_t probs_area(uint32_t num_probs) { return (size_t(num_probs) * 2 + 255) & ~
 
 // The mirror of decoder p on device dev (created on first use).  A mirror whose
 // dic / dicBufSize / probs allocation no longer match p is reset: its device
-// copies no longer describe p.  Least recently used mirrors nobody is using are
-// evicted beyond kMirrorMaxCount or kMirrorMaxBytes (an evicted decoder's next
-// call rebuilds its mirror: correctness never depends on one existing).
-std::shared_ptr<Mirror> mirror_get(const CLzmaDec* p, int dev) {
+// copies no longer describe p.  p's mirrors on other devices are dropped (the
+// host object moves on without them).  Least recently used mirrors nobody is
+// using are evicted beyond kMirrorMaxCount or the byte budget, counting the
+// `want` bytes this call's block will need (an evicted decoder's next call
+// rebuilds its mirror: correctness never depends on one existing).  Dropped
+// mirrors go to `dead`, released by the caller outside the registry lock.
+size_t mirror_budget() {
+  static const size_t b = [] {
+    const char* e = getenv("LZGPU_MIRROR_BUDGET_MB");
+    const long long mb = e ? atoll(e) : 0;
+    return mb > 0 ? size_t(mb) << 20 : kMirrorMaxBytes;
+  }();
+  return b;
+}
+std::shared_ptr<Mirror> mirror_get(const CLzmaDec* p, int dev, size_t want,
+                                   std::vector<std::shared_ptr<Mirror>>& dead) {
   Registry& R = registry();
   std::lock_guard<std::mutex> g(R.mu);
   std::shared_ptr<Mirror> m;
-  for (auto& e : R.v)
-    if (e->key == p && e->dev == dev) {
-      m = e;
-      break;
+  for (size_t i = 0; i < R.v.size();) {
+    auto& e = R.v[i];
+    if (e->key == p && e->dev != dev) {
+      dead.push_back(std::move(e));
+      R.v.erase(R.v.begin() + ptrdiff_t(i));
+      continue;
     }
+    if (e->key == p) m = e;
+    ++i;
+  }
   if (!m) {
     m = std::make_shared<Mirror>();
     m->key = p;
@@ -215,27 +248,28 @@ std::shared_ptr<Mirror> mirror_get(const CLzmaDec* p, int dev) {
   }
   m->tick = ++R.tick;
   // eviction: oldest idle mirrors first
-  size_t bytes = 0;
+  size_t bytes = want > m->block.cap ? want - m->block.cap : 0;
   for (auto& e : R.v) bytes += e->block.cap + e->io.cap;
-  while (R.v.size() > kMirrorMaxCount || bytes > kMirrorMaxBytes) {
+  while (R.v.size() > kMirrorMaxCount || bytes > mirror_budget()) {
     size_t victim = R.v.size();
     for (size_t i = 0; i < R.v.size(); ++i)
       if (R.v[i].use_count() == 1 && (victim == R.v.size() || R.v[i]->tick < R.v[victim]->tick))
         victim = i;
     if (victim == R.v.size()) break;  // all in use
     bytes -= R.v[victim]->block.cap + R.v[victim]->io.cap;
+    dead.push_back(std::move(R.v[victim]));
     R.v.erase(R.v.begin() + ptrdiff_t(victim));
   }
   return m;
 }
 
-// existing mirror of p on dev, or null
-std::shared_ptr<Mirror> mirror_find(const CLzmaDec* p, int dev) {
-  Registry& R = registry();
-  std::lock_guard<std::mutex> g(R.mu);
-  for (auto& e : R.v)
-    if (e->key == p && e->dev == dev) return e;
-  return nullptr;
+// FNV-1a over the table cells the decoder uses (the coherence check of the
+// host table: a few KiB per call)
+uint64_t probs_hash(const CLzmaProb* t, uint32_t cells) {
+  const uint8_t* b = reinterpret_cast<const uint8_t*>(t);
+  uint64_t h = 1469598103934665603ull;
+  for (size_t i = 0; i < size_t(cells) * sizeof(CLzmaProb); ++i) h = (h ^ b[i]) * 1099511628211ull;
+  return h;
 }
 
 void mirror_drop(const CLzmaDec* p) {
@@ -244,30 +278,6 @@ void mirror_drop(const CLzmaDec* p) {
   R.v.erase(std::remove_if(R.v.begin(), R.v.end(),
                            [&](const std::shared_ptr<Mirror>& e) { return e->key == p; }),
             R.v.end());
-}
-
-// The host wrote dic[off, off + n) itself (an LZMA2 stored chunk,
-// Lzma2Dec.c:159-166): write it through to the device copy.  Without a live
-// mirror there is nothing to keep in step (the next call rebuilds it).
-bool mirror_host_wrote(const CLzmaDec* p, SizeT off, SizeT n) {
-  if (n == 0) return true;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return false;
-  std::shared_ptr<Mirror> m = mirror_find(p, dev);
-  if (!m) return true;
-  std::lock_guard<std::mutex> busy(m->busy);
-  if (m->dic != p->dic || m->dic_buf_size != p->dicBufSize || !m->history || !m->block.p)
-    return true;  // stale or not yet holding history: rebuilt from the host on next use
-  ScratchLease L;
-  uint8_t* d_dic = static_cast<uint8_t*>(m->block.p) + kSessBytes + probs_area(m->num_probs);
-  if (!L.s ||
-      !hip_ok(xfer(d_dic + off, p->dic + off, n, hipMemcpyHostToDevice, L.s->stream),
-              "dictionary write-through") ||
-      !hip_ok(hipStreamSynchronize(L.s->stream), "dictionary write-through")) {
-    m->history = false;
-    return false;
-  }
-  return true;
 }
 
 // One LzmaDec_DecodeToDic (mode 0) or LzmaDec_DecodeToBuf (mode 1) call on the
@@ -283,18 +293,21 @@ SRes gpu_session_call(CLzmaDec* p, int mode, SizeT dicLimit, const Byte* src, Si
     set_error("LzmaDec: probabilities not allocated for the current props");
     return SZ_ERROR_PARAM;
   }
+  const size_t pa = probs_area(p->numProbs);
   std::shared_ptr<Mirror> m;
-  try {
-    m = mirror_get(p, dev);
-  } catch (const std::exception&) {
-    set_error("LzmaDec: host allocation failed");
-    return SZ_ERROR_MEM;
+  {
+    std::vector<std::shared_ptr<Mirror>> dead;  // released after the registry lock
+    try {
+      m = mirror_get(p, dev, kSessBytes + pa + p->dicBufSize + 16, dead);
+    } catch (const std::exception&) {
+      set_error("LzmaDec: host allocation failed");
+      return SZ_ERROR_MEM;
+    }
   }
   std::lock_guard<std::mutex> busy(m->busy);
   ScratchLease L;
   if (!L.s) return SZ_ERROR_FAIL;
   const hipStream_t st = L.s->stream;
-  const size_t pa = probs_area(p->numProbs);
   const size_t out_room = mode == 1 ? size_t(*destLen) : 0;
   const void* blk_before = m->block.p;
   uint8_t* blk = static_cast<uint8_t*>(m->block.get(kSessBytes + pa + p->dicBufSize + 16));
@@ -316,6 +329,26 @@ SRes gpu_session_call(CLzmaDec* p, int mode, SizeT dicLimit, const Byte* src, Si
     set_error(what);
     return SZ_ERROR_FAIL;
   };
+  // coherence with host-side writes since the previous call (file header)
+  if (m->history) {
+    const SizeT np = p->dicPos, op = m->end_pos, B = p->dicBufSize;
+    const uint32_t dt = p->processedPos - m->end_total;
+    bool ok = false;
+    if (dt == 0) {
+      ok = np == op || (op == B && np == 0);  // untouched, or the ring wrapped
+    } else if (np <= B && op <= B) {
+      const SizeT o = op == B ? 0 : op;
+      if (np >= o && np - o == dt) {  // the host wrote dic[o, np)
+        ok = xfer(d_dic + o, p->dic + o, np - o, hipMemcpyHostToDevice, st) == hipSuccess;
+      } else if (np < o && (B - o) + np == dt) {  // ... across the ring end
+        ok = xfer(d_dic + o, p->dic + o, B - o, hipMemcpyHostToDevice, st) == hipSuccess &&
+             (np == 0 || xfer(d_dic, p->dic, np, hipMemcpyHostToDevice, st) == hipSuccess);
+      }
+    }
+    if (!ok) m->history = false;
+  }
+  if (m->probs_dev && (m->probs_cells != cells || probs_hash(p->probs, cells) != m->probs_hash))
+    m->probs_dev = false;
   // the table: the device copy is current after every successful call
   if (!m->probs_dev &&
       xfer(d_probs, p->probs, size_t(cells) * 2, hipMemcpyHostToDevice, st) != hipSuccess)
@@ -422,6 +455,10 @@ SRes gpu_session_call(CLzmaDec* p, int mode, SizeT dicLimit, const Byte* src, Si
   p->buf = src + q.in_used;
   m->history = true;
   m->probs_dev = true;
+  m->end_pos = p->dicPos;
+  m->end_total = p->processedPos;
+  m->probs_cells = cells;
+  m->probs_hash = probs_hash(p->probs, cells);
   *in_used = q.in_used;
   *status = ELzmaStatus(q.status);
   return q.res;
@@ -727,11 +764,10 @@ SRes Lzma2Dec_DecodeToDic(CLzma2Dec* p, SizeT dicLimit, const Byte* src, SizeT* 
       }
       if (in_cur > out_cur) in_cur = out_cur;
       if (in_cur == 0) return SZ_ERROR_DATA;
-      // stored chunk: a plain copy into the dictionary (Lzma2Dec.c:159-166),
-      // written through to the decoder's device mirror
+      // stored chunk: a plain copy into the dictionary (Lzma2Dec.c:159-166);
+      // the next LzmaDec_DecodeToDic uploads it (the mirror's coherence check)
       CLzmaDec* d = &p->decoder;
       memcpy(d->dic + d->dicPos, src, in_cur);
-      if (!mirror_host_wrote(d, d->dicPos, in_cur)) return SZ_ERROR_FAIL;
       d->dicPos += in_cur;
       if (d->checkDicSize == 0 && d->prop.dicSize - d->processedPos <= in_cur)
         d->checkDicSize = d->prop.dicSize;
