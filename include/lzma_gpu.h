@@ -169,6 +169,14 @@ void LzmaGpu_DecoderRelease(const CLzmaDec *p);
  * argument may be NULL.  Process-wide. */
 void LzmaGpu_DropinTransferStats(uint64_t *h2d_bytes, uint64_t *d2h_bytes, uint64_t *calls,
                                  int reset);
+/* Coalesced one-call decodes (round 4): LzmaDecode / LzmaUncompress /
+ * Lzma2Decode calls made by several host threads at once share launches
+ * (group commit per device: calls arriving while a batch runs form the next
+ * batch; a lone caller's batch has one item).  Counts since start or the last
+ * reset, summed over devices: batches launched, calls they carried, the
+ * largest batch.  LZGPU_COALESCE=0 gives every call its own launch.  Any
+ * argument may be NULL. */
+void LzmaGpu_CoalesceStats(uint64_t *batches, uint64_t *calls, uint64_t *max_batch, int reset);
 
 /* ---------------------------------------------------------------- drop-in LzmaLib.h */
 
@@ -338,6 +346,10 @@ typedef struct LzmaGpuPlanOptions {
 /* one class per table-width bucket even when several land in the one-lane
  * latency regime (default: those are merged into one class, one launch) */
 #define LZMA_GPU_PLAN_NO_MERGE_LAT 8u
+/* throughput classes run the decision-level loop (round 4: one range-coder
+ * decision per lane per iteration, the lane's phase choosing the cell; the
+ * symbol loop otherwise) */
+#define LZMA_GPU_PLAN_STEP 0x80u
 /* throughput classes keep the probability sections that are not in LDS in
  * per-stream slices (the round-2 layout) instead of lane-interleaved -- cell i
  * of the 32 lanes of a lane group side by side -- in a slot area per class
@@ -445,7 +457,12 @@ SRes LzmaGpu_SessionDecodeBatch(LzmaGpuSession *d_sessions, size_t n, void *stre
  * LzmaGpuResult) equal LzmaGpu_DecodeBatchEx's, i.e. LzmaDecode's per stream.
  * A round's launch is bounded by slice_bytes of output per stream, so work of
  * other streams or tenants queued on the device waits at most one round
- * behind a long stream, and a caller can stop after any round and resume.
+ * behind a long stream, and a caller can stop after any round and resume --
+ * with one exception: a stream whose round hits SZ_ERROR_DATA is decoded
+ * again from its start in that same round as one unbounded call (the
+ * reference's results on corrupt input depend on where its calls start,
+ * LzmaDec.c:797,826; sliced.hip), so one corrupt long stream can hold a round
+ * for a whole stream's worth of decode.
  * LZMA items only (an LZMA2 item: SZ_ERROR_PARAM at plan time). */
 #define LZMA_GPU_SLICED_AUTO 0u
 #define LZMA_GPU_SLICED_LANE 1u   /* one stream per wave, its table staged in LDS per round */
@@ -488,7 +505,7 @@ SRes LzmaGpu_DecodeBatchSliced(const LzmaGpuSlicedPlan *plan, const LzmaGpuStrea
  * after the last; 0 once every stream is done).  Synchronises `stream`. */
 SRes LzmaGpu_SlicedActive(const LzmaGpuSlicedPlan *plan, const void *d_workspace, unsigned round,
                           size_t *active, void *stream);
-/* Host-buffer form (uploads, every round, downloads); rounds_out may be NULL. */
+/* Host-buffer form (uploads, every round, downloads); plan_out may be NULL. */
 SRes LzmaGpu_DecodeBatchSlicedHost(const LzmaGpuStreamDesc *descs, size_t n, const Byte *src,
                                    size_t src_bytes, Byte *dst, size_t dst_bytes,
                                    LzmaGpuResult *results, uint64_t slice_bytes, unsigned kernel,

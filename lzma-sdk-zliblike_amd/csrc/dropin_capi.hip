@@ -42,6 +42,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
 #include <cstddef>
 #include <cstdio>
 #include <cstdlib>
@@ -89,10 +90,218 @@ struct ScratchLease {
 
 // ------------------------------------------------------------------ one-call decodes
 
-// LzmaDecode-style one call over host buffers: a one-item batch on the
-// cooperative kernel (LzmaGpu_PlanBatchOpt with LZMA_GPU_KERNEL_COOP: one
-// 32-lane wave, the whole table in LDS where it fits -- the generic all-global
-// kernel only for lc + lp too wide for LDS).
+// ------------------------------------------------------------------ coalesced one-call decodes
+//
+// One-call decodes (LzmaDecode, LzmaUncompress, Lzma2Decode) made by several
+// host threads at once share launches -- group commit: a call joins its
+// device's pending list; if no batch is running on that device it takes the
+// whole list and runs it as ONE batch (inputs packed into pinned staging, one
+// upload, one plan + launch, one download of results and outputs), otherwise it
+// waits, and the calls that arrive while a batch runs form the next one.  An
+// unchanged multi-threaded caller (the reference's LzmaDecode / LzmaUncompress
+// are reentrant, LzmaDec.c:972-1002, LzmaLib.c:41-46) therefore reaches the
+// batch planner and its throughput / latency kernels; a lone caller pays
+// nothing extra (its batch has one item, planned onto the wave-cooperative
+// kernel as before, and starts at once).  LZGPU_COALESCE=0 gives every call its
+// own launch.
+struct OneCall {
+  uint8_t kind = 0;
+  const Byte* src = nullptr;
+  SizeT in_size = 0;
+  Byte* dest = nullptr;
+  SizeT out_size = 0;
+  Byte props[LZMA_PROPS_SIZE] = {};
+  uint8_t props_size = 0;
+  uint8_t finish = 0;
+  LzmaGpuResult r = {};
+  SRes err = SZ_OK;       // infrastructure failure of the batch (else r.res)
+  const char* msg = "";   // its message (static text)
+  bool done = false;
+};
+
+struct Coalescer {
+  std::mutex mu;
+  std::condition_variable cv;
+  std::vector<OneCall*> pending;
+  bool running = false;
+  // the running leader's resources
+  uint8_t* pin = nullptr;  // pinned staging: inputs | outputs | meta
+  size_t pin_cap = 0;
+  DevBuf io, ws, meta;
+  hipStream_t stream = nullptr;
+  std::atomic<uint64_t> batches{0}, items{0}, max_items{0};
+};
+
+std::atomic<Coalescer*> g_coal[kLzgpuMaxDevices];
+Coalescer* coalescer(int dev) {
+  static std::mutex mu;
+  if (dev < 0 || dev >= kLzgpuMaxDevices) return nullptr;
+  std::lock_guard<std::mutex> g(mu);
+  if (!g_coal[dev].load()) g_coal[dev].store(new (std::nothrow) Coalescer());  // process lifetime
+  return g_coal[dev].load();
+}
+Coalescer* coalescer_if(int dev) { return g_coal[dev].load(); }
+
+bool coalesce_on() {
+  static const bool on = [] {
+    const char* e = getenv("LZGPU_COALESCE");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+size_t align16(size_t v) { return (v + 15) & ~size_t(15); }
+
+// One batch of calls on the current device (the leader, C.mu not held).
+void run_batch(Coalescer& C, const std::vector<OneCall*>& b) {
+  const size_t k = b.size();
+  auto fail_all = [&](SRes e, const char* what) {
+    for (OneCall* c : b) {
+      c->err = e;
+      c->msg = what;
+    }
+  };
+  std::vector<LzmaGpuStreamDesc> d(k);
+  std::vector<uint32_t> order(k);
+  size_t in_total = 0, out_total = 0;
+  for (size_t i = 0; i < k; ++i) {
+    const OneCall& c = *b[i];
+    LzmaGpuStreamDesc& x = d[i];
+    memset(&x, 0, sizeof x);
+    x.src_off = in_total;
+    x.src_len = c.in_size;
+    x.dst_off = out_total;
+    x.dst_cap = c.out_size;
+    memcpy(x.props, c.props, sizeof c.props);
+    x.props_size = c.props_size;
+    x.finish_mode = c.finish;
+    x.kind = c.kind;
+    in_total += align16(c.in_size);
+    out_total += align16(c.out_size);
+  }
+  LzmaGpuPlan plan;
+  LzmaGpuPlanOptions o;
+  memset(&o, 0, sizeof o);
+  // one item: one 32-lane wave with the whole table in LDS (the round-3
+  // single-call path); several: the planner's choice for the batch
+  o.kernel = k == 1 ? LZMA_GPU_KERNEL_COOP : LZMA_GPU_KERNEL_AUTO;
+  {
+    const SRes pr = LzmaGpu_PlanBatchOpt(d.data(), k, order.data(), &plan, &o);
+    if (pr != SZ_OK) return fail_all(pr, "LzmaDecode: batch plan failed");
+  }
+  const size_t meta_bytes = align16(k * sizeof(LzmaGpuStreamDesc)) + align16(k * sizeof(uint32_t));
+  const size_t res_bytes = k * sizeof(LzmaGpuResult);
+  const size_t pin_need = in_total + meta_bytes + res_bytes + 64;
+  if (C.pin_cap < pin_need) {
+    if (C.pin) (void)hipHostFree(C.pin);
+    C.pin = nullptr;
+    C.pin_cap = 0;
+    const size_t want = std::max(pin_need, C.pin_cap * 2);
+    if (hipHostMalloc(reinterpret_cast<void**>(&C.pin), want, hipHostMallocDefault) != hipSuccess) {
+      (void)hipGetLastError();
+      C.pin = nullptr;
+      return fail_all(SZ_ERROR_MEM, "LzmaDecode: pinned staging allocation failed");
+    }
+    C.pin_cap = want;
+  }
+  uint8_t* d_io = static_cast<uint8_t*>(C.io.get(in_total + out_total + 16));
+  void* d_ws = C.ws.get(size_t(plan.workspace_bytes));
+  uint8_t* d_meta = static_cast<uint8_t*>(C.meta.get(meta_bytes + res_bytes + 16));
+  if (!d_io || !d_ws || !d_meta) return fail_all(SZ_ERROR_MEM, "LzmaDecode: device allocation failed");
+  // pack inputs and metadata, one upload each
+  uint8_t* pin_meta = C.pin + in_total;
+  for (size_t i = 0; i < k; ++i)
+    if (b[i]->in_size) memcpy(C.pin + d[i].src_off, b[i]->src, b[i]->in_size);
+  memcpy(pin_meta, d.data(), k * sizeof(LzmaGpuStreamDesc));
+  memcpy(pin_meta + align16(k * sizeof(LzmaGpuStreamDesc)), order.data(), k * sizeof(uint32_t));
+  const hipStream_t st = C.stream;
+  LzmaGpuResult* pin_res = reinterpret_cast<LzmaGpuResult*>(pin_meta + meta_bytes);
+  LzmaGpuResult* d_res = reinterpret_cast<LzmaGpuResult*>(d_meta + meta_bytes);
+  if ((in_total && xfer(d_io, C.pin, in_total, hipMemcpyHostToDevice, st) != hipSuccess) ||
+      xfer(d_meta, pin_meta, meta_bytes, hipMemcpyHostToDevice, st) != hipSuccess)
+    return fail_all(SZ_ERROR_FAIL, "LzmaDecode: upload failed");
+  if (LzmaGpu_DecodeBatchEx(&plan, reinterpret_cast<LzmaGpuStreamDesc*>(d_meta),
+                            reinterpret_cast<uint32_t*>(d_meta + align16(k * sizeof(LzmaGpuStreamDesc))),
+                            d_io, d_io + in_total, d_ws, d_res, st) != SZ_OK) {
+    (void)hipStreamSynchronize(st);
+    return fail_all(SZ_ERROR_FAIL, "LzmaDecode: batch launch failed");
+  }
+  if (xfer(pin_res, d_res, res_bytes, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      hipStreamSynchronize(st) != hipSuccess)
+    return fail_all(SZ_ERROR_FAIL, "LzmaDecode: decode kernel failed");
+  // outputs: straight into each caller's buffer (only the bytes decoded)
+  for (size_t i = 0; i < k; ++i) {
+    OneCall& c = *b[i];
+    c.r = pin_res[i];
+    if (c.r.dest_len > c.out_size) {
+      c.err = SZ_ERROR_FAIL;
+      c.msg = "LzmaDecode: kernel reported more output than its capacity";
+      continue;
+    }
+    if (c.r.dest_len &&
+        xfer(c.dest, d_io + in_total + d[i].dst_off, c.r.dest_len, hipMemcpyDeviceToHost, st) !=
+            hipSuccess) {
+      c.err = SZ_ERROR_FAIL;
+      c.msg = "LzmaDecode: download output failed";
+    }
+  }
+  if (hipStreamSynchronize(st) != hipSuccess) fail_all(SZ_ERROR_FAIL, "LzmaDecode: download output");
+}
+
+// Submit one call; returns when its batch has run.
+void coalesced(OneCall& me, int dev) {
+  Coalescer* Cp = coalescer(dev);
+  if (!Cp) {
+    me.err = SZ_ERROR_MEM;
+    me.msg = "LzmaDecode: host allocation failed";
+    return;
+  }
+  Coalescer& C = *Cp;
+  std::unique_lock<std::mutex> lk(C.mu);
+  if (!C.stream && hipStreamCreateWithFlags(&C.stream, hipStreamNonBlocking) != hipSuccess) {
+    (void)hipGetLastError();
+    C.stream = nullptr;
+    me.err = SZ_ERROR_FAIL;
+    me.msg = "LzmaDecode: stream creation failed";
+    return;
+  }
+  C.pending.push_back(&me);
+  while (!me.done) {
+    if (C.running) {
+      C.cv.wait(lk);
+      continue;
+    }
+    // lead: take everything pending (this call included) as one batch
+    C.running = true;
+    std::vector<OneCall*> batch;
+    batch.swap(C.pending);
+    if (!coalesce_on() && batch.size() > 1) {  // one launch per call: this one now
+      for (OneCall* c : batch)
+        if (c != &me) C.pending.push_back(c);
+      batch.assign(1, &me);
+    }
+    lk.unlock();
+    try {
+      run_batch(C, batch);
+    } catch (const std::exception&) {
+      for (OneCall* c : batch) {
+        c->err = SZ_ERROR_MEM;
+        c->msg = "LzmaDecode: host allocation failed";
+      }
+    }
+    C.batches++;
+    C.items += batch.size();
+    uint64_t mx = C.max_items.load();
+    while (batch.size() > mx && !C.max_items.compare_exchange_weak(mx, batch.size())) {
+    }
+    lk.lock();
+    for (OneCall* c : batch) c->done = true;
+    C.running = false;
+    C.cv.notify_all();
+  }
+}
+
+// LzmaDecode-style one call over host buffers through the device's coalescer.
 SRes gpu_one_call(uint8_t kind, Byte* dest, SizeT* destLen, const Byte* src, SizeT* srcLen,
                   const Byte* props, unsigned propSize, ELzmaFinishMode finishMode,
                   int* status_out) {
@@ -100,65 +309,27 @@ SRes gpu_one_call(uint8_t kind, Byte* dest, SizeT* destLen, const Byte* src, Siz
   *srcLen = 0;
   *destLen = 0;
   if (!ensure_device()) return SZ_ERROR_FAIL;
+  int dev = 0;
+  if (!hip_ok(hipGetDevice(&dev), "current device")) return SZ_ERROR_FAIL;
   ++g_calls;
-  struct Meta {  // one upload: the descriptor and its lane order
-    LzmaGpuStreamDesc d;
-    uint32_t order;
-    uint32_t pad[3];
-  } m;
-  memset(&m, 0, sizeof m);
-  m.d.src_len = in_size;
-  m.d.dst_cap = out_size;
-  memcpy(m.d.props, props, std::min<unsigned>(propSize, 5));
-  m.d.props_size = uint8_t(std::min<unsigned>(propSize, 255));
-  m.d.finish_mode = uint8_t(finishMode);
-  m.d.kind = kind;
-  LzmaGpuPlan plan;
-  LzmaGpuPlanOptions o;
-  memset(&o, 0, sizeof o);
-  o.kernel = LZMA_GPU_KERNEL_COOP;
-  {
-    const SRes pr = LzmaGpu_PlanBatchOpt(&m.d, 1, &m.order, &plan, &o);
-    if (pr != SZ_OK) return pr;
+  OneCall c;
+  c.kind = kind;
+  c.src = src;
+  c.in_size = in_size;
+  c.dest = dest;
+  c.out_size = out_size;
+  memcpy(c.props, props, std::min<unsigned>(propSize, LZMA_PROPS_SIZE));
+  c.props_size = uint8_t(std::min<unsigned>(propSize, 255));
+  c.finish = uint8_t(finishMode);
+  coalesced(c, dev);
+  if (c.err != SZ_OK) {
+    set_error(c.msg);
+    return c.err;
   }
-  ScratchLease L;
-  if (!L.s) return SZ_ERROR_FAIL;
-  CallScratch& S = *L.s;
-  const size_t in_pad = (size_t(in_size) + 15) & ~size_t(15);
-  uint8_t* d_io = static_cast<uint8_t*>(S.buf[0].get(in_pad + out_size + 16));
-  void* d_ws = S.buf[1].get(size_t(plan.workspace_bytes));
-  uint8_t* d_meta = static_cast<uint8_t*>(S.buf[2].get(sizeof(Meta) + sizeof(LzmaGpuResult)));
-  if (!d_io || !d_ws || !d_meta) {
-    set_error("LzmaDecode: device allocation failed");
-    return SZ_ERROR_MEM;
-  }
-  const hipStream_t st = S.stream;
-  LzmaGpuResult r;
-  if (in_size && !hip_ok(xfer(d_io, src, in_size, hipMemcpyHostToDevice, st), "upload src"))
-    return SZ_ERROR_FAIL;
-  if (!hip_ok(xfer(d_meta, &m, sizeof m, hipMemcpyHostToDevice, st), "upload desc"))
-    return SZ_ERROR_FAIL;
-  LzmaGpuResult* d_res = reinterpret_cast<LzmaGpuResult*>(d_meta + sizeof(Meta));
-  if (LzmaGpu_DecodeBatchEx(&plan, reinterpret_cast<LzmaGpuStreamDesc*>(d_meta),
-                            reinterpret_cast<uint32_t*>(d_meta + offsetof(Meta, order)), d_io,
-                            d_io + in_pad, d_ws, d_res, st) != SZ_OK)
-    return SZ_ERROR_FAIL;
-  if (!hip_ok(xfer(&r, d_res, sizeof r, hipMemcpyDeviceToHost, st), "download result") ||
-      !hip_ok(hipStreamSynchronize(st), "decode kernel"))
-    return SZ_ERROR_FAIL;
-  if (r.dest_len > out_size) {
-    set_error("LzmaDecode: kernel reported more output than its capacity");
-    return SZ_ERROR_FAIL;
-  }
-  if (r.dest_len &&
-      (!hip_ok(xfer(dest, d_io + in_pad, r.dest_len, hipMemcpyDeviceToHost, st),
-               "download output") ||
-       !hip_ok(hipStreamSynchronize(st), "download output")))
-    return SZ_ERROR_FAIL;
-  *destLen = r.dest_len;
-  *srcLen = r.src_len;
-  *status_out = r.status;
-  return r.res;
+  *destLen = c.r.dest_len;
+  *srcLen = c.r.src_len;
+  *status_out = c.r.status;
+  return c.r.res;
 }
 
 // ------------------------------------------------------------------ dictionary mirrors
@@ -564,6 +735,20 @@ void LzmaGpu_DropinTransferStats(uint64_t* h2d_bytes, uint64_t* d2h_bytes, uint6
   if (h2d_bytes) *h2d_bytes = reset ? g_h2d.exchange(0) : g_h2d.load();
   if (d2h_bytes) *d2h_bytes = reset ? g_d2h.exchange(0) : g_d2h.load();
   if (calls) *calls = reset ? g_calls.exchange(0) : g_calls.load();
+}
+
+void LzmaGpu_CoalesceStats(uint64_t* batches, uint64_t* calls, uint64_t* max_batch, int reset) {
+  uint64_t b = 0, c = 0, m = 0;
+  for (int dev = 0; dev < kLzgpuMaxDevices; ++dev) {
+    Coalescer* C = coalescer_if(dev);
+    if (!C) continue;
+    b += reset ? C->batches.exchange(0) : C->batches.load();
+    c += reset ? C->items.exchange(0) : C->items.load();
+    m = std::max<uint64_t>(m, reset ? C->max_items.exchange(0) : C->max_items.load());
+  }
+  if (batches) *batches = b;
+  if (calls) *calls = c;
+  if (max_batch) *max_batch = m;
 }
 
 // ------------------------------------------------------------------ decode entry points

@@ -187,7 +187,8 @@ static LzmaGpuPlanOptions env_options() {
             (env_int("LZGPU_MERGE_LAT", 1) ? 0u : LZMA_GPU_PLAN_NO_MERGE_LAT) |
             (env_int("LZGPU_ILV", 1) ? 0u : LZMA_GPU_PLAN_NO_ILV) |
             (env_int("LZGPU_ILV_ANY", 0) ? LZMA_GPU_PLAN_ILV_ANY : 0u) |
-            (env_int("LZGPU_THR_FIT", 1) ? 0u : LZMA_GPU_PLAN_NO_THR_FIT);
+            (env_int("LZGPU_THR_FIT", 1) ? 0u : LZMA_GPU_PLAN_NO_THR_FIT) |
+            (env_int("LZGPU_STEP", 0) ? LZMA_GPU_PLAN_STEP : 0u);
   return o;
 }
 
@@ -450,6 +451,8 @@ static SRes plan_batch(LzmaGpuStreamDesc* descs, size_t n, uint32_t* order, Lzma
       if (in_slots.empty()) in_slots.assign(n, 0);
       for (uint32_t i : bucket_idx[b]) in_slots[i] = 1;
     }
+    if ((o.flags & LZMA_GPU_PLAN_STEP) && (c.lds_mask & ~lzgpu::kIlvBit) == LZGPU_LDS_MASK)
+      c.lds_mask |= lzgpu::kStepBit;
     plan->classes[plan->n_classes++] = c;
     plan->n_lds += c.n;
     if (c.n > best) {

@@ -31,6 +31,8 @@
 
 #include <stdint.h>
 
+#include <type_traits>
+
 #ifdef LZGPU_HOST_EMU
 // Test-only host build of the per-lane logic (tests/emu): lets the CPU test
 // suite exercise exactly this code before it runs on the GPU.  Never part
@@ -500,29 +502,21 @@ typedef GlobalReader16 PlainReader;
 // Bit 31 of a placement mask marks the wave-cooperative kernel (kCoopBit: one
 // stream per wave, every lane holding the same state; lit8_coop).
 constexpr uint32_t kCoopBit = 0x80000000u;
-template <uint32_t M>
-struct BulkReaderFor {
-  typedef PlainReader type;
-};
-template <>
-struct BulkReaderFor<LZGPU_LDS_MASK> {
-  typedef GlobalReaderQ type;
-};
-template <>
-struct BulkReaderFor<LZGPU_LDS_MASK | kIlvBit> {
-  typedef GlobalReaderQ type;
-};
-template <>
-struct BulkReaderFor<LZGPU_LDS_MASK_LAT | kCoopBit> {
-  typedef GlobalReaderQ type;
-};
+// Bit 28 of a placement mask (kStepBit, round 4): the bulk pass runs as the
+// decision-level loop lz_run_step (one range-coder decision per lane per
+// iteration) instead of the symbol loop lz_run; the sections and their
+// placement are those of the rest of the mask.
+constexpr uint32_t kStepBit = 0x10000000u;
 // every section in LDS (cooperative classes with few streams per CU)
 #ifndef LZGPU_LDS_MASK_ALL
 #define LZGPU_LDS_MASK_ALL 0x7FFu
 #endif
-template <>
-struct BulkReaderFor<LZGPU_LDS_MASK_ALL | kCoopBit> {
-  typedef GlobalReaderQ type;
+template <uint32_t M>
+struct BulkReaderFor {
+  static constexpr uint32_t m = M & ~(kIlvBit | kStepBit);
+  static constexpr bool q = m == LZGPU_LDS_MASK || m == (LZGPU_LDS_MASK_LAT | kCoopBit) ||
+                            m == (LZGPU_LDS_MASK_ALL | kCoopBit) || (M & kStepBit) != 0u;
+  typedef typename std::conditional<q, GlobalReaderQ, PlainReader>::type type;
 };
 
 // Matched-byte prefetch per placement: the byte at rep0 is loaded at match end in
@@ -533,7 +527,7 @@ struct BulkReaderFor<LZGPU_LDS_MASK_ALL | kCoopBit> {
 // within noise either way: profiles/r02_ilv/mbpf_latency_ab.log)
 template <uint32_t M>
 __host__ __device__ constexpr bool mb_pf_on() {
-  return ((M & kCoopBit) != 0u) || ((M & ~kIlvBit) == LZGPU_LDS_MASK);
+  return ((M & kCoopBit) != 0u) || ((M & ~(kIlvBit | kStepBit)) == LZGPU_LDS_MASK);
 }
 
 // checkpoint hooks for readers without them: every NORMALIZE checks
@@ -1160,12 +1154,396 @@ __device__ __forceinline__ bool lz_any(bool v) {
 }
 
 
+// ------------------------------------------------------------------ decision-level loop
+//
+// lz_run_step: the same contract as lz_run (one LzmaDec_DecodeReal pass,
+// LzmaDec.c:131-426: symbols until pos reaches `limit` or the reader reaches
+// `in_limit`, checked after each whole symbol; state written back only on
+// success), restructured for SIMT.  lz_run follows the reference's control
+// flow -- a symbol is a nest of branches, and the lanes of a wave sit in
+// different branches (literal runs of different lengths, plain vs matched
+// literals, the match path's kinds), so a wave executes the union of its
+// lanes' paths: 11.1 of 32 lanes active per VALU instruction on config 3
+// (profiles/r03_final/pmc_summary.json).  Here each lane is a small state
+// machine and every iteration of ONE loop makes exactly one range-coder
+// decision per lane: the lane's phase picks the probability cell (IsMatch, a
+// literal-tree node, a rep bit, a length / slot / SpecPos / align node) or a
+// direct bit, and the normalise / bound / compare / update sequence
+// (LzmaDec.c:8-45, 323-344) is shared by all lanes whatever their phase.  At
+// the end of a phase (a tree's last level, a single-bit decision) the lane
+// takes its transition -- the symbol grammar of LzmaDec.c:160-411 -- and
+// match copies run as their own (non-decision) phase.
+enum : uint32_t {
+  PH_LIT = 0,   // literal tree level (LzmaDec.c:161-196): plain, or matched while
+                // the decoded bits follow the match byte
+  PH_ISMATCH,   // IsMatch[state][posState] (:158-160)
+  PH_REP,       // IsRep / IsRepG0 / IsRepG1 / IsRepG2 [state] (:201-258): `aux` = which
+  PH_REP0L,     // IsRep0Long[state][posState] (:213-228)
+  PH_LCH,       // length choice (:263-268)
+  PH_LCH2,      // length choice2 (:270-285)
+  PH_LTREE,     // low / mid / high length tree; len = node + aux at its end
+  PH_SLOT,      // position slot tree (:295-300)
+  PH_SPEC,      // SpecPos reverse tree (:306-321), `aux` = its bits
+  PH_DIRECT,    // direct bits (:323-344), accumulated in `node`
+  PH_ALIGN,     // Align reverse tree (:345-353)
+  PH_COPY,      // the LZ copy of a match / rep / short rep (:373-408), no decision
+  PH_END        // pass over (`err` set on SZ_ERROR_DATA)
+};
+
+__host__ __device__ __forceinline__ uint32_t lz_bitrev(uint32_t v, uint32_t n) {
+#ifdef LZGPU_HOST_EMU
+  uint32_t r = 0;
+  for (uint32_t k = 0; k < n; ++k) r |= ((v >> k) & 1u) << (n - 1 - k);
+  return r;
+#else
+  return n ? (__builtin_bitreverse32(v) >> (32 - n)) : 0u;
+#endif
+}
+
+template <uint32_t M, class Lo, class Rd>
+__device__ __forceinline__ int lz_run_step(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
+                                           uint32_t in_limit) {
+  const Tab<M, Lo> T(s);
+  constexpr auto lds_of = [](uint32_t sec) { return ((M >> sec) & 1u) != 0u; };
+  const uint32_t pb = s.pb, lc = s.lc;
+  const uint32_t pb_mask = (1u << pb) - 1, lp_mask = (1u << s.lp) - 1;
+  gbyte* __restrict__ dic = s.dic;
+  const uint64_t cap = s.cap;
+  const uint32_t full = s.full;
+  uint64_t pos = s.pos;
+  uint32_t total = s.total, st = s.st;
+  uint32_t r0 = s.rep0, r1 = s.rep1, r2 = s.rep2, r3 = s.rep3;
+  uint32_t range = s.range, code = s.code;
+  uint32_t len = 0, prev = 0, mbp = 0;
+  if (full != 0 || total != 0) prev = dic[(pos == 0 ? cap : pos) - 1];
+  if (st >= 7) mbp = dic[ring_back(pos, r0, cap)];
+  const uint32_t o_match = T.L.o[S_MATCH], o_rep = T.L.o[S_REP], o_rep0l = T.L.o[S_REP0L];
+  const uint32_t o_len = T.L.o[S_LEN], o_replen = T.L.o[S_REPLEN], o_lenhi = T.L.o[S_LENHI];
+  const uint32_t o_slot = T.L.o[S_SLOT], o_spec = T.L.o[S_SPEC], o_align = T.L.o[S_ALIGN];
+  const uint32_t o_litp = T.L.o[S_LITP], o_litm = T.L.o[S_LITM];
+  static_assert(lds_of(S_LEN) == lds_of(S_REPLEN), "Len/RepLen placement");
+  // the lane's phase and its current tree: cell = cb + node in the table
+  // `cg` (global) or LDS; `left` decisions to the phase's end
+  uint32_t ph = PH_ISMATCH, node = 1, left = 1, aux = 0, dist = 0;
+  uint32_t cb = o_match + (st << pb) + (total & pb_mask) - 1;
+  bool cg = !lds_of(S_MATCH);
+  // matched literal: `mlm` while the decoded bits equal the match byte's,
+  // `mb` the match byte's remaining bits (MSB at bit 7), `litm` its tree
+  bool mlm = false, lrep = false;
+  uint32_t mb = 0, litm = 0, lcoff = o_len;
+  int err = kOk;
+  uint32_t it = 0;
+  while (lz_any(ph != PH_END)) {
+    if ((it++ & 3u) == 0u) {
+      // reader checkpoint: >= 5 bytes in the window for the next four
+      // iterations (one NORMALIZE each at most)
+      if (ph != PH_END) rd_topup(rd);
+    }
+    if (ph < PH_COPY) {
+      // ---- the decision (every lane in a decision phase, whatever the phase)
+      const uint32_t mk = (mb >> 7) & 1u;
+      const bool ml = mlm && ph == PH_LIT;
+      const uint32_t ci = ml ? litm + (mk << 8) + node : cb + node;
+      const bool g = ml ? !lds_of(S_LITM) : cg;
+      const bool dir = ph == PH_DIRECT;
+      uint32_t p = 0;
+      if (!dir) {
+        if (g)
+          p = *T.g(ci);
+        else
+          p = T.lo[ci];
+      }
+      if (range < kTop) {  // NORMALIZE (LzmaDec.c:17)
+        range <<= 8;
+        code = (code << 8) | rd_take_u(rd);
+      }
+      const uint32_t bound = dir ? (range >> 1) : (range >> 11) * p;
+      // direct bits: the sign of code - range (LzmaDec.c:329-332); else IF_BIT_0
+      const bool bit = dir ? (int32_t(code - bound) >= 0) : (code >= bound);
+      code = bit ? code - bound : code;
+      range = (dir || !bit) ? bound : range - bound;
+      if (!dir) {
+        const int32_t m = bit ? 0 : int32_t(kProbOne - 31);
+        const uint16_t np = uint16_t(int32_t(p) - ((int32_t(p) - m) >> 5));
+        if (g)
+          *T.g(ci) = np;
+        else
+          T.lo[ci] = np;
+      }
+      node = 2 * node + (bit ? 1u : 0u);
+      mlm = ml && (bit ? 1u : 0u) == mk;
+      mb = (mb << 1) & 0xFFu;
+      --left;
+      // ---- the phase's end: the symbol grammar (LzmaDec.c:158-371)
+      if (left == 0) {
+        bool sym_done = false;  // a literal: the loop check follows
+        switch (ph) {
+          case PH_ISMATCH:
+            if (!bit) {
+              uint32_t ctx = 0;
+              if (full != 0 || total != 0) ctx = ((total & lp_mask) << lc) + (prev >> (8 - lc));
+              cb = o_litp + (ctx << 8);
+              cg = !lds_of(S_LITP);
+              if (st >= 7) {
+                mlm = true;
+                mb = mbp & 0xFFu;
+                litm = o_litm + (ctx << 9);
+                st = (st < 10) ? st - 3 : st - 6;
+              } else {
+                st = (st < 4) ? 0 : st - 3;
+              }
+              ph = PH_LIT;
+              node = 1;
+              left = 8;
+            } else {
+              ph = PH_REP;
+              aux = 0;
+              cb = o_rep + st - 1;
+              cg = !lds_of(S_REP);
+              node = 1;
+              left = 1;
+            }
+            break;
+          case PH_LIT:
+            prev = node & 0xFFu;
+            lz_put(dic + pos, prev);
+            ++pos;
+            ++total;
+            mlm = false;
+            sym_done = true;
+            break;
+          case PH_REP:
+            if (aux == 0) {
+              if (!bit) {  // a match: state + 12 marks it until the distance
+                st += 12;
+                lrep = false;
+                ph = PH_LCH;
+              } else if (full == 0 && total == 0) {
+                err = kErrData;
+                ph = PH_END;
+                break;
+              } else {
+                aux = 1;
+              }
+            } else if (aux == 1) {
+              if (!bit) {
+                ph = PH_REP0L;
+                cb = o_rep0l + (st << pb) + (total & pb_mask) - 1;
+                cg = !lds_of(S_REP0L);
+              } else {
+                aux = 2;
+              }
+            } else if (aux == 2 && bit) {
+              aux = 3;
+            } else {
+              uint32_t d;
+              if (aux == 2) {
+                d = r1;
+              } else {
+                if (!bit) {
+                  d = r2;
+                } else {
+                  d = r3;
+                  r3 = r2;
+                }
+                r2 = r1;
+              }
+              r1 = r0;
+              r0 = d;
+              st = (st < 7) ? 8 : 11;
+              lrep = true;
+              ph = PH_LCH;
+            }
+            if (ph == PH_REP) cb = o_rep + 12 * aux + st - 1;
+            node = 1;
+            left = 1;
+            if (ph == PH_LCH) {
+              lcoff = lrep ? o_replen : o_len;
+              cb = lcoff - 1;
+              cg = !lds_of(S_LEN);
+            }
+            break;
+          case PH_REP0L:
+            node = 1;
+            left = 1;
+            if (!bit) {  // short rep: a one-byte copy
+              st = (st < 7) ? 9 : 11;
+              len = 1;
+              ph = PH_COPY;
+            } else {
+              st = (st < 7) ? 8 : 11;
+              lrep = true;
+              lcoff = o_replen;
+              cb = lcoff - 1;
+              cg = !lds_of(S_LEN);
+              ph = PH_LCH;
+            }
+            break;
+          case PH_LCH:
+            if (!bit) {
+              cb = lcoff + 2 + ((total & pb_mask) << 3);
+              left = 3;
+              aux = 0u - 8u;
+              ph = PH_LTREE;
+            } else {
+              cb = lcoff;
+              left = 1;
+              ph = PH_LCH2;
+            }
+            node = 1;
+            break;
+          case PH_LCH2:
+            if (!bit) {
+              cb = lcoff + 2 + (8u << pb) + ((total & pb_mask) << 3);
+              left = 3;
+              aux = 0;
+            } else {
+              cb = o_lenhi + (lrep ? 256u : 0u);
+              cg = !lds_of(S_LENHI);
+              left = 8;
+              aux = 16u - 256u;
+            }
+            node = 1;
+            ph = PH_LTREE;
+            break;
+          case PH_LTREE:
+            len = node + aux;
+            node = 1;
+            if (st >= 12) {
+              cb = o_slot + ((len < 4 ? len : 3u) << 6);
+              cg = !lds_of(S_SLOT);
+              left = 6;
+              ph = PH_SLOT;
+            } else {
+              len += 2;  // kMatchMinLen (LzmaDec.c:371)
+              ph = PH_COPY;
+            }
+            break;
+          case PH_SLOT: {
+            const uint32_t slot = node - 64;
+            if (slot < 4) {
+              dist = slot;
+              ph = PH_END + 1;  // distance complete (below)
+            } else {
+              const uint32_t nb = (slot >> 1) - 1;
+              dist = 2u | (slot & 1u);
+              if (slot < 14) {
+                dist <<= nb;
+                cb = o_spec + dist - slot - 1;
+                cg = !lds_of(S_SPEC);
+                node = 1;
+                left = nb;
+                aux = nb;
+                ph = PH_SPEC;
+              } else {
+                node = dist;  // the direct bits accumulate under it, MSB first
+                left = nb - 4;
+                ph = PH_DIRECT;
+              }
+            }
+            break;
+          }
+          case PH_SPEC:
+            dist |= lz_bitrev(node - (1u << aux), aux);
+            ph = PH_END + 1;
+            break;
+          case PH_DIRECT:
+            dist = node << 4;
+            cb = o_align;
+            cg = !lds_of(S_ALIGN);
+            node = 1;
+            left = 4;
+            ph = PH_ALIGN;
+            break;
+          case PH_ALIGN:
+            dist |= lz_bitrev(node - 16u, 4);
+            ph = PH_END + 1;
+            break;
+        }
+        if (ph == PH_END + 1) {  // the distance of a match is complete (LzmaDec.c:354-371)
+          if (dist == 0xFFFFFFFFu) {  // end marker
+            len += kLenDone;
+            st -= 12;
+            ph = PH_END;
+          } else {
+            r3 = r2;
+            r2 = r1;
+            r1 = r0;
+            r0 = dist + 1;
+            if (full == 0 ? dist >= total : dist >= full) {
+              err = kErrData;
+              ph = PH_END;
+            } else {
+              st = (st < 19) ? 7 : 10;
+              len += 2;
+              ph = PH_COPY;
+            }
+          }
+        }
+        if (sym_done) {
+          // loop condition of LzmaDec_DecodeReal (LzmaDec.c:410)
+          if (pos < limit && rd.used() < in_limit) {
+            ph = PH_ISMATCH;
+            cb = o_match + (st << pb) + (total & pb_mask) - 1;
+            cg = !lds_of(S_MATCH);
+            node = 1;
+            left = 1;
+          } else {
+            ph = PH_END;
+          }
+        }
+      }
+    } else if (ph == PH_COPY) {
+      // ---- the LZ copy (LzmaDec.c:373-408)
+      if (limit == pos) {
+        err = kErrData;
+        ph = PH_END;
+      } else {
+        const uint64_t room = limit - pos;
+        const uint32_t n = (room < len) ? uint32_t(room) : len;
+        const uint64_t from = ring_back(pos, r0, cap);
+        total += n;
+        len -= n;
+        prev = lz_copy(dic, pos, from, n, r0, cap);
+        pos += n;
+        mbp = dic[ring_back(pos, r0, cap)];
+        if (pos < limit && rd.used() < in_limit) {
+          ph = PH_ISMATCH;
+          cb = o_match + (st << pb) + (total & pb_mask) - 1;
+          cg = !lds_of(S_MATCH);
+          node = 1;
+          left = 1;
+        } else {
+          ph = PH_END;
+        }
+      }
+    }
+  }
+  if (err != kOk) return err;
+  if (range < kTop) {  // NORMALIZE after the loop (LzmaDec.c:411)
+    range <<= 8;
+    code = (code << 8) | rd.next();
+  }
+  s.range = range;
+  s.code = code;
+  s.pending = len;
+  s.pos = pos;
+  s.total = total;
+  s.rep0 = r0;
+  s.rep1 = r1;
+  s.rep2 = r2;
+  s.rep3 = r3;
+  s.st = st;
+  return kOk;
+}
+
 // Decode symbols until pos reaches `limit` or the reader index reaches
 // `in_limit` (checked after each whole symbol; the first is always decoded).
 // State is written back only on success, as LzmaDec_DecodeReal does.
 template <uint32_t M, class Lo, class Rd>
 __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
                                       uint32_t in_limit) {
+  if constexpr ((M & kStepBit) != 0u) return lz_run_step<M>(s, limit, rd, in_limit);
   const Tab<M, Lo> T(s);
   const uint32_t pb = s.pb;
   uint32_t st = s.st;

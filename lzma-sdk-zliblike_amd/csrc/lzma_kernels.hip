@@ -278,6 +278,16 @@ static int launch_class(const LzmaGpuStreamDesc* d_descs, const uint32_t* d_orde
                                                       d_results, lanes, stride, waves_per_simd,
                                                       groups_per_cu, max_groups, d_queue, sl,
                                                       stream);
+  // the decision-level loop (lz_run_step) on the throughput placement
+  if (lds_mask == (LZGPU_LDS_MASK | kIlvBit | kStepBit))
+    return launch_lds_w<LZGPU_LDS_MASK | kIlvBit | kStepBit, K2>(
+        d_descs, d_order, n, d_src, d_dst, d_ws, d_results, lanes, stride, waves_per_simd,
+        groups_per_cu, max_groups, d_queue, sl, stream);
+  if (lds_mask == (LZGPU_LDS_MASK | kStepBit))
+    return launch_lds_w<LZGPU_LDS_MASK | kStepBit, K2>(d_descs, d_order, n, d_src, d_dst, d_ws,
+                                                       d_results, lanes, stride, waves_per_simd,
+                                                       groups_per_cu, max_groups, d_queue, sl,
+                                                       stream);
   if (lds_mask == (LZGPU_LDS_MASK_LAT | kCoopBit)) {
     // one wave per workgroup: register budget by workgroups per SIMD
     constexpr uint32_t MC = LZGPU_LDS_MASK_LAT | kCoopBit;

@@ -254,9 +254,13 @@ __device__ __forceinline__ int session_to_dic(LzgpuSession& q, uint64_t dic_limi
 // dic_buf_size bytes; each pass decodes up to the ring end or the caller's
 // remaining room, copies the new bytes to `out`, and stops on an error, on a
 // pass that produced nothing, or when `out` is full).
-// Under the cooperative placement every lane of the wave runs the call and
-// has itself stored every dictionary byte, so the produced bytes are copied out
-// lane-strided (each lane reads only bytes it wrote).
+// Under the cooperative placement every lane of the wave runs the call, and the
+// produced bytes are copied out lane-strided with no barrier: lane i reads
+// bytes other lanes of its wave stored (lz_copy_coop gives byte j of a match
+// to lane j % 32).  What makes that correct is the wave's in-order memory
+// pipeline -- its global stores and later loads to the same address are seen
+// in issue order (one vector L1 per CU) -- the same property lz_copy_coop
+// relies on when a match reads bytes the wave just wrote.
 template <uint32_t M = 0u, class Lo = gu16*>
 __device__ __forceinline__ void lane_session(LzgpuSession& q, Lo lo = Lo()) {
   int status = kStNone;

@@ -17,6 +17,7 @@
 #include <algorithm>
 #include <cstring>
 #include <exception>
+#include <new>
 #include <vector>
 
 #include "lzma_gpu_internal.h"
@@ -357,13 +358,21 @@ SRes read_substreams(Sd& s, Ar& a, SubStreams& ss) {
   // With a kSize section a folder's substreams after its first each need a
   // size (>= 1 header byte): more than that cannot be described by the bytes
   // left.  Without one the reference takes any count it can allocate (sizes
-  // of all but a folder's last substream stay unset there); counts past 2^24
-  // fail as its allocation would (SZ_ERROR_MEM) instead of being attempted.
+  // of all but a folder's last substream stay unset there, 7zIn.c:757-768).
+  // DELIBERATE DEVIATION: counts past 2^24 return
+  // SZ_ERROR_MEM here instead of being attempted -- 2^31 substreams would zero
+  // 28 GB of host memory before failing or succeeding, which a library call
+  // on behalf of an untrusted header must not do.  Below the cap an
+  // allocation failure is reported the same way.
   if (t == kSize && uint64_t(ss.n) > uint64_t(s.n) + a.folders.size()) return SZ_ERROR_ARCHIVE;
   if (ss.n > (1u << 24)) return SZ_ERROR_MEM;
-  ss.sizes.assign(ss.n, 0);
-  ss.defined.assign(ss.n, 0);
-  ss.digests.assign(ss.n, 0);
+  try {
+    ss.sizes.assign(ss.n, 0);
+    ss.defined.assign(ss.n, 0);
+    ss.digests.assign(ss.n, 0);
+  } catch (const std::bad_alloc&) {
+    return SZ_ERROR_MEM;
+  }
   uint32_t si = 0;
   for (Folder& f : a.folders) {
     const uint32_t k = f.num_unpack_streams;

@@ -203,6 +203,7 @@ _sig = {
     "LzmaDec_DecodeToBuf": (ctypes.c_int, [ctypes.POINTER(CLzmaDec), _P, _sp, _P, _sp, ctypes.c_int, _ip]),
     "LzmaGpu_DecoderRelease": (None, [ctypes.POINTER(CLzmaDec)]),
     "LzmaGpu_DropinTransferStats": (None, [ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]),
+    "LzmaGpu_CoalesceStats": (None, [ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64), ctypes.c_int]),
     "LzmaDecode": (ctypes.c_int, [_P, _sp, _P, _sp, ctypes.c_char_p, ctypes.c_uint, ctypes.c_int, _ip, ctypes.POINTER(ISzAlloc)]),
     "LzmaUncompress": (ctypes.c_int, [_P, _sp, _P, _sp, ctypes.c_char_p, ctypes.c_size_t]),
     "Lzma2Dec_AllocateProbs": (ctypes.c_int, [ctypes.POINTER(CLzma2Dec), ctypes.c_ubyte, ctypes.POINTER(ISzAlloc)]),
@@ -308,6 +309,15 @@ def _buf(data):
 
 
 # ---------------------------------------------------------------- one-call API
+
+def coalesce_stats(reset=False):
+    """(batches, calls, largest batch) of the one-call coalescer
+    (LzmaGpu_CoalesceStats); reset zeroes the counters after reading."""
+    b, c, m = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+    _lib.LzmaGpu_CoalesceStats(ctypes.byref(b), ctypes.byref(c), ctypes.byref(m),
+                               1 if reset else 0)
+    return b.value, c.value, m.value
+
 
 def LzmaDecode(src, props, dest_cap, finish=LZMA_FINISH_END):
     """LzmaDecode (LzmaDec.c:972). Returns (res, status, destLen, srcLen, out)."""

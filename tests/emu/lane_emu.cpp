@@ -30,7 +30,7 @@ void emu_decode_batch(const LzmaGpuStreamDesc* descs, size_t n, const uint8_t* s
 void emu_decode_batch_lds(const LzmaGpuStreamDesc* descs, size_t n, const uint8_t* src,
                           uint8_t* dst, uint16_t* ws, LzmaGpuResult* results, uint32_t stride) {
   uint16_t* slab = (uint16_t*)malloc(size_t(stride) * 2 + 16);
-#if defined(EMU_ILV)
+#if defined(EMU_ILV) || defined(EMU_STEP_ILV)
   // lane-interleaved global sections: 32 lane columns of the widest LZMA2
   // layout's global rows; stream i runs in column i % 32, its neighbours'
   // cells left as garbage (columns are reused stream after stream)
@@ -39,7 +39,15 @@ void emu_decode_batch_lds(const LzmaGpuStreamDesc* descs, size_t n, const uint8_
 #endif
   for (size_t i = 0; i < n; ++i) {
     memset(slab, 0xA5, size_t(stride) * 2);  // LDS is not zeroed between workgroups
-#if defined(EMU_ILV)
+#if defined(EMU_STEP_ILV)
+    // the decision-level loop (lz_run_step) on the throughput placement with
+    // lane-interleaved global sections: the round-4 throughput instantiation
+    results[i] = lane_decode_lds<LZGPU_LDS_MASK | kIlvBit | kStepBit>(
+        descs[i], src, dst, ws, slab, stride, slots.data() + (i % kIlv) * kIlvLaneCells);
+#elif defined(EMU_STEP)
+    // the decision-level loop on the placement LZGPU_LDS_MASK (per-stream slices)
+    results[i] = lane_decode_lds<LZGPU_LDS_MASK | kStepBit>(descs[i], src, dst, ws, slab, stride);
+#elif defined(EMU_ILV)
     results[i] = lane_decode_lds<LZGPU_LDS_MASK | kIlvBit>(descs[i], src, dst, ws, slab, stride,
                                                           slots.data() + (i % kIlv) * kIlvLaneCells);
 #elif defined(EMU_COOP_ALL)

@@ -143,8 +143,9 @@ def test_open_huge_counts_do_not_allocate(L):
         assert r == 16, (name, r)  # SZ_ERROR_ARCHIVE
     # one folder claiming 2^31 - 1 substreams and no kSize section: the reference
     # takes any count it can allocate (7zIn.c:757-768, sizes of all but the last
-    # left unset); past 2^24 this build fails as that allocation would
-    # (SZ_ERROR_MEM) instead of attempting 16 GiB
+    # left unset).  DELIBERATE DEVIATION: past 2^24 this build
+    # returns SZ_ERROR_MEM instead of zeroing 28 GB of host memory for an
+    # untrusted header; the reference would attempt the allocation
     one = W.coder(W.M_COPY, b"")
     hdr = (bytes([0x01, 0x04, 0x06, 0x00, 0x01, 0x09, 0x05, 0x00, 0x07, 0x0B, 0x01, 0x00])
            + b"\x01" + one + bytes([0x0C, 0x05, 0x00, 0x08, 0x0D]) + big + b"\x00\x00")

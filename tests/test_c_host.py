@@ -49,6 +49,46 @@ def build_c_batch():
     return BATCH_BIN
 
 
+THREADS_SRC = os.path.join(ROOT, "tests", "c_host", "lzma_c_threads.c")
+THREADS_BIN = os.path.join(ROOT, "tests", "c_host", "build", "lzma_c_threads")
+THREADS_REF = os.path.join(ROOT, "oracle", "_ref", "lzma_c_threads_ref")
+
+
+def build_c_threads():
+    """The multi-threaded LzmaDecode caller against include/lzma_gpu.h, linked
+    to the in-tree library (its reference-linked twin: oracle/Makefile.ref)."""
+    os.makedirs(os.path.dirname(THREADS_BIN), exist_ok=True)
+    subprocess.run(["gcc", "-O2", "-std=c99", "-Wall", "-Wextra", "-Werror",
+                    "-D_POSIX_C_SOURCE=200809L", "-I", os.path.join(ROOT, "include"),
+                    "-o", THREADS_BIN, THREADS_SRC,
+                    "-L", os.path.join(ROOT, "lzma-sdk-zliblike_amd", "lib"), "-llzmagpu",
+                    "-lpthread", "-Wl,-rpath,$ORIGIN/../../../lzma-sdk-zliblike_amd/lib"],
+                   check=True)
+    return THREADS_BIN
+
+
+def write_stream_set(tmp, comps, props, outs):
+    """Files for lzma_c_threads: streams, uint64 lengths, props, output sizes."""
+    import struct
+    f = {k: os.path.join(tmp, k + ".bin") for k in ("src", "lens", "props", "outs")}
+    open(f["src"], "wb").write(b"".join(comps))
+    open(f["lens"], "wb").write(b"".join(struct.pack("<Q", len(c)) for c in comps))
+    open(f["props"], "wb").write(b"".join(props))
+    open(f["outs"], "wb").write(b"".join(struct.pack("<Q", n) for n in outs))
+    return f
+
+
+def run_c_threads(binary, threads, f, repeat=1, env=None, timeout=300):
+    import json
+    # the result line goes to stderr: the reference build prints a debug line
+    # per call to stdout (LzmaDec.c:945), discarded here
+    r = subprocess.run([binary, str(threads), f["src"], f["lens"], f["props"], f["outs"],
+                        str(repeat)], stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True,
+                       timeout=timeout, env=env)
+    assert r.returncode == 0, r.stderr
+    return json.loads([ln for ln in r.stderr.splitlines() if ln.startswith("{")][-1])
+
+
 def _run(tmp, props, src, out_size, in_chunk, out_chunk):
     p, s = os.path.join(tmp, "props.bin"), os.path.join(tmp, "stream.bin")
     open(p, "wb").write(props)
@@ -63,6 +103,7 @@ def test_c_host_builds_and_fails_loudly_without_gpu(tmp_path):
     import lzma
     build_c_host()
     build_c_batch()
+    build_c_threads()
     import torch
     if torch.cuda.is_available():
         pytest.skip("a device is visible: the GPU test covers this host")

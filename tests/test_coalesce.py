@@ -1,0 +1,110 @@
+"""Concurrent one-call decodes share launches (VERDICT r03 item 6b,
+dropin_capi.hip's coalescer): LzmaDecode / LzmaUncompress / Lzma2Decode calls
+made by several host threads at once run as batch launches -- calls arriving
+while a batch runs form the next one -- and every caller still gets exactly
+its own LzmaDecode results (LzmaDec.c:972-1002, LzmaLib.c:41-46).
+
+GPU: 400 calls from 48 Python threads (ctypes drops the GIL) over mixed
+lc/lp/pb streams, corrupt and truncated ones, both finish modes and LZMA2
+items, each checked against the oracle; the coalescer's counters show batches
+of more than one call.  The unchanged multi-threaded C caller
+(tests/c_host/lzma_c_threads.c) linked to the library agrees with the same
+source linked to the reference's LzmaDec.c, stream by stream (CRCs)."""
+import lzma
+import os
+import random
+import zlib
+from concurrent.futures import ThreadPoolExecutor
+
+import pytest
+
+import native
+import test_c_host as TC
+import workloads as W
+
+
+def _cases(n=400, seed=4242):
+    rng = random.Random(seed)
+    out = []
+    for i in range(n):
+        if i % 10 == 9:  # an LZMA2 item through Lzma2Decode
+            data = native.gen("text", 91_000 + i, rng.choice([1000, 9000, 40000]))
+            comp = lzma.compress(data, format=lzma.FORMAT_RAW,
+                                 filters=[{"id": lzma.FILTER_LZMA2, "dict_size": 1 << 16}])
+            out.append(("lzma2", comp, 16, len(data) + rng.choice([0, 0, 5]), 1))
+            continue
+        lc = rng.randrange(5)
+        lp = rng.randrange(5 - lc)
+        pb = rng.randrange(5)
+        dsz = rng.choice([4096, 1 << 16])
+        data = native.gen(rng.choice(["text", "random"]), 90_000 + i,
+                          rng.choice([0, 100, 4096, 20000]))
+        comp = bytearray(lzma.compress(data, format=lzma.FORMAT_RAW, filters=[
+            {"id": lzma.FILTER_LZMA1, "dict_size": dsz, "lc": lc, "lp": lp, "pb": pb}]))
+        if i % 7 == 3 and len(comp) > 8:
+            comp[rng.randrange(5, len(comp))] ^= 0x21
+        if i % 11 == 5:
+            comp = comp[:rng.randrange(len(comp) + 1)]
+        out.append(("lzma", bytes(comp), W.props_bytes(lc, lp, pb, dsz),
+                    len(data) + rng.choice([0, 0, 3]), rng.randrange(2)))
+    return out
+
+
+def test_coalesce_case_mix_is_varied():
+    kinds = {c[0] for c in _cases()}
+    assert kinds == {"lzma", "lzma2"}
+
+
+@pytest.mark.gpu
+def test_gpu_concurrent_calls_coalesce_and_match_oracle():
+    import lzmagpu as L
+    orc = native.oracle()
+    cases = _cases()
+    want = []
+    for kind, comp, props, cap, fin in cases:
+        if kind == "lzma":
+            want.append(native.decode(orc, "orc", comp, props, cap, fin))
+        else:
+            want.append(native.lzma2_decode(orc, "orc", comp, props, cap, fin))
+
+    def call(k):
+        kind, comp, props, cap, fin = cases[k]
+        if kind == "lzma":
+            return L.LzmaDecode(comp, props, cap, fin)
+        return L.Lzma2Decode(comp, props, cap, fin)
+
+    L.coalesce_stats(reset=True)
+    with ThreadPoolExecutor(48) as ex:
+        got = list(ex.map(call, range(len(cases))))
+    batches, calls, biggest = L.coalesce_stats()
+    bad = []
+    for k, (g, w) in enumerate(zip(got, want)):
+        res, st, dl, sl, out = g
+        wres, wst, wdl, wsl, wout = w
+        if (res, dl, sl) != (wres, wdl, wsl) or out != wout or (res == 0 and st != wst):
+            bad.append((k, cases[k][0], (res, st, dl, sl), (wres, wst, wdl, wsl)))
+    assert not bad, bad[:5]
+    assert calls == len(cases) and batches < calls and biggest > 1, (batches, calls, biggest)
+
+
+@pytest.mark.gpu
+def test_gpu_c_threads_caller_matches_reference_build(tmp_path):
+    if not os.path.exists(TC.THREADS_BIN):
+        TC.build_c_threads()
+    plain, comp, lens, props = W.uniform_batch(600, 4096, 0, 0, 0, 4096)
+    offs = [0]
+    for ln in lens:
+        offs.append(offs[-1] + int(ln))
+    comps = [comp[offs[i]:offs[i + 1]].tobytes() for i in range(600)]
+    f = TC.write_stream_set(str(tmp_path), comps, [props] * 600, [4096] * 600)
+    want = 0
+    for i in range(600):
+        want ^= zlib.crc32(plain[i * 4096:(i + 1) * 4096].tobytes(), i)
+    for threads in (1, 16, 64):
+        d = TC.run_c_threads(TC.THREADS_BIN, threads, f)
+        assert d["fails"] == 0 and d["crc_xor"] == "%08x" % want, d
+        if threads > 1:
+            assert d["max_batch"] > 1, d
+    if os.path.exists(TC.THREADS_REF):
+        d = TC.run_c_threads(TC.THREADS_REF, 16, f)
+        assert d["fails"] == 0 and d["crc_xor"] == "%08x" % want, d

@@ -38,6 +38,12 @@ EMU_VARIANTS = {
     "interleaved_global_instantiation": "-DEMU_ILV",
     "coop_instantiation": "-DEMU_COOP",
     "coop_all_lds_instantiation": "-DEMU_COOP_ALL",
+    # round 4: the decision-level loop (lz_run_step) on the throughput
+    # instantiation and on other placements of the same code
+    "step_interleaved_instantiation": "-DEMU_STEP_ILV",
+    "step_latency_mask": "-DEMU_STEP -DLZGPU_LDS_MASK=0x1BF",
+    "step_all_lds": "-DEMU_STEP -DLZGPU_LDS_MASK=0x7FF",
+    "step_all_global": "-DEMU_STEP -DLZGPU_LDS_MASK=0",
 }
 
 

@@ -50,7 +50,12 @@ ILV, PLAN_NO_ILV = 0x40000000, 16
 # stream)
 THR = ("throughput", "throughput_np", "throughput_slices", "throughput_slices_np",
        "throughput_reuse")
-KERNELS = THR + ("latency", "coop", "coop_lat", "global")
+# round 4: the decision-level loop (lz_run_step, LZMA_GPU_PLAN_STEP) on the same
+# throughput launches -- interleaved rows, per-stream slices, one stream per
+# lane, a lane decoding many streams in one column, and 16-lane waves
+STEP_BIT, PLAN_STEP = 0x10000000, 0x80
+STEP = ("step", "step_np", "step_slices", "step_reuse", "step_w16")
+KERNELS = THR + STEP + ("latency", "coop", "coop_lat", "global")
 
 
 @pytest.fixture(scope="module")
@@ -71,6 +76,17 @@ def torch():
 def _check_plan(plan, kernel):
     """The forced instantiation is the one the plan launches."""
     cls = [plan.classes[k] for k in range(plan.n_classes)]
+    if kernel in STEP:
+        assert plan.n_lds > 0 and cls
+        assert all(c.lds_mask & STEP_BIT for c in cls), [hex(c.lds_mask) for c in cls]
+        assert all((c.lds_mask & ~(STEP_BIT | ILV)) == M_THR for c in cls)
+        if kernel == "step":
+            assert any(c.lds_mask & ILV and c.lanes_per_group == 32 for c in cls)
+        if kernel == "step_slices":
+            assert not any(c.lds_mask & ILV for c in cls)
+        if kernel == "step_w16":
+            assert any(c.lds_mask & ILV and c.lanes_per_group == 16 for c in cls)
+        return
     if kernel == "global":
         assert plan.n_lds == 0 and plan.n_classes == 0
         return
@@ -110,6 +126,20 @@ def _check_plan(plan, kernel):
 def _opts(L, kernel):
     # plan as if the batch were spread over a few CUs, so that the throughput
     # shape (>= 64 streams per CU) is what a real 64K batch gets
+    if kernel == "step":
+        return L.plan_options("throughput", cus=8, flags=PLAN_STEP)
+    if kernel == "step_np":
+        return L.plan_options("throughput", cus=8, persistent=2, lanes_per_group=32,
+                              flags=PLAN_STEP)
+    if kernel == "step_slices":
+        return L.plan_options("throughput", cus=8, flags=PLAN_STEP | PLAN_NO_ILV)
+    if kernel == "step_reuse":
+        return L.plan_options("throughput", cus=1, groups_per_cu=1, lanes_per_group=32,
+                              flags=PLAN_STEP)
+    if kernel == "step_w16":
+        # 16-lane waves, 4 per SIMD, interleaved rows half used (PLAN_ILV_ANY)
+        return L.plan_options("throughput", cus=8, lanes_per_group=16, waves_per_simd=4,
+                              flags=PLAN_STEP | 32)
     if kernel == "coop_lat":
         return L.plan_options("coop", cus=8, flags=4)
     if kernel == "throughput_np":
@@ -162,7 +192,7 @@ def test_goldens_through_each_kernel(L, kernel):
     r, res, dst = L.decode_batch_host(descs, src, dst_bytes, _opts(L, kernel), plan)
     assert r == 0, L.last_error()
     _check_plan(plan, kernel)
-    if kernel in ("throughput", "throughput_slices"):
+    if kernel in ("throughput", "throughput_slices", "step", "step_slices"):
         # the lc0/lp0 goldens run the config-3 launch shape: 32 streams per wave
         assert max(plan.classes[k].lanes_per_group for k in range(plan.n_classes)) == 32
     bad = []
