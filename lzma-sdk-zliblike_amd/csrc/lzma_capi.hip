@@ -343,8 +343,10 @@ static SRes plan_batch(LzmaGpuStreamDesc* descs, size_t n, uint32_t* order, Lzma
                          bool any_groups, bool allow_fit = false) -> LzmaGpuLdsClass {
     bool lat = false;
     const int regime = o.kernel == LZMA_GPU_KERNEL_THROUGHPUT ? 1 : 0;
-    LzmaGpuLdsClass c = plan_lds_class(stride_lo, idx.size(), LZGPU_LDS_MASK, cus, regime, o,
-                                       &lat);
+    // the decision-level loop keeps one spare LDS cell per lane (lz_run_step)
+    const uint32_t spare = (o.flags & LZMA_GPU_PLAN_STEP) ? 1u : 0u;
+    LzmaGpuLdsClass c = plan_lds_class(stride_lo + spare, idx.size(), LZGPU_LDS_MASK, cus, regime,
+                                       o, &lat);
     const bool want_lat = o.kernel == LZMA_GPU_KERNEL_LATENCY || o.kernel == LZMA_GPU_KERNEL_COOP ||
                           (o.kernel == LZMA_GPU_KERNEL_AUTO && lat);
     if (!want_lat) return c;

@@ -1200,11 +1200,23 @@ __host__ __device__ __forceinline__ uint32_t lz_bitrev(uint32_t v, uint32_t n) {
 #endif
 }
 
+// Code shape (the second of two builds measured): lane
+// flags as integers (no lane-mask merges at every join), NORMALIZE as selects
+// on the checkpoint reader, the probability read from LDS for every lane (a
+// spare cell for lanes whose cell is global or who decode a direct bit) with
+// only the global read and store under a branch, and the literal path's
+// transitions (IsMatch -> literal -> IsMatch) ahead of the rest of the grammar.
 template <uint32_t M, class Lo, class Rd>
 __device__ __forceinline__ int lz_run_step(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
                                            uint32_t in_limit) {
   const Tab<M, Lo> T(s);
   constexpr auto lds_of = [](uint32_t sec) { return ((M >> sec) & 1u) != 0u; };
+  constexpr uint32_t G_MATCH = lds_of(S_MATCH) ? 0u : 1u, G_REP = lds_of(S_REP) ? 0u : 1u,
+                     G_REP0L = lds_of(S_REP0L) ? 0u : 1u, G_LEN = lds_of(S_LEN) ? 0u : 1u,
+                     G_LENHI = lds_of(S_LENHI) ? 0u : 1u, G_SLOT = lds_of(S_SLOT) ? 0u : 1u,
+                     G_SPEC = lds_of(S_SPEC) ? 0u : 1u, G_ALIGN = lds_of(S_ALIGN) ? 0u : 1u,
+                     G_LITP = lds_of(S_LITP) ? 0u : 1u, G_LITM = lds_of(S_LITM) ? 0u : 1u;
+  static_assert(lds_of(S_LEN) == lds_of(S_REPLEN), "Len/RepLen placement");
   const uint32_t pb = s.pb, lc = s.lc;
   const uint32_t pb_mask = (1u << pb) - 1, lp_mask = (1u << s.lp) - 1;
   gbyte* __restrict__ dic = s.dic;
@@ -1221,275 +1233,231 @@ __device__ __forceinline__ int lz_run_step(LzStateT<Lo>& s, uint64_t limit, Rd& 
   const uint32_t o_len = T.L.o[S_LEN], o_replen = T.L.o[S_REPLEN], o_lenhi = T.L.o[S_LENHI];
   const uint32_t o_slot = T.L.o[S_SLOT], o_spec = T.L.o[S_SPEC], o_align = T.L.o[S_ALIGN];
   const uint32_t o_litp = T.L.o[S_LITP], o_litm = T.L.o[S_LITM];
-  static_assert(lds_of(S_LEN) == lds_of(S_REPLEN), "Len/RepLen placement");
-  // the lane's phase and its current tree: cell = cb + node in the table
-  // `cg` (global) or LDS; `left` decisions to the phase's end
+  // the lane's spare LDS cell (one past its sections; the planner reserves
+  // it): reads and stores of lanes whose cell is global, or who decode a
+  // direct bit, go there instead of behind a branch
+  const uint32_t spare = T.L.lds_cells;
   uint32_t ph = PH_ISMATCH, node = 1, left = 1, aux = 0, dist = 0;
-  uint32_t cb = o_match + (st << pb) + (total & pb_mask) - 1;
-  bool cg = !lds_of(S_MATCH);
-  // matched literal: `mlm` while the decoded bits equal the match byte's,
-  // `mb` the match byte's remaining bits (MSB at bit 7), `litm` its tree
-  bool mlm = false, lrep = false;
-  uint32_t mb = 0, litm = 0, lcoff = o_len;
+  uint32_t cb = o_match + (st << pb) + (total & pb_mask) - 1, cg = G_MATCH;
+  uint32_t mlm = 0, lrep = 0, mb = 0, litm = 0, lcoff = o_len;
   int err = kOk;
   uint32_t it = 0;
   while (lz_any(ph != PH_END)) {
-    if ((it++ & 3u) == 0u) {
-      // reader checkpoint: >= 5 bytes in the window for the next four
-      // iterations (one NORMALIZE each at most)
-      if (ph != PH_END) rd_topup(rd);
-    }
+    // reader checkpoint every 4 iterations (one NORMALIZE each at most); a
+    // finished lane's reader keeps used() unchanged
+    if ((it++ & 3u) == 0u) rd_topup(rd);
     if (ph < PH_COPY) {
-      // ---- the decision (every lane in a decision phase, whatever the phase)
       const uint32_t mk = (mb >> 7) & 1u;
-      const bool ml = mlm && ph == PH_LIT;
-      const uint32_t ci = ml ? litm + (mk << 8) + node : cb + node;
-      const bool g = ml ? !lds_of(S_LITM) : cg;
-      const bool dir = ph == PH_DIRECT;
-      uint32_t p = 0;
-      if (!dir) {
-        if (g)
-          p = *T.g(ci);
-        else
-          p = T.lo[ci];
-      }
-      if (range < kTop) {  // NORMALIZE (LzmaDec.c:17)
-        range <<= 8;
-        code = (code << 8) | rd_take_u(rd);
+      const uint32_t ci = mlm ? litm + (mk << 8) + node : cb + node;
+      const uint32_t g = mlm ? G_LITM : cg;
+      const uint32_t dir = ph == PH_DIRECT ? 1u : 0u;  // DIRECT lanes carry cg = 0
+      const uint32_t la = (g | dir) ? spare : ci;
+      uint32_t p = T.lo[la];
+      if (g) p = *T.g(ci);
+      // NORMALIZE (LzmaDec.c:17)
+      if constexpr (kIsQ<Rd>) {
+        const bool n = range < kTop;
+        code = n ? (code << 8) | uint32_t(rd.win & 0xFFu) : code;
+        range = n ? range << 8 : range;
+        rd.win = n ? rd.win >> 8 : rd.win;
+        rd.nb -= n ? 1u : 0u;
+      } else {
+        if (range < kTop) {
+          range <<= 8;
+          code = (code << 8) | rd.next();
+        }
       }
       const uint32_t bound = dir ? (range >> 1) : (range >> 11) * p;
-      // direct bits: the sign of code - range (LzmaDec.c:329-332); else IF_BIT_0
-      const bool bit = dir ? (int32_t(code - bound) >= 0) : (code >= bound);
+      const uint32_t bit = dir ? (int32_t(code - bound) >= 0 ? 1u : 0u) : (code >= bound ? 1u : 0u);
       code = bit ? code - bound : code;
-      range = (dir || !bit) ? bound : range - bound;
-      if (!dir) {
-        const int32_t m = bit ? 0 : int32_t(kProbOne - 31);
-        const uint16_t np = uint16_t(int32_t(p) - ((int32_t(p) - m) >> 5));
-        if (g)
-          *T.g(ci) = np;
-        else
-          T.lo[ci] = np;
-      }
-      node = 2 * node + (bit ? 1u : 0u);
-      mlm = ml && (bit ? 1u : 0u) == mk;
+      range = (dir | (bit ^ 1u)) ? bound : range - bound;
+      const int32_t m = bit ? 0 : int32_t(kProbOne - 31);
+      const uint32_t np = uint32_t(int32_t(p) - ((int32_t(p) - m) >> 5));
+      T.lo[la] = uint16_t(np);
+      if (g) *T.g(ci) = uint16_t(np);
+      node = 2 * node + bit;
+      mlm &= (bit == mk) ? 1u : 0u;
       mb = (mb << 1) & 0xFFu;
       --left;
-      // ---- the phase's end: the symbol grammar (LzmaDec.c:158-371)
       if (left == 0) {
-        bool sym_done = false;  // a literal: the loop check follows
-        switch (ph) {
-          case PH_ISMATCH:
-            if (!bit) {
-              uint32_t ctx = 0;
-              if (full != 0 || total != 0) ctx = ((total & lp_mask) << lc) + (prev >> (8 - lc));
-              cb = o_litp + (ctx << 8);
-              cg = !lds_of(S_LITP);
-              if (st >= 7) {
-                mlm = true;
-                mb = mbp & 0xFFu;
-                litm = o_litm + (ctx << 9);
-                st = (st < 10) ? st - 3 : st - 6;
-              } else {
-                st = (st < 4) ? 0 : st - 3;
-              }
-              ph = PH_LIT;
-              node = 1;
-              left = 8;
-            } else {
-              ph = PH_REP;
-              aux = 0;
-              cb = o_rep + st - 1;
-              cg = !lds_of(S_REP);
-              node = 1;
-              left = 1;
-            }
-            break;
-          case PH_LIT:
-            prev = node & 0xFFu;
-            lz_put(dic + pos, prev);
-            ++pos;
-            ++total;
-            mlm = false;
-            sym_done = true;
-            break;
-          case PH_REP:
-            if (aux == 0) {
-              if (!bit) {  // a match: state + 12 marks it until the distance
+        if (ph == PH_LIT) {
+          // ---- a literal is complete (LzmaDec.c:196-197)
+          prev = node & 0xFFu;
+          lz_put(dic + pos, prev);
+          ++pos;
+          ++total;
+          mlm = 0;
+          const bool more = pos < limit && rd.used() < in_limit;  // LzmaDec.c:410
+          ph = more ? PH_ISMATCH : PH_END;
+          cb = o_match + (st << pb) + (total & pb_mask) - 1;
+          cg = G_MATCH;
+          node = 1;
+          left = 1;
+        } else if (ph == PH_ISMATCH) {
+          if (!bit) {
+            // ---- a literal (LzmaDec.c:161-196)
+            const uint32_t ctx =
+                (full != 0 || total != 0) ? ((total & lp_mask) << lc) + (prev >> (8 - lc)) : 0u;
+            cb = o_litp + (ctx << 8);
+            cg = G_LITP;
+            mlm = st >= 7 ? 1u : 0u;
+            mb = mbp & 0xFFu;
+            litm = o_litm + (ctx << 9);
+            st = st < 4 ? 0u : (st < 10 ? st - 3 : st - 6);
+            ph = PH_LIT;
+            left = 8;
+          } else {
+            ph = PH_REP;
+            aux = 0;
+            cb = o_rep + st - 1;
+            cg = G_REP;
+            left = 1;
+          }
+          node = 1;
+        } else {
+          // ---- the rest of the grammar (LzmaDec.c:199-371)
+          switch (ph) {
+            case PH_REP:
+              if (aux == 0 && !bit) {  // a match: state + 12 marks it until the distance
                 st += 12;
-                lrep = false;
+                lrep = 0;
                 ph = PH_LCH;
-              } else if (full == 0 && total == 0) {
+              } else if (aux == 0 && full == 0 && total == 0) {
                 err = kErrData;
                 ph = PH_END;
-                break;
-              } else {
-                aux = 1;
-              }
-            } else if (aux == 1) {
-              if (!bit) {
+              } else if (aux == 1 && !bit) {
                 ph = PH_REP0L;
                 cb = o_rep0l + (st << pb) + (total & pb_mask) - 1;
-                cg = !lds_of(S_REP0L);
+                cg = G_REP0L;
+              } else if (aux < 2 || (aux == 2 && bit)) {
+                ++aux;
+                cb = o_rep + 12 * aux + st - 1;
               } else {
-                aux = 2;
-              }
-            } else if (aux == 2 && bit) {
-              aux = 3;
-            } else {
-              uint32_t d;
-              if (aux == 2) {
-                d = r1;
-              } else {
-                if (!bit) {
-                  d = r2;
+                uint32_t d;
+                if (aux == 2) {
+                  d = r1;
                 } else {
-                  d = r3;
-                  r3 = r2;
+                  d = bit ? r3 : r2;
+                  r3 = bit ? r2 : r3;
+                  r2 = r1;
                 }
-                r2 = r1;
+                r1 = r0;
+                r0 = d;
+                st = st < 7 ? 8u : 11u;
+                lrep = 1;
+                ph = PH_LCH;
               }
-              r1 = r0;
-              r0 = d;
-              st = (st < 7) ? 8 : 11;
-              lrep = true;
-              ph = PH_LCH;
-            }
-            if (ph == PH_REP) cb = o_rep + 12 * aux + st - 1;
-            node = 1;
-            left = 1;
-            if (ph == PH_LCH) {
-              lcoff = lrep ? o_replen : o_len;
-              cb = lcoff - 1;
-              cg = !lds_of(S_LEN);
-            }
-            break;
-          case PH_REP0L:
-            node = 1;
-            left = 1;
-            if (!bit) {  // short rep: a one-byte copy
-              st = (st < 7) ? 9 : 11;
-              len = 1;
-              ph = PH_COPY;
-            } else {
-              st = (st < 7) ? 8 : 11;
-              lrep = true;
-              lcoff = o_replen;
-              cb = lcoff - 1;
-              cg = !lds_of(S_LEN);
-              ph = PH_LCH;
-            }
-            break;
-          case PH_LCH:
-            if (!bit) {
-              cb = lcoff + 2 + ((total & pb_mask) << 3);
-              left = 3;
-              aux = 0u - 8u;
+              break;
+            case PH_REP0L:
+              if (!bit) {  // short rep: a one-byte copy (LzmaDec.c:213-228)
+                st = st < 7 ? 9u : 11u;
+                len = 1;
+                ph = PH_COPY;
+              } else {
+                st = st < 7 ? 8u : 11u;
+                lrep = 1;
+                ph = PH_LCH;
+              }
+              break;
+            case PH_LCH:
+              if (!bit) {
+                cb = lcoff + 2 + ((total & pb_mask) << 3);
+                left = 3;
+                aux = 0u - 8u;
+                ph = PH_LTREE;
+              } else {
+                cb = lcoff;
+                ph = PH_LCH2;
+              }
+              break;
+            case PH_LCH2:
+              if (!bit) {
+                cb = lcoff + 2 + (8u << pb) + ((total & pb_mask) << 3);
+                left = 3;
+                aux = 0;
+              } else {
+                cb = o_lenhi + (lrep ? 256u : 0u);
+                cg = G_LENHI;
+                left = 8;
+                aux = 16u - 256u;
+              }
               ph = PH_LTREE;
-            } else {
-              cb = lcoff;
-              left = 1;
-              ph = PH_LCH2;
-            }
-            node = 1;
-            break;
-          case PH_LCH2:
-            if (!bit) {
-              cb = lcoff + 2 + (8u << pb) + ((total & pb_mask) << 3);
-              left = 3;
-              aux = 0;
-            } else {
-              cb = o_lenhi + (lrep ? 256u : 0u);
-              cg = !lds_of(S_LENHI);
-              left = 8;
-              aux = 16u - 256u;
-            }
-            node = 1;
-            ph = PH_LTREE;
-            break;
-          case PH_LTREE:
-            len = node + aux;
-            node = 1;
-            if (st >= 12) {
-              cb = o_slot + ((len < 4 ? len : 3u) << 6);
-              cg = !lds_of(S_SLOT);
-              left = 6;
-              ph = PH_SLOT;
-            } else {
-              len += 2;  // kMatchMinLen (LzmaDec.c:371)
-              ph = PH_COPY;
-            }
-            break;
-          case PH_SLOT: {
-            const uint32_t slot = node - 64;
-            if (slot < 4) {
-              dist = slot;
-              ph = PH_END + 1;  // distance complete (below)
-            } else {
+              break;
+            case PH_LTREE:
+              len = node + aux;
+              if (st >= 12) {
+                cb = o_slot + ((len < 4 ? len : 3u) << 6);
+                cg = G_SLOT;
+                left = 6;
+                ph = PH_SLOT;
+              } else {
+                len += 2;  // kMatchMinLen (LzmaDec.c:371)
+                ph = PH_COPY;
+              }
+              break;
+            case PH_SLOT: {
+              const uint32_t slot = node - 64;
               const uint32_t nb = (slot >> 1) - 1;
-              dist = 2u | (slot & 1u);
-              if (slot < 14) {
+              dist = slot < 4 ? slot : (2u | (slot & 1u));
+              if (slot < 4) {
+                ph = PH_END + 1;
+              } else if (slot < 14) {
                 dist <<= nb;
                 cb = o_spec + dist - slot - 1;
-                cg = !lds_of(S_SPEC);
-                node = 1;
+                cg = G_SPEC;
                 left = nb;
                 aux = nb;
                 ph = PH_SPEC;
               } else {
-                node = dist;  // the direct bits accumulate under it, MSB first
                 left = nb - 4;
+                cg = 0;
                 ph = PH_DIRECT;
               }
+              break;
             }
-            break;
+            case PH_SPEC:
+              dist |= lz_bitrev(node - (1u << aux), aux);
+              ph = PH_END + 1;
+              break;
+            case PH_DIRECT:
+              dist = node << 4;
+              cb = o_align;
+              cg = G_ALIGN;
+              left = 4;
+              ph = PH_ALIGN;
+              break;
+            case PH_ALIGN:
+              dist |= lz_bitrev(node - 16u, 4);
+              ph = PH_END + 1;
+              break;
           }
-          case PH_SPEC:
-            dist |= lz_bitrev(node - (1u << aux), aux);
-            ph = PH_END + 1;
-            break;
-          case PH_DIRECT:
-            dist = node << 4;
-            cb = o_align;
-            cg = !lds_of(S_ALIGN);
-            node = 1;
-            left = 4;
-            ph = PH_ALIGN;
-            break;
-          case PH_ALIGN:
-            dist |= lz_bitrev(node - 16u, 4);
-            ph = PH_END + 1;
-            break;
-        }
-        if (ph == PH_END + 1) {  // the distance of a match is complete (LzmaDec.c:354-371)
-          if (dist == 0xFFFFFFFFu) {  // end marker
-            len += kLenDone;
-            st -= 12;
-            ph = PH_END;
-          } else {
-            r3 = r2;
-            r2 = r1;
-            r1 = r0;
-            r0 = dist + 1;
-            if (full == 0 ? dist >= total : dist >= full) {
-              err = kErrData;
+          if (ph == PH_LCH) {
+            lcoff = lrep ? o_replen : o_len;
+            cb = lcoff - 1;
+            cg = G_LEN;
+          }
+          left = left ? left : 1u;  // single-bit phases
+          // the direct bits accumulate under (2 | slot & 1) in node, MSB first
+          node = ph == PH_DIRECT ? dist : 1u;
+          if (ph == PH_END + 1) {  // the distance of a match (LzmaDec.c:354-371)
+            if (dist == 0xFFFFFFFFu) {  // end marker
+              len += kLenDone;
+              st -= 12;
               ph = PH_END;
             } else {
-              st = (st < 19) ? 7 : 10;
-              len += 2;
-              ph = PH_COPY;
+              r3 = r2;
+              r2 = r1;
+              r1 = r0;
+              r0 = dist + 1;
+              if (full == 0 ? dist >= total : dist >= full) {
+                err = kErrData;
+                ph = PH_END;
+              } else {
+                st = st < 19 ? 7u : 10u;
+                len += 2;
+                ph = PH_COPY;
+              }
             }
-          }
-        }
-        if (sym_done) {
-          // loop condition of LzmaDec_DecodeReal (LzmaDec.c:410)
-          if (pos < limit && rd.used() < in_limit) {
-            ph = PH_ISMATCH;
-            cb = o_match + (st << pb) + (total & pb_mask) - 1;
-            cg = !lds_of(S_MATCH);
-            node = 1;
-            left = 1;
-          } else {
-            ph = PH_END;
           }
         }
       }
@@ -1507,15 +1475,12 @@ __device__ __forceinline__ int lz_run_step(LzStateT<Lo>& s, uint64_t limit, Rd& 
         prev = lz_copy(dic, pos, from, n, r0, cap);
         pos += n;
         mbp = dic[ring_back(pos, r0, cap)];
-        if (pos < limit && rd.used() < in_limit) {
-          ph = PH_ISMATCH;
-          cb = o_match + (st << pb) + (total & pb_mask) - 1;
-          cg = !lds_of(S_MATCH);
-          node = 1;
-          left = 1;
-        } else {
-          ph = PH_END;
-        }
+        const bool more = pos < limit && rd.used() < in_limit;
+        ph = more ? PH_ISMATCH : PH_END;
+        cb = o_match + (st << pb) + (total & pb_mask) - 1;
+        cg = G_MATCH;
+        node = 1;
+        left = 1;
       }
     }
   }

@@ -122,7 +122,9 @@ __device__ __forceinline__ LzmaGpuResult lane_decode_lds(const LzmaGpuStreamDesc
       return r;
     } else {
     // chunks may switch lc/lp/pb (lc + lp <= 4): the slice holds the widest layout
-    if (d.probs_off == LZMA_GPU_NO_WORKSPACE || lzma2_lds_cells(M) > lo_cap) {
+    // (+1: the decision-level loop's spare cell, lz_run_step)
+    if (d.probs_off == LZMA_GPU_NO_WORKSPACE ||
+        lzma2_lds_cells(M) + ((M & kStepBit) ? 1u : 0u) > lo_cap) {
       r.res = (d.props[0] > 40) ? kErrUnsupported : kErrMem;
       return r;
     }
@@ -158,7 +160,7 @@ __device__ __forceinline__ LzmaGpuResult lane_decode_lds(const LzmaGpuStreamDesc
   r.res = lz_props_parse(d.props, d.props_size, s.lc, s.lp, s.pb, s.dict_size);
   if (r.res != kOk) return r;
   if (d.probs_off == LZMA_GPU_NO_WORKSPACE ||
-      make_layout(s.lc, s.lp, s.pb, M).lds_cells > lo_cap) {
+      make_layout(s.lc, s.lp, s.pb, M).lds_cells + ((M & kStepBit) ? 1u : 0u) > lo_cap) {
     r.res = kErrMem;
     return r;
   }

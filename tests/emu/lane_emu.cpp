@@ -34,7 +34,10 @@ void emu_decode_batch_lds(const LzmaGpuStreamDesc* descs, size_t n, const uint8_
   // lane-interleaved global sections: 32 lane columns of the widest LZMA2
   // layout's global rows; stream i runs in column i % 32, its neighbours'
   // cells left as garbage (columns are reused stream after stream)
-  const size_t rows = (make_layout(4, 0, 4, LZGPU_LDS_MASK).glb_cells + 1) & ~size_t(1);
+  // (rows for the widest table the planner puts on an LDS class: lc + lp <= 6
+  // with pb 4 -- LZMA2's lc + lp <= 4 fits inside -- as LzmaGpu_PlanBatchEx
+  // sizes slot_cells by the widest stream of the class)
+  const size_t rows = (make_layout(6, 0, 4, LZGPU_LDS_MASK).glb_cells + 1) & ~size_t(1);
   std::vector<uint16_t> slots(rows * kIlv, 0x5A5A);
 #endif
   for (size_t i = 0; i < n; ++i) {

@@ -84,7 +84,10 @@ def test_gpu_concurrent_calls_coalesce_and_match_oracle():
         if (res, dl, sl) != (wres, wdl, wsl) or out != wout or (res == 0 and st != wst):
             bad.append((k, cases[k][0], (res, st, dl, sl), (wres, wst, wdl, wsl)))
     assert not bad, bad[:5]
-    assert calls == len(cases) and batches < calls and biggest > 1, (batches, calls, biggest)
+    # every call reaches the device except LzmaDecode's own early exit on fewer
+    # than 5 input bytes (SZ_ERROR_INPUT_EOF before any decode, LzmaDec.c:980)
+    reach = sum(1 for c in cases if c[0] == "lzma2" or len(c[1]) >= 5)
+    assert calls == reach and batches < calls and biggest > 1, (batches, calls, biggest, reach)
 
 
 @pytest.mark.gpu

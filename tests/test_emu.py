@@ -58,7 +58,7 @@ def emu(request):
     # into the tree atomically
     out = os.path.join(vdir, f"liblane_emu_{request.param}.{os.getpid()}.so")
     subprocess.run(["make", "-s", "-f", "tests/emu/Makefile", f"EMU_OUT={out}",
-                    f"EMU_FLAGS={EMU_VARIANTS[request.param]}"], cwd=native.ROOT, check=True)
+                    f"EMU_FLAGS={EMU_VARIANTS[request.param]} {os.environ.get('LZGPU_EMU_EXTRA', '')}"], cwd=native.ROOT, check=True)
     if request.param == "default":
         tmp = f"{EMU_SO}.{os.getpid()}"
         shutil.copyfile(out, tmp)

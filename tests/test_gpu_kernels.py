@@ -81,10 +81,12 @@ def _check_plan(plan, kernel):
         assert all(c.lds_mask & STEP_BIT for c in cls), [hex(c.lds_mask) for c in cls]
         assert all((c.lds_mask & ~(STEP_BIT | ILV)) == M_THR for c in cls)
         if kernel == "step":
-            assert any(c.lds_mask & ILV and c.lanes_per_group == 32 for c in cls)
+            # interleaved rows wherever whole 32-lane groups run (the throughput rule)
+            assert all(bool(c.lds_mask & ILV) == (c.lanes_per_group in (32, 64)) for c in cls)
         if kernel == "step_slices":
             assert not any(c.lds_mask & ILV for c in cls)
         if kernel == "step_w16":
+            assert all(c.lanes_per_group <= 16 for c in cls)
             assert any(c.lds_mask & ILV and c.lanes_per_group == 16 for c in cls)
         return
     if kernel == "global":
