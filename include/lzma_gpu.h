@@ -169,13 +169,15 @@ void LzmaGpu_DecoderRelease(const CLzmaDec *p);
  * argument may be NULL.  Process-wide. */
 void LzmaGpu_DropinTransferStats(uint64_t *h2d_bytes, uint64_t *d2h_bytes, uint64_t *calls,
                                  int reset);
-/* Coalesced one-call decodes (round 4): LzmaDecode / LzmaUncompress /
- * Lzma2Decode calls made by several host threads at once share launches
- * (group commit per device: calls arriving while a batch runs form the next
- * batch; a lone caller's batch has one item).  Counts since start or the last
- * reset, summed over devices: batches launched, calls they carried, the
- * largest batch.  LZGPU_COALESCE=0 gives every call its own launch.  Any
- * argument may be NULL. */
+/* Coalesced calls (round 4): LzmaDecode / LzmaUncompress / Lzma2Decode calls
+ * made by several host threads at once share batch launches, and so do
+ * LzmaDec_DecodeToDic / LzmaDec_DecodeToBuf calls on different decoders (one
+ * launch of the session kernels, one wave per decoder) -- group commit per
+ * device: calls arriving while a launch runs form the next one; a lone
+ * caller's launch has one item.  Counts since start or the last reset, summed
+ * over devices and both kinds: launches, calls they carried, the largest
+ * launch.  LZGPU_COALESCE=0 gives every call its own launch.  Any argument may
+ * be NULL. */
 void LzmaGpu_CoalesceStats(uint64_t *batches, uint64_t *calls, uint64_t *max_batch, int reset);
 
 /* ---------------------------------------------------------------- drop-in LzmaLib.h */

@@ -451,6 +451,129 @@ void mirror_drop(const CLzmaDec* p) {
             R.v.end());
 }
 
+// ------------------------------------------------------------------ coalesced session calls
+//
+// Dictionary-interface calls (LzmaDec_DecodeToDic / LzmaDec_DecodeToBuf) made
+// by several host threads at once, each on its own decoder, share launches the
+// same way one-call decodes do: each call prepares its mirror (uploads its
+// input, table and history on its own stream) and hands the device session
+// state to its device's session queue; the call that finds no launch running
+// takes the whole queue as ONE launch of the session kernels (one 32-lane wave
+// per decoder) and every caller then downloads its own table and bytes.
+struct SessCall {
+  LzgpuSession q;  // in: the call; out: the state after it
+  uint32_t cells = 0;
+  int err = 0;     // launch failure
+  bool done = false;
+};
+
+struct SessCoalescer {
+  std::mutex mu;
+  std::condition_variable cv;
+  std::vector<SessCall*> pending;
+  bool running = false;
+  DevBuf arr;                  // the batch's LzgpuSession array
+  std::vector<LzgpuSession> h;  // its host copy
+  hipStream_t stream = nullptr;
+  std::atomic<uint64_t> batches{0}, items{0}, max_items{0};
+};
+
+std::atomic<SessCoalescer*> g_scoal[kLzgpuMaxDevices];
+SessCoalescer* sess_coalescer(int dev) {
+  static std::mutex mu;
+  if (dev < 0 || dev >= kLzgpuMaxDevices) return nullptr;
+  std::lock_guard<std::mutex> g(mu);
+  if (!g_scoal[dev].load()) g_scoal[dev].store(new (std::nothrow) SessCoalescer());
+  return g_scoal[dev].load();
+}
+
+// One launch for a batch of session calls (the leader, C.mu not held):
+// wave-cooperative sessions in one launch, tables wider than 64 KiB on the
+// one-lane global session kernel.
+void run_sess_batch(SessCoalescer& C, const std::vector<SessCall*>& b) {
+  const size_t k = b.size();
+  std::vector<size_t> coop, glob;
+  uint32_t lds_cells = 0;
+  for (size_t i = 0; i < k; ++i) {
+    if (b[i]->cells <= kSessCoopMaxCells) {
+      coop.push_back(i);
+      lds_cells = std::max(lds_cells, b[i]->cells);
+    } else {
+      glob.push_back(i);
+    }
+  }
+  C.h.resize(k);
+  size_t j = 0;
+  for (size_t i : coop) C.h[j++] = b[i]->q;
+  for (size_t i : glob) C.h[j++] = b[i]->q;
+  LzgpuSession* d = static_cast<LzgpuSession*>(C.arr.get(k * sizeof(LzgpuSession)));
+  const hipStream_t st = C.stream;
+  int e = (d && xfer(d, C.h.data(), k * sizeof(LzgpuSession), hipMemcpyHostToDevice, st) ==
+                    hipSuccess) ? 0 : 1;
+  if (!e && !coop.empty() &&
+      lzgpu_launch_session_coop(d, uint32_t(coop.size()), lds_cells, 0, st) != 0)
+    e = 1;
+  if (!e && !glob.empty() && lzgpu_launch_session(d + coop.size(), uint32_t(glob.size()), st) != 0)
+    e = 1;
+  if (!e && (xfer(C.h.data(), d, k * sizeof(LzgpuSession), hipMemcpyDeviceToHost, st) !=
+                 hipSuccess ||
+             hipStreamSynchronize(st) != hipSuccess))
+    e = 1;
+  if (e) (void)hipStreamSynchronize(st);
+  j = 0;
+  for (size_t i : coop) b[i]->q = C.h[j++];
+  for (size_t i : glob) b[i]->q = C.h[j++];
+  for (SessCall* c : b) c->err = e;
+}
+
+// Run one prepared session call through the device's queue; returns when
+// its launch has finished (c.err set on a launch failure).
+void sess_coalesced(SessCall& me, int dev) {
+  SessCoalescer* Cp = sess_coalescer(dev);
+  if (!Cp) {
+    me.err = 1;
+    return;
+  }
+  SessCoalescer& C = *Cp;
+  std::unique_lock<std::mutex> lk(C.mu);
+  if (!C.stream && hipStreamCreateWithFlags(&C.stream, hipStreamNonBlocking) != hipSuccess) {
+    (void)hipGetLastError();
+    C.stream = nullptr;
+    me.err = 1;
+    return;
+  }
+  C.pending.push_back(&me);
+  while (!me.done) {
+    if (C.running) {
+      C.cv.wait(lk);
+      continue;
+    }
+    C.running = true;
+    std::vector<SessCall*> batch;
+    batch.swap(C.pending);
+    if (!coalesce_on() && batch.size() > 1) {
+      for (SessCall* c : batch)
+        if (c != &me) C.pending.push_back(c);
+      batch.assign(1, &me);
+    }
+    lk.unlock();
+    try {
+      run_sess_batch(C, batch);
+    } catch (const std::exception&) {
+      for (SessCall* c : batch) c->err = 1;
+    }
+    C.batches++;
+    C.items += batch.size();
+    uint64_t mx = C.max_items.load();
+    while (batch.size() > mx && !C.max_items.compare_exchange_weak(mx, batch.size())) {
+    }
+    lk.lock();
+    for (SessCall* c : batch) c->done = true;
+    C.running = false;
+    C.cv.notify_all();
+  }
+}
+
 // One LzmaDec_DecodeToDic (mode 0) or LzmaDec_DecodeToBuf (mode 1) call on the
 // GPU over a host CLzmaDec, through its mirror.
 SRes gpu_session_call(CLzmaDec* p, int mode, SizeT dicLimit, const Byte* src, SizeT in_size,
@@ -563,25 +686,30 @@ SRes gpu_session_call(CLzmaDec* p, int mode, SizeT dicLimit, const Byte* src, Si
   q.out = d_io + in_pad;
   q.out_len = out_room;
   const SizeT pos0 = p->dicPos;
-  if (xfer(d_sess, &q, sizeof q, hipMemcpyHostToDevice, st) != hipSuccess)
-    return fail("LzmaDec: upload session");
-  const int lr = cells <= kSessCoopMaxCells ? lzgpu_launch_session_coop(d_sess, 1, cells, 1, st)
-                                            : lzgpu_launch_session(d_sess, 1, st);
-  if (lr != 0) return fail("LzmaDec: session kernel launch failed");
-  // state + table back in one copy (the table sits right after the state)
+  (void)d_sess;
+  // this call's uploads are complete before it joins the device's session
+  // queue; the launch (shared with concurrent calls on other decoders) runs
+  // on the queue's stream
+  if (hipStreamSynchronize(st) != hipSuccess) return fail("LzmaDec: uploads");
+  SessCall call;
+  call.q = q;
+  call.cells = cells;
+  sess_coalesced(call, dev);
+  if (call.err) return fail("LzmaDec: session kernel");
+  q = call.q;
+  // the table back (the kernel wrote it to the mirror's device copy)
   std::vector<uint8_t> back;
   try {
     back.resize(kSessBytes + size_t(cells) * 2);
   } catch (const std::exception&) {
-    (void)hipStreamSynchronize(st);
     m->history = m->probs_dev = false;
     set_error("LzmaDec: host allocation failed");
     return SZ_ERROR_MEM;
   }
-  if (xfer(back.data(), blk, back.size(), hipMemcpyDeviceToHost, st) != hipSuccess ||
+  if (xfer(back.data() + kSessBytes, d_probs, size_t(cells) * 2, hipMemcpyDeviceToHost, st) !=
+          hipSuccess ||
       hipStreamSynchronize(st) != hipSuccess)
-    return fail("LzmaDec: session kernel");
-  memcpy(&q, back.data(), sizeof q);
+    return fail("LzmaDec: download probs");
   // the decoded bytes: DecodeToDic's new dictionary bytes, DecodeToBuf's output
   if (mode == 0) {
     if (q.dic_pos < pos0 || q.dic_pos > p->dicBufSize) return fail("LzmaDec: bad session state");
@@ -741,6 +869,13 @@ void LzmaGpu_CoalesceStats(uint64_t* batches, uint64_t* calls, uint64_t* max_bat
   uint64_t b = 0, c = 0, m = 0;
   for (int dev = 0; dev < kLzgpuMaxDevices; ++dev) {
     Coalescer* C = coalescer_if(dev);
+    if (!C) continue;
+    b += reset ? C->batches.exchange(0) : C->batches.load();
+    c += reset ? C->items.exchange(0) : C->items.load();
+    m = std::max<uint64_t>(m, reset ? C->max_items.exchange(0) : C->max_items.load());
+  }
+  for (int dev = 0; dev < kLzgpuMaxDevices; ++dev) {
+    SessCoalescer* C = g_scoal[dev].load();
     if (!C) continue;
     b += reset ? C->batches.exchange(0) : C->batches.load();
     c += reset ? C->items.exchange(0) : C->items.load();

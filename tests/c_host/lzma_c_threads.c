@@ -9,9 +9,13 @@
  *                                         in place (oracle/Makefile.ref): the
  *                                         CPU baseline on the same host cores
  *
- *   lzma_c_threads THREADS SRC LENS PROPS OUT_SIZES REPEAT
+ *   lzma_c_threads THREADS SRC LENS PROPS OUT_SIZES REPEAT [MODE]
  * SRC: streams back to back; LENS / OUT_SIZES: uint64 per stream; PROPS: 5
- * bytes per stream.  Prints one JSON line on STDERR (the fork's reference
+ * bytes per stream.  MODE "one" (default): one LzmaDecode per stream; "buf":
+ * the fork's zlib-like streaming shape per stream (LzmaDec_Allocate + Init,
+ * then LzmaDec_DecodeToBuf with 1 KiB of input and 1 KiB of output per call,
+ * 7zDec.c:567-648) -- each thread its own decoder, so concurrent calls run on
+ * different CLzmaDec objects.  Prints one JSON line on STDERR (the fork's reference
  * decoder prints a debug line to stdout per call, LzmaDec.c:945): threads,
  * streams, decoded bytes, seconds, MB/s, failures, and the XOR of every
  * stream's (index-salted) CRC-32 so the two builds can be compared.
@@ -60,7 +64,7 @@ static unsigned char *read_file(const char *path, size_t *n) {
 }
 
 typedef struct {
-  int tid, nthreads, repeat;
+  int tid, nthreads, repeat, buf_mode;
   size_t n;
   const unsigned char *src, *props;
   const uint64_t *off, *len, *out;
@@ -80,8 +84,33 @@ static void *worker(void *arg) {
     for (i = (size_t)w->tid; i < w->n; i += (size_t)w->nthreads) {
       SizeT dl = w->out[i], sl = w->len[i];
       ELzmaStatus st;
-      SRes res = LzmaDecode(buf, &dl, w->src + w->off[i], &sl, w->props + 5 * i, 5,
-                            LZMA_FINISH_ANY, &st, &g_Alloc);
+      SRes res;
+      if (!w->buf_mode) {
+        res = LzmaDecode(buf, &dl, w->src + w->off[i], &sl, w->props + 5 * i, 5,
+                         LZMA_FINISH_ANY, &st, &g_Alloc);
+      } else {
+        CLzmaDec dec;
+        size_t ip = 0, op = 0;
+        LzmaDec_Construct(&dec);
+        res = LzmaDec_Allocate(&dec, w->props + 5 * i, 5, &g_Alloc);
+        if (res == SZ_OK) {
+          LzmaDec_Init(&dec);
+          for (;;) {
+            SizeT s1 = w->len[i] - ip, d1 = w->out[i] - op;
+            if (s1 > 1024) s1 = 1024;
+            if (d1 > 1024) d1 = 1024;
+            res = LzmaDec_DecodeToBuf(&dec, buf + op, &d1, w->src + w->off[i] + ip, &s1,
+                                      LZMA_FINISH_ANY, &st);
+            ip += s1;
+            op += d1;
+            if (res != SZ_OK || st == LZMA_STATUS_FINISHED_WITH_MARK || op == w->out[i] ||
+                (s1 == 0 && d1 == 0))
+              break;
+          }
+          LzmaDec_Free(&dec, &g_Alloc);
+        }
+        dl = op;
+      }
       if (res != SZ_OK || dl != w->out[i]) w->fails++;
       w->bytes += dl;
       if (r == 0) w->crc ^= crc32_of(buf, dl, (unsigned)i);
@@ -101,8 +130,8 @@ int main(int argc, char **argv) {
   Work *w;
   struct timespec a, b;
   double sec;
-  if (argc != 7) {
-    fprintf(stderr, "usage: %s THREADS SRC LENS PROPS OUT_SIZES REPEAT\n", argv[0]);
+  if (argc != 7 && argc != 8) {
+    fprintf(stderr, "usage: %s THREADS SRC LENS PROPS OUT_SIZES REPEAT [one|buf]\n", argv[0]);
     return 2;
   }
   T = atoi(argv[1]);
@@ -124,6 +153,7 @@ int main(int argc, char **argv) {
     w[t].tid = t;
     w[t].nthreads = T;
     w[t].repeat = repeat;
+    w[t].buf_mode = argc == 8 && strcmp(argv[7], "buf") == 0;
     w[t].n = n;
     w[t].src = src;
     w[t].props = props;
@@ -146,10 +176,11 @@ int main(int argc, char **argv) {
     uint64_t nb = 0, nc = 0, mx = 0;
     if (LzmaGpu_CoalesceStats) LzmaGpu_CoalesceStats(&nb, &nc, &mx, 0);
     fprintf(stderr,
-            "{\"threads\": %d, \"streams\": %zu, \"repeat\": %d, \"bytes\": %llu, "
+            "{\"mode\": \"%s\", \"threads\": %d, \"streams\": %zu, \"repeat\": %d, \"bytes\": %llu, "
             "\"seconds\": %.6f, \"MBps\": %.2f, \"fails\": %llu, \"crc_xor\": \"%08x\", "
             "\"batches\": %llu, \"batched_calls\": %llu, \"max_batch\": %llu}\n",
-            T, n, repeat, (unsigned long long)bytes, sec, sec > 0 ? (double)bytes / sec / 1e6 : 0.0,
+            (argc == 8 && strcmp(argv[7], "buf") == 0) ? "buf" : "one", T, n, repeat,
+            (unsigned long long)bytes, sec, sec > 0 ? (double)bytes / sec / 1e6 : 0.0,
             (unsigned long long)fails, crc, (unsigned long long)nb, (unsigned long long)nc,
             (unsigned long long)mx);
   }

@@ -78,12 +78,12 @@ def write_stream_set(tmp, comps, props, outs):
     return f
 
 
-def run_c_threads(binary, threads, f, repeat=1, env=None, timeout=300):
+def run_c_threads(binary, threads, f, repeat=1, env=None, timeout=300, mode="one"):
     import json
     # the result line goes to stderr: the reference build prints a debug line
     # per call to stdout (LzmaDec.c:945), discarded here
     r = subprocess.run([binary, str(threads), f["src"], f["lens"], f["props"], f["outs"],
-                        str(repeat)], stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True,
+                        str(repeat), mode], stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True,
                        timeout=timeout, env=env)
     assert r.returncode == 0, r.stderr
     return json.loads([ln for ln in r.stderr.splitlines() if ln.startswith("{")][-1])

@@ -7,7 +7,9 @@ its own LzmaDecode results (LzmaDec.c:972-1002, LzmaLib.c:41-46).
 GPU: 400 calls from 48 Python threads (ctypes drops the GIL) over mixed
 lc/lp/pb streams, corrupt and truncated ones, both finish modes and LZMA2
 items, each checked against the oracle; the coalescer's counters show batches
-of more than one call.  The unchanged multi-threaded C caller
+of more than one call.  The same for the dictionary interface: threads each
+running the fork's DecodeToBuf loop on their own decoder share session
+launches.  The unchanged multi-threaded C caller
 (tests/c_host/lzma_c_threads.c) linked to the library agrees with the same
 source linked to the reference's LzmaDec.c, stream by stream (CRCs)."""
 import lzma
@@ -103,11 +105,12 @@ def test_gpu_c_threads_caller_matches_reference_build(tmp_path):
     want = 0
     for i in range(600):
         want ^= zlib.crc32(plain[i * 4096:(i + 1) * 4096].tobytes(), i)
-    for threads in (1, 16, 64):
-        d = TC.run_c_threads(TC.THREADS_BIN, threads, f)
-        assert d["fails"] == 0 and d["crc_xor"] == "%08x" % want, d
-        if threads > 1:
-            assert d["max_batch"] > 1, d
-    if os.path.exists(TC.THREADS_REF):
-        d = TC.run_c_threads(TC.THREADS_REF, 16, f)
-        assert d["fails"] == 0 and d["crc_xor"] == "%08x" % want, d
+    for mode in ("one", "buf"):
+        for threads in (1, 16, 64):
+            d = TC.run_c_threads(TC.THREADS_BIN, threads, f, mode=mode)
+            assert d["fails"] == 0 and d["crc_xor"] == "%08x" % want, d
+            if threads > 1:
+                assert d["max_batch"] > 1, d
+        if os.path.exists(TC.THREADS_REF):
+            d = TC.run_c_threads(TC.THREADS_REF, 16, f, mode=mode)
+            assert d["fails"] == 0 and d["crc_xor"] == "%08x" % want, d
