@@ -111,7 +111,10 @@ __device__ __forceinline__ int lz2_decode_to_dic(Lz2StateT<Lo>& p, uint64_t dic_
       if (in_cur > out_cur) in_cur = out_cur;
       if (in_cur == 0) return kErrData;
       // stored chunk (LzmaDec_UpdateWithUncompressed, Lzma2Dec.c:159-166)
-      for (uint64_t i = 0; i < in_cur; ++i) p.dec.dic[p.dec.pos + i] = src[i];
+      for (uint64_t i = 0; i < in_cur; ++i) {
+        p.dec.dic[p.dec.pos + i] = src[i];
+        if constexpr (win_on<M>()) win_put(p.dec.win, src[i]);
+      }
       p.dec.pos += in_cur;
       if (p.dec.full == 0 && p.dec.dict_size - p.dec.total <= in_cur)
         p.dec.full = p.dec.dict_size;

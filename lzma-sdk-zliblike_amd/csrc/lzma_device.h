@@ -222,6 +222,37 @@ constexpr uint32_t kIlvLaneCells = 1u;
 #define LZGPU_PROF 0
 #endif
 
+// LDS history window (round 4, placement bit kWinBit, the wave-cooperative
+// kernels): the most recent decoded bytes are kept in LDS as well as in the
+// dictionary, so a match copy (and the matched literal's byte) at a distance
+// the window covers is read from LDS instead of global memory -- where, in the
+// in-order vmcnt queue, every such load waited for the wave's earlier output
+// stores.  The window is a write-through cache of the
+// dictionary's last `av` bytes (<= mask + 1): slot = write counter & mask.
+// Every byte the decoder writes goes to both; reads it cannot serve fall back
+// to the dictionary, which is always complete.
+constexpr uint32_t kWinBit = 0x08000000u;
+#ifdef LZGPU_HOST_EMU
+typedef uint8_t lds_u8;
+#else
+typedef __attribute__((address_space(3))) uint8_t lds_u8;
+#endif
+struct LzWin {
+  lds_u8* b;
+  uint32_t mask;  // window bytes - 1 (a power of two)
+  uint32_t t;     // bytes written through the window
+  uint32_t av;    // of them, still held (the last av)
+};
+__device__ __forceinline__ void win_put(LzWin& w, uint32_t v) {
+  w.b[w.t & w.mask] = uint8_t(v);
+  ++w.t;
+  w.av += (w.av <= w.mask) ? 1u : 0u;
+}
+template <uint32_t M>
+__host__ __device__ constexpr bool win_on() {
+  return (M & kWinBit) != 0u;
+}
+
 // Per-lane decoder state (CLzmaDec fields, LzmaDec.h:50-69).  lo = the LDS
 // table (pointer type Lo: lds_u16*; or gu16* aliasing gl when everything is
 // global), gl = the global table.
@@ -242,6 +273,7 @@ struct LzStateT {
   uint32_t need_rc_init, need_state_init;
   uint32_t tmp_n;
   uint8_t tmp[kLookahead];
+  LzWin win;  // kWinBit placements only
 #if LZGPU_PROF
   // [0..4] cycles: literal batches, match decode, copies + tail, calls, refills;
   // [5..13] wave-level counts: batch iterations, active / matched-literal lanes
@@ -993,46 +1025,75 @@ __device__ __forceinline__ uint32_t lz_mod_small(uint32_t j, uint32_t d, float r
 // Lanes of one wave see each other's global stores in order (one vector L1).
 // Returns the last byte copied; `mb` gets the next matched byte.
 constexpr uint32_t kCoopLanes = 32u;
+// WIN: the LDS history window `w` is kept up to date (every copied byte is
+// also written there) and serves the loads when dist <= w.av (the byte at
+// window index k of the match is at distance dist - k < dist: held).
+template <bool WIN = false>
 __device__ __forceinline__ uint32_t lz_copy_coop(gbyte* dic, uint64_t pos, uint64_t from,
                                                  uint32_t n, uint32_t dist, uint64_t cap,
-                                                 uint32_t& mb) {
+                                                 uint32_t& mb, LzWin* w = nullptr) {
   const bool per = dist <= n;  // the match overlaps itself: period dist
 #ifdef LZGPU_HOST_EMU
   // one lane plays every lane: all loads (sources lie before pos), then stores
   uint8_t v[kLenDone];  // n <= 273
+  const bool inwin = WIN && dist <= w->av;
   for (uint32_t j = 0; j <= n; ++j) {
-    uint64_t a = from + (per ? j % dist : j);
-    v[j] = dic[a >= cap ? a - cap : a];
+    const uint32_t k = per ? j % dist : j;
+    uint64_t a = from + k;
+    v[j] = inwin ? w->b[(w->t - dist + k) & w->mask] : dic[a >= cap ? a - cap : a];
   }
   for (uint32_t j = 0; j < n; ++j) dic[pos + j] = v[j];
+  if constexpr (WIN) {
+    for (uint32_t j = 0; j < n; ++j) w->b[(w->t + j) & w->mask] = v[j];
+    w->t += n;
+    w->av = (w->av + n > w->mask + 1) ? w->mask + 1 : w->av + n;
+  }
   mb = v[n];
   return v[n - 1];
 #else
   const float rd = per ? __builtin_amdgcn_rcpf(float(dist)) : 0.f;
   const uint32_t lane = lz_lane_id() & (kCoopLanes - 1u);
-  // window index of byte j (j <= n); j > n: a harmless in-window address
+  // the match's index k of byte j (j <= n); j > n: a harmless in-range index
+  auto k_of = [&](uint32_t j) -> uint32_t {
+    return j > n ? 0u : (per ? lz_mod_small(j, dist, rd) : j);
+  };
   auto src_of = [&](uint32_t j) -> uint64_t {
-    const uint32_t k = j > n ? 0u : (per ? lz_mod_small(j, dist, rd) : j);
-    const uint64_t a = from + k;
+    const uint64_t a = from + k_of(j);
     return a >= cap ? a - cap : a;
+  };
+  // window-served loads: every lane decides alike (wave-uniform condition)
+  const bool inwin = WIN && dist <= w->av;
+  auto load = [&](uint32_t j) -> uint32_t {
+    if constexpr (WIN) {
+      if (inwin) return w->b[(w->t - dist + k_of(j)) & w->mask];
+    }
+    return dic[src_of(j)];
+  };
+  auto store = [&](uint32_t j, uint32_t v) {
+    dic[pos + j] = uint8_t(v);
+    if constexpr (WIN) w->b[(w->t + j) & w->mask] = uint8_t(v);
   };
   uint32_t my_last = 0, my_mb = 0;
   // the first 64 bytes (almost every match): both loads before any store
   const uint32_t j0 = lane, j1 = lane + kCoopLanes;
-  const uint32_t v0 = dic[src_of(j0)];
+  const uint32_t v0 = load(j0);
   uint32_t v1 = 0;
-  if (n >= kCoopLanes) v1 = dic[src_of(j1)];
-  if (j0 < n) dic[pos + j0] = uint8_t(v0);
-  if (j1 < n) dic[pos + j1] = uint8_t(v1);
+  if (n >= kCoopLanes) v1 = load(j1);
+  if (j0 < n) store(j0, v0);
+  if (j1 < n) store(j1, v1);
   my_last = (j0 + 1 == n) ? v0 : ((j1 + 1 == n) ? v1 : 0u);
   my_mb = (j0 == n) ? v0 : ((j1 == n) ? v1 : 0u);
   // longer matches: 32 bytes per round trip
   for (uint32_t b = 2 * kCoopLanes; b <= n; b += kCoopLanes) {
     const uint32_t j = b + lane;
-    const uint32_t v = dic[src_of(j)];
-    if (j < n) dic[pos + j] = uint8_t(v);
+    const uint32_t v = load(j);
+    if (j < n) store(j, v);
     my_last = (j + 1 == n) ? v : my_last;
     my_mb = (j == n) ? v : my_mb;
+  }
+  if constexpr (WIN) {
+    w->t += n;
+    w->av = (w->av + n > w->mask + 1) ? w->mask + 1 : w->av + n;
   }
   mb = uint32_t(__builtin_amdgcn_readlane(int(my_mb), int(n & (kCoopLanes - 1u))));
   return uint32_t(__builtin_amdgcn_readlane(int(my_last), int((n - 1) & (kCoopLanes - 1u))));
@@ -1068,7 +1129,7 @@ __device__ __forceinline__ void lz_literal(Rc<Rd>& rc, const Tab<M, Lo>& T, uint
                                            uint32_t& prev, uint32_t& total, uint32_t full,
                                            uint32_t lc, uint32_t lp_mask, gbyte* dic,
                                            uint64_t& pos, uint64_t cap, uint32_t r0,
-                                           uint32_t mb_pf) {
+                                           uint32_t mb_pf, LzWin* w = nullptr) {
   uint32_t sym = 1;
   uint32_t ctx = 0;
   if (full != 0 || total != 0) ctx = ((total & lp_mask) << lc) + (prev >> (8 - lc));
@@ -1126,6 +1187,7 @@ __device__ __forceinline__ void lz_literal(Rc<Rd>& rc, const Tab<M, Lo>& T, uint
   }
   prev = sym & 0xFFu;
   lz_put(dic + pos, prev);
+  if constexpr (win_on<M>()) win_put(*w, prev);
   pos++;
   total++;
 }
@@ -1577,7 +1639,8 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
           tB = lz_clock();
           did_lit = true;
 #endif
-          lz_literal<M>(rc, T, st, prev, total, full, lc, lp_mask, dic, pos, cap, r0, mb_pf);
+          lz_literal<M>(rc, T, st, prev, total, full, lc, lp_mask, dic, pos, cap, r0, mb_pf,
+                        &s.win);
 #if LZGPU_PROF && !defined(LZGPU_HOST_EMU)
           tC = lz_clock();
 #endif
@@ -1637,7 +1700,8 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
           if constexpr ((M & kCoopBit) != 0u) {
             // short rep = a one-byte copy: the byte and the next matched byte
             // in one load batch
-            prev = lz_copy_coop(dic, pos, ring_back(pos, r0, cap), 1, r0, cap, mb_pf);
+            prev = lz_copy_coop<win_on<M>()>(dic, pos, ring_back(pos, r0, cap), 1, r0, cap,
+                                             mb_pf, &s.win);
             pos++;
           } else {
             prev = dic[ring_back(pos, r0, cap)];
@@ -1824,7 +1888,7 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
       total += n;
       len -= n;
       if constexpr ((M & kCoopBit) != 0u) {
-        prev = lz_copy_coop(dic, pos, from, n, r0, cap, mb_pf);
+        prev = lz_copy_coop<win_on<M>()>(dic, pos, from, n, r0, cap, mb_pf, &s.win);
         pos += n;
       } else {
         prev = lz_copy(dic, pos, from, n, r0, cap);
@@ -1849,7 +1913,7 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
   return kOk;
 }
 
-template <class Lo>
+template <uint32_t M = 0u, class Lo>
 __device__ __forceinline__ void lz_flush_pending(LzStateT<Lo>& s, uint64_t limit) {
   if (s.pending == 0 || s.pending >= kLenDone) return;
   uint32_t n = s.pending;
@@ -1858,7 +1922,9 @@ __device__ __forceinline__ void lz_flush_pending(LzStateT<Lo>& s, uint64_t limit
   s.total += n;
   s.pending -= n;
   while (n-- != 0) {
-    s.dic[s.pos] = s.dic[ring_back(s.pos, s.rep0, s.cap)];
+    const uint8_t b = s.dic[ring_back(s.pos, s.rep0, s.cap)];
+    s.dic[s.pos] = b;
+    if constexpr (win_on<M>()) win_put(s.win, b);
     s.pos++;
   }
 }
@@ -1874,7 +1940,7 @@ __device__ __forceinline__ int lz_run_split(LzStateT<Lo>& s, uint64_t limit, Rd&
     }
     if (lz_run<M>(s, lim, rd, in_limit) != kOk) return kErrData;
     if (s.total >= s.dict_size) s.full = s.dict_size;
-    lz_flush_pending(s, limit);
+    lz_flush_pending<M>(s, limit);
   } while (s.pos < limit && rd.used() < in_limit && s.pending < kLenDone);
   if (s.pending > kLenDone) s.pending = kLenDone;
   return kOk;
@@ -2114,7 +2180,7 @@ __device__ __forceinline__ int lz_decode_to_dic(LzStateT<Lo>& s, uint64_t dic_li
                                                 int& status) {
   uint64_t avail = src_len;
   src_len = 0;
-  lz_flush_pending(s, dic_limit);
+  lz_flush_pending<M>(s, dic_limit);
   status = kStNone;
 
   while (s.pending != kLenDone) {

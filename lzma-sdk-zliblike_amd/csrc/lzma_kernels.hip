@@ -102,18 +102,24 @@ __global__ void __launch_bounds__(64, W) lzgpu_decode_lds_kernel(
 // flow and memory traffic are those of one lane -- except the literal tree,
 // whose levels are decided several at a time by speculating over the lanes
 // (spec_stage in lzma_device.h).  Lane 0 takes the next stream from the queue.
+// Under kWinBit the workgroup's LDS holds, after the table (`stride` cells,
+// 16-byte aligned), the LDS history window of `win_bytes` (lzma_device.h):
+// match copies and matched bytes within its reach are LDS reads.
 template <int W, uint32_t M, bool K2>
 __global__ void __launch_bounds__(32, W) lzgpu_decode_coop_kernel(
     const LzmaGpuStreamDesc* __restrict__ descs, const uint32_t* __restrict__ order, uint32_t n,
     const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, uint16_t* __restrict__ ws,
-    LzmaGpuResult* __restrict__ results, uint32_t stride, uint32_t* __restrict__ queue) {
+    LzmaGpuResult* __restrict__ results, uint32_t stride, uint32_t* __restrict__ queue,
+    uint32_t win_bytes) {
   extern __shared__ uint32_t lz_smem[];
   lds_u16* lo = (lds_u16*)((uint16_t*)lz_smem);
+  lds_u8* win = (lds_u8*)((uint8_t*)lz_smem) + ((size_t(stride) * 2 + 15) & ~size_t(15));
   uint32_t idx = blockIdx.x;
   while (idx < n) {
     const uint32_t id = order ? order[idx] : idx;
     const LzmaGpuStreamDesc d = descs[id];
-    const LzmaGpuResult r = lane_decode_lds<M, K2>(d, src, dst, ws, lo, stride);
+    const LzmaGpuResult r =
+        lane_decode_lds<M, K2>(d, src, dst, ws, lo, stride, nullptr, win, win_bytes);
     uint32_t next = 0;
     if (threadIdx.x == 0) {
       results[id] = r;
@@ -139,11 +145,17 @@ __global__ void __launch_bounds__(64) lzgpu_session_kernel(LzgpuSession* __restr
 // access an LDS round trip instead of a global one), written back.  Placement
 // 0x7FF keeps the all-global layout's offsets, so the copy is a straight one.
 // Dynamic LDS: the widest table of the batch's sessions (the launcher checks).
+// WIN: the LDS history window (win_bytes, after the table) is preloaded per
+// call with the dictionary bytes a match can reach (lane_session).
 constexpr uint32_t kSessCoopMask = LZGPU_LDS_MASK_ALL | kCoopBit;
+template <bool WIN>
 __global__ void __launch_bounds__(32) lzgpu_session_coop_kernel(LzgpuSession* __restrict__ sess,
-                                                                 uint32_t n, uint32_t lds_cells) {
+                                                                 uint32_t n, uint32_t lds_cells,
+                                                                 uint32_t win_bytes) {
   extern __shared__ uint32_t lz_smem[];
   lds_u16* lo = (lds_u16*)((uint16_t*)lz_smem);
+  lds_u8* win = (lds_u8*)((uint8_t*)lz_smem) + ((size_t(lds_cells) * 2 + 15) & ~size_t(15));
+  constexpr uint32_t MS = kSessCoopMask | (WIN ? kWinBit : 0u);
   for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
     LzgpuSession q = sess[i];
     const uint32_t cells = table_cells(q.lc, q.lp, q.pb);
@@ -157,7 +169,7 @@ __global__ void __launch_bounds__(32) lzgpu_session_coop_kernel(LzgpuSession* __
     gu16* gp = (gu16*)q.probs;
     for (uint32_t j = threadIdx.x; j < cells; j += blockDim.x) lo[j] = gp[j];
     __syncthreads();
-    lane_session<kSessCoopMask>(q, lo);
+    lane_session<MS>(q, lo, win, win_bytes);
     __syncthreads();
     for (uint32_t j = threadIdx.x; j < cells; j += blockDim.x) gp[j] = lo[j];
     if (threadIdx.x == 0) sess[i] = q;
@@ -165,18 +177,45 @@ __global__ void __launch_bounds__(32) lzgpu_session_coop_kernel(LzgpuSession* __
   }
 }
 
+// Window for a launch of `grid` one-wave workgroups whose tables take
+// `table_bytes` of LDS: the largest power of two that still leaves room for
+// every workgroup a CU holds at once (one each while the grid fits the CUs),
+// at most 128 KiB; 0 (no window) below 4 KiB.  LZGPU_WIN=0 disables it.
+static uint32_t window_bytes(uint64_t grid, size_t table_bytes, uint32_t groups_per_cu) {
+  static const bool off = [] {
+    const char* e = getenv("LZGPU_WIN");
+    return e && e[0] == '0';
+  }();
+  if (off) return 0;
+  const uint32_t cus = lzgpu_host::device_cus();
+  uint64_t per_cu = (grid + cus - 1) / cus;
+  if (groups_per_cu && per_cu > groups_per_cu) per_cu = groups_per_cu;
+  if (per_cu == 0) per_cu = 1;
+  const size_t share = (size_t(160 * 1024) / per_cu) & ~size_t(511);
+  const size_t tb = (table_bytes + 15) & ~size_t(15);
+  if (share <= tb + 4096) return 0;
+  uint32_t w = 1u << 17;
+  while (w > share - tb) w >>= 1;
+  return w >= 4096 ? w : 0;
+}
+
 extern "C" int lzgpu_launch_session_coop(LzgpuSession* d_sess, uint32_t n, uint32_t lds_cells,
                                          uint32_t max_groups, hipStream_t stream) {
   if (n == 0) return 0;
-  const size_t lds = size_t(lds_cells) * 2;
-  if (lds_cells == 0 || lds > 160 * 1024) return -1;
-  if (lds > 64 * 1024 &&
-      allow_full_lds(reinterpret_cast<const void*>(lzgpu_session_coop_kernel)) != 0)
-    return -1;
+  if (lds_cells == 0 || size_t(lds_cells) * 2 > 160 * 1024) return -1;
   uint32_t grid = n;
   if (max_groups && grid > max_groups) grid = max_groups;
-  hipLaunchKernelGGL(lzgpu_session_coop_kernel, dim3(grid), dim3(32), lds, stream, d_sess, n,
-                     lds_cells);
+  const uint32_t win = window_bytes(grid, size_t(lds_cells) * 2, 0);
+  const size_t lds = win ? ((size_t(lds_cells) * 2 + 15) & ~size_t(15)) + win : size_t(lds_cells) * 2;
+  const void* kfn = win ? reinterpret_cast<const void*>(lzgpu_session_coop_kernel<true>)
+                        : reinterpret_cast<const void*>(lzgpu_session_coop_kernel<false>);
+  if (lds > 64 * 1024 && allow_full_lds(kfn) != 0) return -1;
+  if (win)
+    hipLaunchKernelGGL(lzgpu_session_coop_kernel<true>, dim3(grid), dim3(32), lds, stream, d_sess,
+                       n, lds_cells, win);
+  else
+    hipLaunchKernelGGL(lzgpu_session_coop_kernel<false>, dim3(grid), dim3(32), lds, stream,
+                       d_sess, n, lds_cells, 0u);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -225,24 +264,28 @@ static int launch_lds(const LzmaGpuStreamDesc* d_descs, const uint32_t* d_order,
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-template <int W, uint32_t M, bool K2>
+// MW: the same placement with the LDS history window, launched instead when
+// the launch leaves room for one (window_bytes); 0 = no window build.
+template <int W, uint32_t M, bool K2, uint32_t MW = 0u>
 static int launch_coop(const LzmaGpuStreamDesc* d_descs, const uint32_t* d_order, uint32_t n,
                        const uint8_t* d_src, uint8_t* d_dst, uint16_t* d_ws,
                        LzmaGpuResult* d_results, uint32_t stride, uint32_t groups_per_cu,
                        uint32_t max_groups, uint32_t* d_queue, hipStream_t stream) {
-  if (allow_full_lds(reinterpret_cast<const void*>(lzgpu_decode_coop_kernel<W, M, K2>)) != 0)
-    return -1;
+  uint32_t grid = n;
+  if (max_groups && grid > max_groups) grid = max_groups;
+  const uint32_t win = MW ? window_bytes(grid, size_t(stride) * 2, groups_per_cu) : 0u;
+  auto kfn = win ? lzgpu_decode_coop_kernel<W, (MW ? MW : M), K2> : lzgpu_decode_coop_kernel<W, M, K2>;
+  if (allow_full_lds(reinterpret_cast<const void*>(kfn)) != 0) return -1;
   if (hipMemsetAsync(d_queue, 0, sizeof(uint32_t), stream) != hipSuccess) return -1;
   size_t lds = size_t(stride) * 2;
-  if (groups_per_cu) {
+  if (win) {
+    lds = ((lds + 15) & ~size_t(15)) + win;
+  } else if (groups_per_cu) {
     const size_t share = (size_t(160 * 1024) / groups_per_cu) & ~size_t(511);
     if (share > lds) lds = share;
   }
-  uint32_t grid = n;
-  if (max_groups && grid > max_groups) grid = max_groups;
-  auto kfn = lzgpu_decode_coop_kernel<W, M, K2>;
   hipLaunchKernelGGL(kfn, dim3(grid), dim3(32), lds, stream, d_descs, d_order, n, d_src, d_dst,
-                     d_ws, d_results, stride, d_queue);
+                     d_ws, d_results, stride, d_queue, win);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -299,13 +342,16 @@ static int launch_class(const LzmaGpuStreamDesc* d_descs, const uint32_t* d_orde
                                   groups_per_cu, max_groups, d_queue, stream);
   }
   if (lds_mask == (LZGPU_LDS_MASK_ALL | kCoopBit)) {
+    // the whole table in LDS, plus the history window where the launch has room
     constexpr uint32_t MC = LZGPU_LDS_MASK_ALL | kCoopBit;
     const uint32_t w = (groups_per_cu + 3) / 4;
     if (w <= 2)
-      return launch_coop<2, MC, K2>(d_descs, d_order, n, d_src, d_dst, d_ws, d_results, stride,
-                                    groups_per_cu, max_groups, d_queue, stream);
-    return launch_coop<4, MC, K2>(d_descs, d_order, n, d_src, d_dst, d_ws, d_results, stride,
-                                  groups_per_cu, max_groups, d_queue, stream);
+      return launch_coop<2, MC, K2, MC | kWinBit>(d_descs, d_order, n, d_src, d_dst, d_ws,
+                                                  d_results, stride, groups_per_cu, max_groups,
+                                                  d_queue, stream);
+    return launch_coop<4, MC, K2, MC | kWinBit>(d_descs, d_order, n, d_src, d_dst, d_ws, d_results,
+                                                stride, groups_per_cu, max_groups, d_queue,
+                                                stream);
   }
   if (lds_mask == LZGPU_LDS_MASK_LAT)
     return launch_lds_w<LZGPU_LDS_MASK_LAT, K2>(d_descs, d_order, n, d_src, d_dst, d_ws,

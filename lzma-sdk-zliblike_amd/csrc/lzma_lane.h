@@ -97,12 +97,17 @@ __host__ __device__ __forceinline__ uint32_t lzma2_lds_cells(uint32_t m) {
 // One LZMA (or LZMA2) batch item with the LDS-placed sections (LZGPU_LDS_MASK)
 // in the lane's LDS slice (lo_cap cells) and the others in its global
 // workspace slice.  The planner only routes items here whose LDS part fits.
+// Under kWinBit (wave-cooperative kernels) `win` is the LDS history window of
+// `win_bytes` (a power of two, >= 1024) for this item, empty at its start.
 template <uint32_t M = LZGPU_LDS_MASK, bool K2 = true>
 __device__ __forceinline__ LzmaGpuResult lane_decode_lds(const LzmaGpuStreamDesc& d,
                                                          const uint8_t* __restrict__ src,
                                                          uint8_t* __restrict__ dst,
                                                          uint16_t* __restrict__ ws, lds_u16* lo,
-                                                         uint32_t lo_cap, gu16* gcol = nullptr) {
+                                                         uint32_t lo_cap, gu16* gcol = nullptr,
+                                                         lds_u8* win = nullptr,
+                                                         uint32_t win_bytes = 0) {
+  const LzWin w0 = {win, win_bytes - 1, 0, 0};
   // global sections: the stream's own workspace slice, or under kIlvBit the
   // lane's column of its group's interleaved slot rows
   auto gtab = [&]() -> gu16* {
@@ -132,6 +137,7 @@ __device__ __forceinline__ LzmaGpuResult lane_decode_lds(const LzmaGpuStreamDesc
     r.res = lz2_init(p, d.props[0], lo, gtab(), (gbyte*)(dst + d.dst_off),
                      d.dst_cap);
     if (r.res != kOk) return r;
+    p.dec.win = w0;
     uint64_t sl = d.src_len;
     int status = kStNone;
 #if LZGPU_PROF && !defined(LZGPU_HOST_EMU)
@@ -166,6 +172,7 @@ __device__ __forceinline__ LzmaGpuResult lane_decode_lds(const LzmaGpuStreamDesc
   }
   s.lo = lo;
   s.gl = gtab();
+  s.win = w0;
   s.dic = (gbyte*)(dst + d.dst_off);
   s.cap = d.dst_cap;
   s.pos = 0;
@@ -204,8 +211,9 @@ __device__ __forceinline__ LzmaGpuResult lane_decode_lds(const LzmaGpuStreamDesc
 template <uint32_t M = 0u, class Lo = gu16*>
 __device__ __forceinline__ int session_to_dic(LzgpuSession& q, uint64_t dic_limit,
                                               const gbyte* in, uint64_t& in_len, int fin,
-                                              int& status, Lo lo = Lo()) {
+                                              int& status, Lo lo = Lo(), LzWin* w = nullptr) {
   LzStateT<Lo> s;
+  if constexpr (win_on<M>()) s.win = *w;
   s.lc = q.lc;
   s.lp = q.lp;
   s.pb = q.pb;
@@ -233,6 +241,7 @@ __device__ __forceinline__ int session_to_dic(LzgpuSession& q, uint64_t dic_limi
   s.tmp_n = q.temp_buf_size;
   for (int i = 0; i < int(kLookahead); ++i) s.tmp[i] = q.temp_buf[i];
   const int res = lz_decode_to_dic<true, M>(s, dic_limit, in, in_len, fin, status);
+  if constexpr (win_on<M>()) *w = s.win;
   q.dic_pos = s.pos;
   q.range = s.range;
   q.code = s.code;
@@ -263,12 +272,35 @@ __device__ __forceinline__ int session_to_dic(LzgpuSession& q, uint64_t dic_limi
 // pipeline -- its global stores and later loads to the same address are seen
 // in issue order (one vector L1 per CU) -- the same property lz_copy_coop
 // relies on when a match reads bytes the wave just wrote.
+// kWinBit: `win` (win_bytes) is the call's LDS history window, preloaded here
+// with the last bytes of the session's dictionary that a match can reach --
+// the bytes written since its last dictionary init (processedPos), or the
+// whole ring once it has been filled (checkDicSize) -- by the wave's lanes.
 template <uint32_t M = 0u, class Lo = gu16*>
-__device__ __forceinline__ void lane_session(LzgpuSession& q, Lo lo = Lo()) {
+__device__ __forceinline__ void lane_session(LzgpuSession& q, Lo lo = Lo(), lds_u8* win = nullptr,
+                                             uint32_t win_bytes = 0) {
   int status = kStNone;
+  LzWin w = {win, win_bytes - 1, 0, 0};
+  if constexpr (win_on<M>()) {
+    uint64_t hv = q.check_dic_size != 0 ? q.dic_buf_size : q.processed_pos;
+    if (hv > q.dic_buf_size) hv = q.dic_buf_size;
+    if (hv > win_bytes) hv = win_bytes;
+    const gbyte* dic = (const gbyte*)q.dic;
+#ifdef LZGPU_HOST_EMU
+    const uint32_t l0 = 0, step = 1;
+#else
+    const uint32_t l0 = threadIdx.x, step = blockDim.x;
+#endif
+    // window slot i holds the byte at distance hv - i
+    for (uint32_t i = l0; i < uint32_t(hv); i += step)
+      win[i] = dic[ring_back(q.dic_pos, uint32_t(hv) - i, q.dic_buf_size)];
+    w.t = uint32_t(hv);
+    w.av = uint32_t(hv);
+  }
   if (q.mode != 1) {
     uint64_t sl = q.in_len;
-    q.res = session_to_dic<M>(q, q.dic_limit, (const gbyte*)q.in, sl, q.finish_mode, status, lo);
+    q.res = session_to_dic<M>(q, q.dic_limit, (const gbyte*)q.in, sl, q.finish_mode, status, lo,
+                              &w);
     q.status = status;
     q.in_used = sl;
     return;
@@ -290,7 +322,7 @@ __device__ __forceinline__ void lane_session(LzgpuSession& q, Lo lo = Lo()) {
       fin = q.finish_mode;
     }
     uint64_t in_cur = in_left;
-    res = session_to_dic<M>(q, lim, in + in_done, in_cur, fin, status, lo);
+    res = session_to_dic<M>(q, lim, in + in_done, in_cur, fin, status, lo, &w);
     in_done += in_cur;
     in_left -= in_cur;
     const uint64_t produced = q.dic_pos - start;

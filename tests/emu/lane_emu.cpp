@@ -26,6 +26,10 @@ void emu_decode_batch(const LzmaGpuStreamDesc* descs, size_t n, const uint8_t* s
   for (size_t i = 0; i < n; ++i) results[i] = lane_decode(descs[i], src, dst, ws);
 }
 
+#ifndef EMU_WIN_BYTES
+#define EMU_WIN_BYTES 4096
+#endif
+
 // LDS-variant kernel body: each lane gets a private "LDS" slice of stride cells.
 void emu_decode_batch_lds(const LzmaGpuStreamDesc* descs, size_t n, const uint8_t* src,
                           uint8_t* dst, uint16_t* ws, LzmaGpuResult* results, uint32_t stride) {
@@ -53,6 +57,15 @@ void emu_decode_batch_lds(const LzmaGpuStreamDesc* descs, size_t n, const uint8_
 #elif defined(EMU_ILV)
     results[i] = lane_decode_lds<LZGPU_LDS_MASK | kIlvBit>(descs[i], src, dst, ws, slab, stride,
                                                           slots.data() + (i % kIlv) * kIlvLaneCells);
+#elif defined(EMU_COOP_ALL_WIN)
+    // ... with the LDS history window (EMU_WIN_BYTES: 4 KiB exercises the
+    // dictionary fallback for longer distances and the slot wrap)
+    {
+      static std::vector<uint8_t> win(EMU_WIN_BYTES);
+      memset(win.data(), 0x5C, win.size());  // stale LDS contents
+      results[i] = lane_decode_lds<LZGPU_LDS_MASK_ALL | kCoopBit | kWinBit>(
+          descs[i], src, dst, ws, slab, stride, nullptr, win.data(), EMU_WIN_BYTES);
+    }
 #elif defined(EMU_COOP_ALL)
     // the wave-cooperative kernel with every section in LDS (its default
     // placement where the whole table fits)
@@ -77,6 +90,23 @@ void emu_decode_batch_lds(const LzmaGpuStreamDesc* descs, size_t n, const uint8_
 // kernel's body), same contract as orc_lzma_stream_decode.  buf_mode 1: each
 // DecodeToBuf call is one session call in mode 1 (the device ring loop);
 // buf_mode 0: the ring loop runs here over mode-0 (DecodeToDic) calls.
+// One session call: lane_session on the session's table in place, or under
+// EMU_SESS_COOP_WIN the cooperative session kernel's body -- the table staged
+// into an "LDS" copy and back, and the LDS history window preloaded per call.
+static void run_session(LzgpuSession& q) {
+#if defined(EMU_SESS_COOP_WIN)
+  const uint32_t cells = table_cells(q.lc, q.lp, q.pb);
+  std::vector<uint16_t> lo(cells + 8);
+  memcpy(lo.data(), q.probs, size_t(cells) * 2);
+  static std::vector<uint8_t> win(EMU_WIN_BYTES);
+  memset(win.data(), 0x5C, win.size());
+  lane_session<LZGPU_LDS_MASK_ALL | kCoopBit | kWinBit>(q, lo.data(), win.data(), EMU_WIN_BYTES);
+  memcpy((void*)q.probs, lo.data(), size_t(cells) * 2);
+#else
+  lane_session(q);
+#endif
+}
+
 static int stream_decode(const uint8_t* props, const uint8_t* src, size_t src_total, uint8_t* out,
                          size_t out_total, size_t in_chunk, size_t out_chunk, int finish_mode,
                          long long* trace, int max_calls, size_t* out_len, size_t* in_used,
@@ -104,7 +134,7 @@ static int stream_decode(const uint8_t* props, const uint8_t* src, size_t src_to
       q.mode = 1;
       q.in = src + in_pos; q.in_len = sl; q.out = out + out_pos; q.out_len = dl;
       q.finish_mode = finish_mode;
-      lane_session(q);
+      run_session(q);
       res = q.res; st = q.status; got_in = q.in_used; got_out = q.out_len;
     } else {
       // ---- LzmaDec_DecodeToBuf (LzmaDec.c:840-878) over mode-0 calls
@@ -119,7 +149,7 @@ static int stream_decode(const uint8_t* props, const uint8_t* src, size_t src_to
         if (out_left > q.dic_buf_size - start) { lim = q.dic_buf_size; fin = 0; }
         else { lim = start + out_left; fin = finish_mode; }
         q.in = s; q.in_len = in_left; q.dic_limit = lim; q.finish_mode = fin;
-        lane_session(q);
+        run_session(q);
         res = q.res; st = q.status;
         s += q.in_used; in_left -= q.in_used; got_in += q.in_used;
         size_t produced = q.dic_pos - start;

@@ -38,6 +38,13 @@ EMU_VARIANTS = {
     "interleaved_global_instantiation": "-DEMU_ILV",
     "coop_instantiation": "-DEMU_COOP",
     "coop_all_lds_instantiation": "-DEMU_COOP_ALL",
+    # round 4: the LDS history window of the cooperative kernels (a 4 KiB window
+    # falls back to the dictionary for longer distances and wraps; 64 KiB holds
+    # most streams whole), batch items and device-resident sessions
+    "coop_window_4k": "-DEMU_COOP_ALL_WIN -DEMU_WIN_BYTES=4096",
+    "coop_window_64k": "-DEMU_COOP_ALL_WIN -DEMU_WIN_BYTES=65536",
+    "session_coop_window_4k": "-DEMU_SESS_COOP_WIN -DEMU_WIN_BYTES=4096",
+    "session_coop_window_64k": "-DEMU_SESS_COOP_WIN -DEMU_WIN_BYTES=65536",
     # round 4: the decision-level loop (lz_run_step) on the throughput
     # instantiation and on other placements of the same code
     "step_interleaved_instantiation": "-DEMU_STEP_ILV",
