@@ -259,7 +259,7 @@ size_t LzmaGpu_PlanBatch(LzmaGpuStreamDesc *descs, size_t n, uint32_t *order);
  * LZGPU_OCC=<1|2|4 waves per SIMD>, LZGPU_CUS, LZGPU_COOP=0|1,
  * LZGPU_PERSIST=0 (one stream per lane), LZGPU_CLASSES=1 (one LDS launch),
  * LZGPU_SLICE_ALIGN8=1, LZGPU_KERNEL_LZMA2=1, LZGPU_COOP_LAT=1, LZGPU_MERGE_LAT=0, LZGPU_ILV=0,
- * LZGPU_ILV_ANY=1, LZGPU_THR_FIT=0 (the
+ * LZGPU_ILV_ANY=1, LZGPU_THR_FIT=0, LZGPU_SCALAR=0..4 (the
  * LZMA_GPU_PLAN_* flags below); DecodeBatchEx reads LZGPU_CLASS_STREAMS=0
  * (classes launched one after another on the caller's stream).
  * workspace_bytes includes the LDS launches' work counters at queue_offset
@@ -288,6 +288,11 @@ typedef struct LzmaGpuLdsClass {
 /* the class holds LZMA2 items: launched on the kernel build with the LZMA2 chunk
  * walker (without it the LZMA-only build runs, fewer registers) */
 #define LZMA_GPU_CLASS_HAS_LZMA2 1u
+/* bits 4-6: of every four one-lane waves of a latency class (placement 0x1BF,
+ * lanes_per_group 1), how many run the decoder in scalar registers on the CU's
+ * scalar ALU instead of the vector ALU (0-4; set by the planner, see
+ * LzmaGpuPlanOptions.scalar_waves) */
+#define LZMA_GPU_CLASS_SCALAR_SHIFT 4
 
 typedef struct LzmaGpuPlan {
   uint64_t workspace_bytes;
@@ -333,7 +338,9 @@ typedef struct LzmaGpuPlanOptions {
   uint32_t coop;            /* AUTO only: 0 = by streams per CU, 1 = always, 2 = never */
   uint32_t one_class;       /* 1: all LDS-eligible streams in one launch */
   uint32_t flags;           /* LZMA_GPU_PLAN_* bits */
-  uint32_t reserved;
+  /* one-lane latency waves running the scalar-register decoder: 0 = planner
+   * default, 1 + k = k of every four (k = 0..4; LZGPU_SCALAR=k) */
+  uint32_t scalar_waves;
 } LzmaGpuPlanOptions;
 /* per-lane LDS slices 8-byte aligned (default: an odd number of dwords, so that
  * 32 lanes reading the same cell index hit 32 different LDS banks) */

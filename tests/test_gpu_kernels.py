@@ -55,7 +55,11 @@ THR = ("throughput", "throughput_np", "throughput_slices", "throughput_slices_np
 # lane, a lane decoding many streams in one column, and 16-lane waves
 STEP_BIT, PLAN_STEP = 0x10000000, 0x80
 STEP = ("step", "step_np", "step_slices", "step_reuse", "step_w16")
-KERNELS = THR + STEP + ("latency", "coop", "coop_lat", "global")
+# round 4: one-lane latency waves on the scalar-register build
+# (lzgpu_decode_one_kernel): all of them, none, or half of the class's grid
+# beside the vector build on a second stream (LzmaGpuPlanOptions.scalar_waves)
+SCALAR = {"latency_scalar": 4, "latency_split": 2, "latency_vector": 0}
+KERNELS = THR + STEP + ("latency",) + tuple(SCALAR) + ("coop", "coop_lat", "global")
 
 
 @pytest.fixture(scope="module")
@@ -102,6 +106,9 @@ def _check_plan(plan, kernel):
                 assert c.slot_cells > 0 and c.slot_groups > 0 and c.slot_off % 64 == 0
         elif kernel == "latency":
             assert c.lds_mask == M_LAT and c.lanes_per_group == 1, hex(c.lds_mask)
+        elif kernel in SCALAR:
+            assert c.lds_mask == M_LAT and c.lanes_per_group == 1, hex(c.lds_mask)
+            assert (c.flags >> 4) & 7 == SCALAR[kernel], hex(c.flags)
         elif kernel == "coop":
             # all sections in LDS where the whole table fits the class's
             # streams per CU, else the latency placement
@@ -144,6 +151,8 @@ def _opts(L, kernel):
                               flags=PLAN_STEP | 32)
     if kernel == "coop_lat":
         return L.plan_options("coop", cus=8, flags=4)
+    if kernel in SCALAR:
+        return L.plan_options("latency", cus=8, scalar_waves=SCALAR[kernel] + 1)
     if kernel == "throughput_np":
         # 32 streams per wave wherever the slices fit: the interleaved rows
         # without persistent lanes on every batch, not only lc+lp = 0 classes
