@@ -608,10 +608,13 @@ def print_prof(L):
         buf = (ctypes.c_ulonglong * 24)()
         L.lib.LzmaGpu_ProfileRead(buf, 0)
         lanes = max(1, buf[23])
+        # "a|b|c": the counter's meaning in the per-lane (PROF=2) / global-slot /
+        # LDS-slot (cooperative, round 4) builds
         names = ("literal_batches", "match_decode", "copy_tail", "decode_to_dic_total",
-                 "refills", "batch_iters|slot_sub3_a", "lit_lanes|slot_sub3_b", "mlit_lanes|n_slot",
+                 "refills", "batch_iters|slot_sub3_a|cyc_slot",
+                 "lit_lanes|slot_sub3_b|cyc_direct", "mlit_lanes|n_slot|cyc_align",
                  "mixed_iters|cyc_rep_bits", "match_entries|cyc_len", "match_lanes|cyc_dist",
-                 "live_lanes|n_dist", "bytes", "matches|cyc_drain",
+                 "live_lanes|n_dist", "bytes", "matches|cyc_drain|cyc_specpos",
                  "cyc_ismatch", "cyc_literal", "cyc_lit_tail", "cyc_iterations")
         prof = {k: buf[i] / lanes for i, k in enumerate(names)}
         prof["other_in_decode_to_dic"] = prof["decode_to_dic_total"] - sum(

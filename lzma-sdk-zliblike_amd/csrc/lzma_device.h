@@ -56,6 +56,12 @@ constexpr uint32_t kProbOne = 2048u;
 constexpr uint32_t kProbInit = 1024u;
 constexpr uint32_t kLookahead = 20u;  // LZMA_REQUIRED_INPUT_MAX
 constexpr uint32_t kLenDone = 274u;   // kMatchSpecLenStart
+// direct bits decided several per step on the cooperative kernel (direct_coop;
+// -DLZGPU_DIRECT_CHUNKS=0 restores the bit-serial loop for A/B)
+#ifndef LZGPU_DIRECT_CHUNKS
+#define LZGPU_DIRECT_CHUNKS 1
+#endif
+constexpr bool kDirectChunks = LZGPU_DIRECT_CHUNKS != 0;
 
 // ------------------------------------------------------------------ compact layout
 
@@ -854,6 +860,72 @@ __device__ __forceinline__ uint32_t spec_stage(Rc<Rd>& rc, P probs, uint32_t m0)
   rc.rd->win = o.win;
   rc.rd->nb = o.nb;
   return (m0 << L) | w;
+}
+
+// Direct bits of a distance (LzmaDec.c:323-344), several per step, on the
+// wave-cooperative kernel (round 4).  A direct bit reads
+// no probability: NORMALIZE, range >>= 1, the bit is code >= range (the
+// reference's sign trick equals the compare while code < 2^31 + range), and
+// code -= range on a 1.  Between two normalisations the ranges are R >> 1,
+// R >> 2, ... -- fixed before any bit is known -- and, because each is more
+// than the sum of all later ones, the k bits the serial loop decodes are the
+// largest v whose weight S(v) = sum over the 1-bits i of v (MSB = bit 1) of
+// R >> i is <= code.  So a chunk of k <= 5 bits (k no larger than the bits the
+// range allows before the next NORMALIZE: 8 - clz(R)) is decided in one step:
+// lane j computes S(j), the lanes with S(j) <= code are exactly 0..v, v is
+// their count - 1 (a ballot), and the winner's S is taken by readlane:
+// code -= S(v), range = R >> k.  A state outside the sign trick's reach
+// (code >= 2^31 + (R >> k): only a corrupt stream) takes the chunk bit by
+// bit.  Returns with range >= 2^24 not guaranteed (the caller's next decision
+// normalises first, as the reference does).
+template <class Rd>
+__device__ __forceinline__ void direct_coop(Rc<Rd>& rc, uint32_t& dist, uint32_t left) {
+#ifndef LZGPU_HOST_EMU
+  const uint32_t j = lz_lane_id() & 31u;
+#endif
+  do {
+    rc.norm();
+    const uint32_t R = rc.range, C = rc.code;
+    uint32_t k = 8u - uint32_t(__builtin_clz(R));  // bits before the next NORMALIZE
+    k = k < left ? k : left;
+    k = k < 5u ? k : 5u;
+    const uint32_t Rk = R >> k;
+    if (C >= 0x80000000u + Rk) {
+      // outside the compare's reach (corrupt input): the reference's own steps
+      for (uint32_t i = 0; i < k; ++i) {
+        if (i) rc.norm();
+        rc.range >>= 1;
+        rc.code -= rc.range;
+        const uint32_t t = 0u - (rc.code >> 31);
+        dist = (dist << 1) + (t + 1u);
+        rc.code += rc.range & t;
+      }
+    } else {
+#ifdef LZGPU_HOST_EMU
+      uint32_t v = 0, sv = 0;
+      for (uint32_t c = 0; c < (1u << k); ++c) {
+        uint32_t S = 0;
+        for (uint32_t t = 0; t < k; ++t)
+          if ((c >> t) & 1u) S += R >> (k - t);
+        if (S <= C) v = c, sv = S;
+      }
+#else
+      // lane j's k-bit candidate: bit t of j (LSB = the chunk's last bit)
+      // weighs R >> (k - t); lanes j >= 2^k hold no candidate
+      uint32_t S = 0;
+#pragma unroll
+      for (uint32_t t = 0; t < 5u; ++t)
+        S += ((j >> t) & 1u) ? (R >> ((k - t) & 31u)) : 0u;
+      const bool ok = (j >> k) == 0u && S <= C;
+      const uint32_t v = uint32_t(__builtin_popcountll(__builtin_amdgcn_ballot_w64(ok))) - 1u;
+      const uint32_t sv = uint32_t(__builtin_amdgcn_readlane(int(S), int(v)));
+#endif
+      rc.code = C - sv;
+      rc.range = Rk;
+      dist = (dist << k) | v;
+    }
+    left -= k;
+  } while (left != 0);
 }
 
 // the plain literal tree in two cooperative stages (5 + 3 levels); the caller's
@@ -1803,8 +1875,17 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
         dist = rc.sub3(sl_t, rc.sub3(sl_t, 1)) - 64;
 #endif
       } else {
+#if LZGPU_PROF == 1 && !defined(LZGPU_HOST_EMU)
+        const uint64_t t0 = lz_clock();
         dist = rc.template tree<6>(T.template at<S_SLOT>(lstate << 6));
+        s.prof[5] += lz_clock() - t0;  // slot tree (LDS placements)
+#else
+        dist = rc.template tree<6>(T.template at<S_SLOT>(lstate << 6));
+#endif
       }
+#if LZGPU_PROF == 1 && !defined(LZGPU_HOST_EMU)
+      const uint64_t t_tail = lz_clock();
+#endif
       if (dist >= 4) {
         const uint32_t slot = dist;
         uint32_t nbits = (slot >> 1) - 1;
@@ -1835,9 +1916,19 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
             mask <<= 1;
             --nbits;
           }
+#if LZGPU_PROF == 1 && !defined(LZGPU_HOST_EMU)
+          s.prof[13] += lz_clock() - t_tail;  // SpecPos bits
+#endif
         } else {
           nbits -= 4;
-          do rc.direct(dist); while (--nbits != 0);
+          if constexpr ((M & kCoopBit) != 0u && kDirectChunks)
+            direct_coop(rc, dist, nbits);
+          else
+            do rc.direct(dist); while (--nbits != 0);
+#if LZGPU_PROF == 1 && !defined(LZGPU_HOST_EMU)
+          const uint64_t t_al = lz_clock();
+          s.prof[6] += t_al - t_tail;  // direct bits
+#endif
           dist <<= 4;
           uint32_t node = 1;
           if constexpr (((M >> S_ALIGN) & 1u) == 0u) {
@@ -1860,6 +1951,9 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
               dist |= b << k;
             }
           }
+#if LZGPU_PROF == 1 && !defined(LZGPU_HOST_EMU)
+          s.prof[7] += lz_clock() - t_al;  // align bits
+#endif
           if (dist == 0xFFFFFFFFu) {
             len += kLenDone;
             st -= 12;

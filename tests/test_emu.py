@@ -226,3 +226,19 @@ def test_emu_fuzz_vs_oracle(emu, lds):
         got = (res[k].res, res[k].status, res[k].dest_len, res[k].src_len)
         out = dst[items[k]["dst_off"]:items[k]["dst_off"] + res[k].dest_len]
         assert got == exp[k][:4] and out == exp[k][4], (k, got, exp[k][:4])
+
+
+def test_direct_chunks_match_serial_direct_bits(tmp_path):
+    """direct_coop decides up to five direct bits per step (closed form over the
+    range's halvings, one ballot); it must leave range, code, the distance bits
+    and the input position exactly where the reference's bit-serial loop
+    (LzmaDec.c:323-344) does, for well-formed and corrupt states alike."""
+    import subprocess
+    src = os.path.join(native.ROOT, "tests", "emu", "direct_chunks.cpp")
+    exe = str(tmp_path / "direct_chunks")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-I",
+                    os.path.join(native.ROOT, "lzma-sdk-zliblike_amd", "csrc"), "-I",
+                    os.path.join(native.ROOT, "include"), src, "-o", exe], check=True)
+    r = subprocess.run([exe, "400000"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "0 mismatches" in r.stdout
