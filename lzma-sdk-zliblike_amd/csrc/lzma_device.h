@@ -549,9 +549,16 @@ constexpr uint32_t kStepBit = 0x10000000u;
 #ifndef LZGPU_LDS_MASK_ALL
 #define LZGPU_LDS_MASK_ALL 0x7FFu
 #endif
+// The history window (kWinBit) does not change the reader: the cooperative
+// kernels keep the checkpoint reader and with it the speculative literal stages
+// (lit8_coop).  -DLZGPU_WIN_Q=0 (A/B only) gives windowed builds the per-byte
+// reader and the serial literal tree, as the first window build did.
+#ifndef LZGPU_WIN_Q
+#define LZGPU_WIN_Q 1
+#endif
 template <uint32_t M>
 struct BulkReaderFor {
-  static constexpr uint32_t m = M & ~(kIlvBit | kStepBit);
+  static constexpr uint32_t m = M & ~(kIlvBit | kStepBit | (LZGPU_WIN_Q ? kWinBit : 0u));
   static constexpr bool q = m == LZGPU_LDS_MASK || m == (LZGPU_LDS_MASK_LAT | kCoopBit) ||
                             m == (LZGPU_LDS_MASK_ALL | kCoopBit) || (M & kStepBit) != 0u;
   typedef typename std::conditional<q, GlobalReaderQ, PlainReader>::type type;
