@@ -259,6 +259,69 @@ __host__ __device__ constexpr bool win_on() {
   return (M & kWinBit) != 0u;
 }
 
+// A zero the compiler must treat as per-lane (written by an instruction it
+// cannot see through).  The wave-cooperative kernels add it to their stream's
+// offsets: every lane of such a wave holds the same decoder state, and with the
+// state in registers (LzTmp below) the compiler proves that and moves the whole
+// serial decoder to the scalar unit -- measured slower there (config 4 3,060 ->
+// 2,607 MB/s: the scalar build spills hundreds of scalar registers to vector
+// lanes; profiles/r04_tmp/), so the cooperative state stays in vector registers.
+__device__ __forceinline__ uint32_t lz_vzero() {
+#ifdef LZGPU_HOST_EMU
+  return 0;
+#else
+  uint32_t z;
+  asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+  return z;
+#endif
+}
+
+// The lookahead buffer (CLzmaDec.tempBuf, LzmaDec.h:68: kLookahead bytes) as
+// three 64-bit words.  As a byte array indexed by a run-time position it would
+// be a dynamically indexed private array inside the decoder state, and the
+// compiler keeps a structure that an unknown index reaches into in scratch
+// memory as a whole -- the range coder, positions and reps included -- with
+// every value read back from it a per-lane load; as words it is registers.
+// (-DLZGPU_TMP_BYTES=1: the byte array, A/B only.)
+#ifndef LZGPU_TMP_BYTES
+#define LZGPU_TMP_BYTES 0
+#endif
+#if LZGPU_TMP_BYTES
+struct LzTmp {
+  uint8_t b[kLookahead];
+  __device__ __forceinline__ uint32_t get(uint32_t i) const { return b[i]; }
+  __device__ __forceinline__ void set(uint32_t i, uint32_t v) { b[i] = uint8_t(v); }
+};
+#else
+struct LzTmp {
+  uint64_t w0, w1, w2;
+  __device__ __forceinline__ uint32_t get(uint32_t i) const {
+    const uint64_t w = i < 8u ? w0 : (i < 16u ? w1 : w2);
+    return uint32_t(w >> (8u * (i & 7u))) & 0xFFu;
+  }
+  __device__ __forceinline__ void set(uint32_t i, uint32_t b) {
+    const uint32_t sh = 8u * (i & 7u);
+    const uint64_t m = ~(uint64_t(0xFFu) << sh), v = uint64_t(b & 0xFFu) << sh;
+    w0 = i < 8u ? ((w0 & m) | v) : w0;
+    w1 = (i >= 8u && i < 16u) ? ((w1 & m) | v) : w1;
+    w2 = i >= 16u ? ((w2 & m) | v) : w2;
+  }
+};
+#endif
+// byte pointer over an LzTmp (the look-ahead probe of the tempBuf path)
+struct LzTmpIter {
+  LzTmp t;
+  uint32_t i;
+  __device__ __forceinline__ LzTmpIter operator+(uint64_t n) const { return {t, i + uint32_t(n)}; }
+  __device__ __forceinline__ bool operator>=(const LzTmpIter& o) const { return i >= o.i; }
+  __device__ __forceinline__ uint32_t operator*() const { return t.get(i); }
+  __device__ __forceinline__ LzTmpIter operator++(int) {
+    const LzTmpIter r = *this;
+    ++i;
+    return r;
+  }
+};
+
 // Per-lane decoder state (CLzmaDec fields, LzmaDec.h:50-69).  lo = the LDS
 // table (pointer type Lo: lds_u16*; or gu16* aliasing gl when everything is
 // global), gl = the global table.
@@ -278,7 +341,7 @@ struct LzStateT {
   uint32_t pending;  // remainLen
   uint32_t need_rc_init, need_state_init;
   uint32_t tmp_n;
-  uint8_t tmp[kLookahead];
+  LzTmp tmp;
   LzWin win;  // kWinBit placements only
 #if LZGPU_PROF
   // [0..4] cycles: literal batches, match decode, copies + tail, calls, refills;
@@ -549,12 +612,13 @@ constexpr uint32_t kStepBit = 0x10000000u;
 #ifndef LZGPU_LDS_MASK_ALL
 #define LZGPU_LDS_MASK_ALL 0x7FFu
 #endif
-// The history window (kWinBit) does not change the reader: the cooperative
-// kernels keep the checkpoint reader and with it the speculative literal stages
-// (lit8_coop).  -DLZGPU_WIN_Q=0 (A/B only) gives windowed builds the per-byte
-// reader and the serial literal tree, as the first window build did.
+// Windowed cooperative builds (kWinBit) take the per-byte reader and with it
+// the serial literal tree (lz_literal without lit8_coop): measured faster than
+// the checkpoint reader with the speculative stages once the window is there --
+// config 4 3,187 vs 3,060 MB/s, xz 2,834 vs 2,642, config 1 2.71 vs 2.49 MB/s
+// (profiles/r04_tmp/).  -DLZGPU_WIN_Q=1 (A/B only) keeps the checkpoint reader.
 #ifndef LZGPU_WIN_Q
-#define LZGPU_WIN_Q 1
+#define LZGPU_WIN_Q 0
 #endif
 template <uint32_t M>
 struct BulkReaderFor {
@@ -590,13 +654,13 @@ __device__ __forceinline__ uint32_t rd_take_u(Rd& rd) {
 
 // Reader over a lane-private byte array (the tempBuf path).
 struct LocalReader {
-  const uint8_t* p;
+  LzTmp t;
   uint32_t idx;
-  __device__ __forceinline__ void init(const uint8_t* q) { p = q; idx = 0; }
+  __device__ __forceinline__ void init(const LzTmp& q) { t = q; idx = 0; }
   __device__ __forceinline__ uint32_t used() const { return idx; }
-  __device__ __forceinline__ uint32_t peek() const { return p[idx]; }
+  __device__ __forceinline__ uint32_t peek() const { return t.get(idx); }
   __device__ __forceinline__ void advance(bool n) { idx += n ? 1u : 0u; }
-  __device__ __forceinline__ uint32_t next() { return p[idx++]; }
+  __device__ __forceinline__ uint32_t next() { return t.get(idx++); }
 };
 
 // ------------------------------------------------------------------ range decoder
@@ -2288,14 +2352,13 @@ __device__ __forceinline__ int lz_decode_to_dic(LzStateT<Lo>& s, uint64_t dic_li
     bool at_end_check = false;
     if (s.need_rc_init) {
       while (avail > 0 && s.tmp_n < 5) {
-        s.tmp[s.tmp_n++] = *src++;
+        s.tmp.set(s.tmp_n++, *src++);
         src_len++;
         avail--;
       }
       if (s.tmp_n < 5) { status = kStMoreInput; return kOk; }
-      if (s.tmp[0] != 0) return kErrData;
-      s.code = (uint32_t(s.tmp[1]) << 24) | (uint32_t(s.tmp[2]) << 16) |
-               (uint32_t(s.tmp[3]) << 8) | uint32_t(s.tmp[4]);
+      if (s.tmp.get(0) != 0) return kErrData;
+      s.code = (s.tmp.get(1) << 24) | (s.tmp.get(2) << 16) | (s.tmp.get(3) << 8) | s.tmp.get(4);
       s.range = 0xFFFFFFFFu;
       s.need_rc_init = 0;
       s.tmp_n = 0;
@@ -2313,7 +2376,7 @@ __device__ __forceinline__ int lz_decode_to_dic(LzStateT<Lo>& s, uint64_t dic_li
       if (avail < kLookahead || at_end_check) {
         int k = lz_probe<M>(s, src, avail);
         if (k == PROBE_SHORT) {
-          for (uint32_t i = 0; i < uint32_t(avail); ++i) s.tmp[i] = src[i];
+          for (uint32_t i = 0; i < uint32_t(avail); ++i) s.tmp.set(i, src[i]);
           s.tmp_n = uint32_t(avail);
           src_len += avail;
           status = kStMoreInput;
@@ -2340,10 +2403,10 @@ __device__ __forceinline__ int lz_decode_to_dic(LzStateT<Lo>& s, uint64_t dic_li
       avail -= used;
     } else {
       uint32_t have = s.tmp_n, taken = 0;
-      while (have < kLookahead && taken < avail) s.tmp[have++] = src[taken++];
+      while (have < kLookahead && taken < avail) s.tmp.set(have++, src[taken++]);
       s.tmp_n = have;
       if (have < kLookahead || at_end_check) {
-        int k = lz_probe<M>(s, (const uint8_t*)s.tmp, have);
+        int k = lz_probe<M>(s, LzTmpIter{s.tmp, 0u}, have);
         if (k == PROBE_SHORT) {
           src_len += taken;
           status = kStMoreInput;

@@ -168,7 +168,11 @@ __global__ void __launch_bounds__(32, W) lzgpu_decode_coop_kernel(
   uint32_t idx = blockIdx.x;
   while (idx < n) {
     const uint32_t id = order ? order[idx] : idx;
-    const LzmaGpuStreamDesc d = descs[id];
+    LzmaGpuStreamDesc d = descs[id];
+    // keep the shared decoder state in vector registers (lz_vzero)
+    const uint32_t z = lz_vzero();
+    d.src_off += z;
+    d.dst_off += z;
     const LzmaGpuResult r =
         lane_decode_lds<M, K2>(d, src, dst, ws, lo, stride, nullptr, win, win_bytes);
     uint32_t next = 0;
@@ -209,6 +213,12 @@ __global__ void __launch_bounds__(32) lzgpu_session_coop_kernel(LzgpuSession* __
   constexpr uint32_t MS = kSessCoopMask | (WIN ? kWinBit : 0u);
   for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
     LzgpuSession q = sess[i];
+    // keep the shared decoder state in vector registers (lz_vzero)
+    {
+      const uint32_t z = lz_vzero();
+      q.in = (const uint8_t*)q.in + z;
+      q.dic = (uint8_t*)q.dic + z;
+    }
     const uint32_t cells = table_cells(q.lc, q.lp, q.pb);
     if (cells > lds_cells) {  // planned for narrower tables: refuse, state untouched
       if (threadIdx.x == 0) {

@@ -239,7 +239,7 @@ __device__ __forceinline__ int session_to_dic(LzgpuSession& q, uint64_t dic_limi
   s.need_rc_init = q.need_flush;
   s.need_state_init = q.need_init_state;
   s.tmp_n = q.temp_buf_size;
-  for (int i = 0; i < int(kLookahead); ++i) s.tmp[i] = q.temp_buf[i];
+  for (uint32_t i = 0; i < kLookahead; ++i) s.tmp.set(i, q.temp_buf[i]);
   const int res = lz_decode_to_dic<true, M>(s, dic_limit, in, in_len, fin, status);
   if constexpr (win_on<M>()) *w = s.win;
   q.dic_pos = s.pos;
@@ -256,7 +256,7 @@ __device__ __forceinline__ int session_to_dic(LzgpuSession& q, uint64_t dic_limi
   q.need_flush = s.need_rc_init;
   q.need_init_state = s.need_state_init;
   q.temp_buf_size = s.tmp_n;
-  for (int i = 0; i < int(kLookahead); ++i) q.temp_buf[i] = s.tmp[i];
+  for (uint32_t i = 0; i < kLookahead; ++i) q.temp_buf[i] = uint8_t(s.tmp.get(i));
   return res;
 }
 
