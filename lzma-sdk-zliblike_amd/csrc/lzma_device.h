@@ -266,8 +266,11 @@ __host__ __device__ constexpr bool win_on() {
 // serial decoder to the scalar unit -- measured slower there (config 4 3,060 ->
 // 2,607 MB/s: the scalar build spills hundreds of scalar registers to vector
 // lanes; profiles/r04_tmp/), so the cooperative state stays in vector registers.
+#ifndef LZGPU_COOP_VREG
+#define LZGPU_COOP_VREG 1  // 0: let the cooperative state go scalar (A/B only)
+#endif
 __device__ __forceinline__ uint32_t lz_vzero() {
-#ifdef LZGPU_HOST_EMU
+#if defined(LZGPU_HOST_EMU) || !LZGPU_COOP_VREG
   return 0;
 #else
   uint32_t z;
