@@ -248,6 +248,7 @@ struct LzWin {
   uint32_t mask;  // window bytes - 1 (a power of two)
   uint32_t t;     // bytes written through the window
   uint32_t av;    // of them, still held (the last av)
+  uint32_t fl;    // of them, not yet stored to the dictionary (deferred output)
 };
 __device__ __forceinline__ void win_put(LzWin& w, uint32_t v) {
   w.b[w.t & w.mask] = uint8_t(v);
@@ -258,6 +259,18 @@ template <uint32_t M>
 __host__ __device__ constexpr bool win_on() {
   return (M & kWinBit) != 0u;
 }
+// Deferred output (round 4; cooperative kernels with a window): decoded bytes
+// go to the window only and reach the dictionary in bursts of >= kDeferBytes,
+// stored by all lanes of the wave at once (win_flush), and before the bulk pass
+// returns.  The last `fl` bytes are then missing from the dictionary, but
+// nothing reads them there: a read at distance <= fl <= av is served by the
+// window.  One store instruction per 32 bytes instead of one per literal, and
+// far loads stop queueing behind the literal stores (in-order vmcnt).
+// -DLZGPU_WIN_DEFER=0 (A/B only) writes every byte through.
+#ifndef LZGPU_WIN_DEFER
+#define LZGPU_WIN_DEFER 1
+#endif
+constexpr uint32_t kDeferBytes = 64u;
 
 // A zero the compiler must treat as per-lane (written by an instruction it
 // cannot see through).  The wave-cooperative kernels add it to their stream's
@@ -606,6 +619,10 @@ typedef GlobalReader16 PlainReader;
 // Bit 31 of a placement mask marks the wave-cooperative kernel (kCoopBit: one
 // stream per wave, every lane holding the same state; lit8_coop).
 constexpr uint32_t kCoopBit = 0x80000000u;
+template <uint32_t M>
+__host__ __device__ constexpr bool def_on() {
+  return LZGPU_WIN_DEFER != 0 && win_on<M>() && (M & kCoopBit) != 0u;
+}
 // Bit 28 of a placement mask (kStepBit, round 4): the bulk pass runs as the
 // decision-level loop lz_run_step (one range-coder decision per lane per
 // iteration) instead of the symbol loop lz_run; the sections and their
@@ -1171,10 +1188,22 @@ __device__ __forceinline__ uint32_t lz_mod_small(uint32_t j, uint32_t d, float r
 // Lanes of one wave see each other's global stores in order (one vector L1).
 // Returns the last byte copied; `mb` gets the next matched byte.
 constexpr uint32_t kCoopLanes = 32u;
+// Store the window's `fl` deferred bytes -- dictionary positions [end - fl,
+// end), contiguous within a bulk pass -- with every lane of the wave.
+__device__ __forceinline__ void win_flush(LzWin& w, gbyte* dic, uint64_t end) {
+#ifdef LZGPU_HOST_EMU
+  const uint32_t l0 = 0, step = 1;
+#else
+  const uint32_t l0 = lz_lane_id() & (kCoopLanes - 1u), step = kCoopLanes;
+#endif
+  for (uint32_t k = l0; k < w.fl; k += step) dic[end - w.fl + k] = w.b[(w.t - w.fl + k) & w.mask];
+  w.fl = 0;
+}
 // WIN: the LDS history window `w` is kept up to date (every copied byte is
 // also written there) and serves the loads when dist <= w.av (the byte at
 // window index k of the match is at distance dist - k < dist: held).
-template <bool WIN = false>
+// DEF: deferred output (def_on): the copy writes the window only.
+template <bool WIN = false, bool DEF = false>
 __device__ __forceinline__ uint32_t lz_copy_coop(gbyte* dic, uint64_t pos, uint64_t from,
                                                  uint32_t n, uint32_t dist, uint64_t cap,
                                                  uint32_t& mb, LzWin* w = nullptr) {
@@ -1188,11 +1217,16 @@ __device__ __forceinline__ uint32_t lz_copy_coop(gbyte* dic, uint64_t pos, uint6
     uint64_t a = from + k;
     v[j] = inwin ? w->b[(w->t - dist + k) & w->mask] : dic[a >= cap ? a - cap : a];
   }
-  for (uint32_t j = 0; j < n; ++j) dic[pos + j] = v[j];
+  if constexpr (!DEF)
+    for (uint32_t j = 0; j < n; ++j) dic[pos + j] = v[j];
   if constexpr (WIN) {
     for (uint32_t j = 0; j < n; ++j) w->b[(w->t + j) & w->mask] = v[j];
     w->t += n;
     w->av = (w->av + n > w->mask + 1) ? w->mask + 1 : w->av + n;
+  }
+  if constexpr (DEF) {
+    w->fl += n;
+    if (w->fl >= kDeferBytes) win_flush(*w, dic, pos + n);
   }
   mb = v[n];
   return v[n - 1];
@@ -1216,7 +1250,7 @@ __device__ __forceinline__ uint32_t lz_copy_coop(gbyte* dic, uint64_t pos, uint6
     return dic[src_of(j)];
   };
   auto store = [&](uint32_t j, uint32_t v) {
-    dic[pos + j] = uint8_t(v);
+    if constexpr (!DEF) dic[pos + j] = uint8_t(v);
     if constexpr (WIN) w->b[(w->t + j) & w->mask] = uint8_t(v);
   };
   uint32_t my_last = 0, my_mb = 0;
@@ -1240,6 +1274,12 @@ __device__ __forceinline__ uint32_t lz_copy_coop(gbyte* dic, uint64_t pos, uint6
   if constexpr (WIN) {
     w->t += n;
     w->av = (w->av + n > w->mask + 1) ? w->mask + 1 : w->av + n;
+  }
+  if constexpr (DEF) {
+    // (the window bytes other lanes just wrote are seen by the flush's LDS
+    // reads: one wave's LDS operations complete in order)
+    w->fl += n;
+    if (w->fl >= kDeferBytes) win_flush(*w, dic, pos + n);
   }
   mb = uint32_t(__builtin_amdgcn_readlane(int(my_mb), int(n & (kCoopLanes - 1u))));
   return uint32_t(__builtin_amdgcn_readlane(int(my_last), int((n - 1) & (kCoopLanes - 1u))));
@@ -1332,8 +1372,13 @@ __device__ __forceinline__ void lz_literal(Rc<Rd>& rc, const Tab<M, Lo>& T, uint
     }
   }
   prev = sym & 0xFFu;
-  lz_put(dic + pos, prev);
-  if constexpr (win_on<M>()) win_put(*w, prev);
+  if constexpr (def_on<M>()) {
+    win_put(*w, prev);
+    if (++w->fl >= kDeferBytes) win_flush(*w, dic, pos + 1);
+  } else {
+    lz_put(dic + pos, prev);
+    if constexpr (win_on<M>()) win_put(*w, prev);
+  }
   pos++;
   total++;
 }
@@ -1846,8 +1891,8 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
           if constexpr ((M & kCoopBit) != 0u) {
             // short rep = a one-byte copy: the byte and the next matched byte
             // in one load batch
-            prev = lz_copy_coop<win_on<M>()>(dic, pos, ring_back(pos, r0, cap), 1, r0, cap,
-                                             mb_pf, &s.win);
+            prev = lz_copy_coop<win_on<M>(), def_on<M>()>(dic, pos, ring_back(pos, r0, cap), 1,
+                                                          r0, cap, mb_pf, &s.win);
             pos++;
           } else {
             prev = dic[ring_back(pos, r0, cap)];
@@ -2056,7 +2101,7 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
       total += n;
       len -= n;
       if constexpr ((M & kCoopBit) != 0u) {
-        prev = lz_copy_coop<win_on<M>()>(dic, pos, from, n, r0, cap, mb_pf, &s.win);
+        prev = lz_copy_coop<win_on<M>(), def_on<M>()>(dic, pos, from, n, r0, cap, mb_pf, &s.win);
         pos += n;
       } else {
         prev = lz_copy(dic, pos, from, n, r0, cap);
@@ -2067,6 +2112,7 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
     LZ_PROF_MARK(s, 2, t_prof);
   } while (pos < limit && rd.used() < in_limit);
 
+  if constexpr (def_on<M>()) win_flush(s.win, dic, pos);  // the dictionary complete again
   rc.norm();
   s.range = rc.range;
   s.code = rc.code;
