@@ -34,3 +34,15 @@ done
 LZGPU_LIB=$V/liblzmagpu_prof.so timeout -k 10 300 python -u bench.py --config cfg4 --steps 2 --warmup 1 \
   --no-cpu-baseline --no-gather > $O/prof_cfg4.json 2> $O/prof_cfg4.err || exit $?
 echo "prof: $(grep PROF $O/prof_cfg4.err | cut -c1-1200)"
+# one-lane waves at one wave per SIMD (1,024 config-2 streams, 4 per CU):
+# vector vs scalar-register build, and the cooperative kernel the planner picks
+for round in 1 2; do
+  for q in 0 4; do
+    LZGPU_KERNEL=latency LZGPU_SCALAR=$q timeout -k 10 300 python bench.py --config cfg2 --streams 1024 \
+      --steps 5 --warmup 1 --no-cpu-baseline --no-e2e --no-crc > $O/cfg2s1k_lat_q${q}_r$round.json 2>> $O/ab.err || exit $?
+    echo "cfg2x1024 latency scalar=$q r$round: $(python -c "import json;d=json.load(open('$O/cfg2s1k_lat_q${q}_r$round.json'));print(d['value'], d['ms_per_step'], d['verified'])")"
+  done
+  timeout -k 10 300 python bench.py --config cfg2 --streams 1024 --steps 5 --warmup 1 --no-cpu-baseline \
+    --no-e2e --no-crc > $O/cfg2s1k_auto_r$round.json 2>> $O/ab.err || exit $?
+  echo "cfg2x1024 auto(coop) r$round: $(python -c "import json;d=json.load(open('$O/cfg2s1k_auto_r$round.json'));print(d['value'], d['ms_per_step'], d['verified'])")"
+done
