@@ -640,6 +640,11 @@ constexpr uint32_t kStepBit = 0x10000000u;
 #ifndef LZGPU_WIN_Q
 #define LZGPU_WIN_Q 0
 #endif
+// the checkpoint reader's cooperative kernels decide the plain literal tree by
+// lane speculation (lit8_coop); -DLZGPU_COOP_SPEC=0 (A/B only): one level at a time
+#ifndef LZGPU_COOP_SPEC
+#define LZGPU_COOP_SPEC 1
+#endif
 template <uint32_t M>
 struct BulkReaderFor {
   static constexpr uint32_t m = M & ~(kIlvBit | kStepBit | (LZGPU_WIN_Q ? kWinBit : 0u));
@@ -1321,7 +1326,7 @@ __device__ __forceinline__ void lz_literal(Rc<Rd>& rc, const Tab<M, Lo>& T, uint
   if (full != 0 || total != 0) ctx = ((total & lp_mask) << lc) + (prev >> (8 - lc));
   if (st < 7) {
     st = (st < 4) ? 0 : st - 3;
-    if constexpr (((M & kCoopBit) != 0u) && kIsQ<Rd>) {
+    if constexpr (((M & kCoopBit) != 0u) && kIsQ<Rd> && LZGPU_COOP_SPEC) {
       sym = lit8_coop(rc, T.template at<S_LITP>(ctx << 8));
     } else {
       auto lp = T.template at<S_LITP>(ctx << 8);
