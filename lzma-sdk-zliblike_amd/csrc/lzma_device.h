@@ -640,10 +640,14 @@ constexpr uint32_t kStepBit = 0x10000000u;
 #ifndef LZGPU_WIN_Q
 #define LZGPU_WIN_Q 0
 #endif
-// the checkpoint reader's cooperative kernels decide the plain literal tree by
-// lane speculation (lit8_coop); -DLZGPU_COOP_SPEC=0 (A/B only): one level at a time
+// The cooperative kernels decide the plain literal tree one level at a time,
+// like every other kernel: the lane speculation of rounds 2-3 (lit8_coop, 5 + 3
+// levels per stage) measured slower on the round-4 build everywhere it ran --
+// 8 LZMA2 blocks per CU (no window, checkpoint reader) 5,146 vs 5,494 MB/s, the
+// windowed config 4 3,100 vs 3,318 MB/s (profiles/r04_coop8/, r04_qserial/).
+// -DLZGPU_COOP_SPEC=1 (A/B only) speculates again.
 #ifndef LZGPU_COOP_SPEC
-#define LZGPU_COOP_SPEC 1
+#define LZGPU_COOP_SPEC 0
 #endif
 template <uint32_t M>
 struct BulkReaderFor {
