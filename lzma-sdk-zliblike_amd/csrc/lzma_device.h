@@ -192,6 +192,11 @@ typedef __attribute__((address_space(1))) uint32_t gu32;
 // to its column with cell arithmetic scaled by the row length.
 constexpr uint32_t kIlvBit = 0x40000000u;
 constexpr uint32_t kIlv = 32u;
+// Bit 28 of a placement mask (kStepBit, round 4): the bulk pass runs as the
+// decision-level loop lz_run_step (one range-coder decision per lane per
+// iteration) instead of the symbol loop lz_run; the sections and their
+// placement are those of the rest of the mask.
+constexpr uint32_t kStepBit = 0x10000000u;
 struct GS {
   gu16* p;
   __device__ __forceinline__ GS operator+(uint32_t k) const { return GS{p + kIlv * k}; }
@@ -199,6 +204,22 @@ struct GS {
   __device__ __forceinline__ gu16& operator*() const { return *p; }
 };
 constexpr uint32_t kIlvLaneCells = 1u;
+// The LDS slices of a lane-interleaved throughput class the same way (round 4):
+// cell i of lane l of a 32-lane group at i * 32 + l, so the lanes' reads of
+// different cells (tree nodes of diverging paths) fall in different LDS banks
+// -- bank = (16 i + l / 2) mod 64 -- instead of colliding at random between
+// per-lane slices (config 3: 79 M bank-conflict cycles per launch with slices).
+// Not under the decision-level loop (it indexes the slice directly) nor in the
+// host emulation.  -DLZGPU_LDS_ILV=0 (A/B only) keeps per-lane slices.
+#ifndef LZGPU_LDS_ILV
+#define LZGPU_LDS_ILV 1
+#endif
+struct LS {
+  lds_u16* p;
+  __device__ __forceinline__ LS operator+(uint32_t k) const { return LS{p + kIlv * k}; }
+  __device__ __forceinline__ lds_u16& operator[](uint32_t k) const { return p[kIlv * k]; }
+  __device__ __forceinline__ lds_u16& operator*() const { return *p; }
+};
 
 // Build-time knobs still in use (A/B runs):
 //   LZGPU_LIT_BATCH    literals decoded per pass of the symbol loop before a
@@ -368,6 +389,15 @@ struct LzStateT {
 #endif
 };
 
+template <uint32_t M>
+__host__ __device__ constexpr bool lds_ilv() {
+#ifdef LZGPU_HOST_EMU
+  return false;
+#else
+  return LZGPU_LDS_ILV != 0 && (M & kIlvBit) != 0u && (M & kStepBit) == 0u;
+#endif
+}
+
 // Section accessor for placement mask M (compile-time): at<S>(i) is a pointer to
 // cell i of section S in whichever table holds it.
 template <uint32_t M, class Lo>
@@ -386,10 +416,14 @@ struct Tab {
   }
   template <uint32_t S>
   __device__ __forceinline__ auto at(uint32_t i) const {
-    if constexpr (((M >> S) & 1u) != 0u)
-      return lo + (L.o[S] + i);
-    else
+    if constexpr (((M >> S) & 1u) != 0u) {
+      if constexpr (lds_ilv<M>())
+        return LS{lo + kIlv * (L.o[S] + i)};
+      else
+        return lo + (L.o[S] + i);
+    } else {
       return g(L.o[S] + i);
+    }
   }
 };
 
@@ -623,11 +657,7 @@ template <uint32_t M>
 __host__ __device__ constexpr bool def_on() {
   return LZGPU_WIN_DEFER != 0 && win_on<M>() && (M & kCoopBit) != 0u;
 }
-// Bit 28 of a placement mask (kStepBit, round 4): the bulk pass runs as the
-// decision-level loop lz_run_step (one range-coder decision per lane per
-// iteration) instead of the symbol loop lz_run; the sections and their
-// placement are those of the rest of the mask.
-constexpr uint32_t kStepBit = 0x10000000u;
+// (kStepBit, the decision-level loop's placement bit: with kIlvBit above)
 // every section in LDS (cooperative classes with few streams per CU)
 #ifndef LZGPU_LDS_MASK_ALL
 #define LZGPU_LDS_MASK_ALL 0x7FFu
@@ -2366,7 +2396,11 @@ __device__ __forceinline__ void lz_init_state_real(LzStateT<Lo>& s) {
   } else
 #endif
   {
-    if constexpr ((M & ~kCoopBit) != 0u) fill_prob_init(s.lo, L.lds_cells);
+    if constexpr (lds_ilv<M>()) {
+      for (uint32_t i = 0; i < L.lds_cells; ++i) s.lo[kIlv * i] = uint16_t(kProbInit);
+    } else if constexpr ((M & ~kCoopBit) != 0u) {
+      fill_prob_init(s.lo, L.lds_cells);
+    }
     if constexpr ((M & kIlvBit) != 0u) {
       // the lane's column: one cell per row (the lanes of a group that start
       // together store whole 64-byte rows)

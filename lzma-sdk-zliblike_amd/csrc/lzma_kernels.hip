@@ -94,7 +94,13 @@ __global__ void __launch_bounds__(64, W) lzgpu_decode_lds_kernel(
     LzmaGpuResult* __restrict__ results, uint32_t stride, uint32_t* __restrict__ queue,
     uint64_t slot_off, uint32_t slot_cells, uint32_t base, uint32_t start) {
   extern __shared__ uint32_t lz_smem[];
-  lds_u16* lo = (lds_u16*)((uint16_t*)lz_smem) + threadIdx.x * stride;
+  // the lane's LDS slice; interleaved (lds_ilv): its column of its 32-lane
+  // group's rows
+  lds_u16* lo = (lds_u16*)((uint16_t*)lz_smem);
+  if constexpr (lds_ilv<M>())
+    lo += (threadIdx.x / kIlv) * (kIlv * stride) + (threadIdx.x % kIlv);
+  else
+    lo += threadIdx.x * stride;
   uint32_t idx = base + blockIdx.x * blockDim.x + threadIdx.x;
   gu16* gcol = nullptr;
   if constexpr ((M & kIlvBit) != 0u) {
@@ -302,8 +308,9 @@ static int launch_lds(const LzmaGpuStreamDesc* d_descs, const uint32_t* d_order,
     return -1;
   if (hipMemsetAsync(d_queue, 0, sizeof(uint32_t), stream) != hipSuccess) return -1;
   // pad each workgroup's LDS so that exactly groups_per_cu fit on a CU (an
-  // even split over its four SIMDs), whatever the dispatcher would pack
-  size_t lds = size_t(lanes) * stride * 2;
+  // even split over its four SIMDs), whatever the dispatcher would pack;
+  // interleaved slices take whole 32-lane rows
+  size_t lds = size_t(lds_ilv<M>() ? (lanes + kIlv - 1) / kIlv * kIlv : lanes) * stride * 2;
   if (groups_per_cu) {
     const size_t share = (size_t(160 * 1024) / groups_per_cu) & ~size_t(511);
     if (share > lds) lds = share;
