@@ -179,6 +179,14 @@ void LzmaGpu_DropinTransferStats(uint64_t *h2d_bytes, uint64_t *d2h_bytes, uint6
  * launch.  LZGPU_COALESCE=0 gives every call its own launch.  Any argument may
  * be NULL. */
 void LzmaGpu_CoalesceStats(uint64_t *batches, uint64_t *calls, uint64_t *max_batch, int reset);
+/* Host nanoseconds the one-call batches (LzmaDecode, LzmaUncompress,
+ * Lzma2Decode) spent per phase, summed over batches since the last reset:
+ * ns[0] plan, [1] staging (buffers, packing), [2] upload enqueue, [3] launch
+ * enqueue, [4] waiting for the kernel and the results, [5] output download,
+ * [6] whole batches, [7] every call from entry to return (queueing included);
+ * *batches = batches timed.  Either pointer may be NULL. */
+#define LZMA_GPU_COALESCE_PHASES 8
+void LzmaGpu_CoalesceTimes(uint64_t *ns, uint64_t *batches, int reset);
 
 /* ---------------------------------------------------------------- drop-in LzmaLib.h */
 
@@ -259,7 +267,7 @@ size_t LzmaGpu_PlanBatch(LzmaGpuStreamDesc *descs, size_t n, uint32_t *order);
  * LZGPU_OCC=<1|2|4 waves per SIMD>, LZGPU_CUS, LZGPU_COOP=0|1,
  * LZGPU_PERSIST=0 (one stream per lane), LZGPU_CLASSES=1 (one LDS launch),
  * LZGPU_SLICE_ALIGN8=1, LZGPU_KERNEL_LZMA2=1, LZGPU_COOP_LAT=1, LZGPU_MERGE_LAT=0, LZGPU_ILV=0,
- * LZGPU_ILV_ANY=1, LZGPU_THR_FIT=0, LZGPU_SCALAR=0..4 (the
+ * LZGPU_ILV_ANY=1, LZGPU_THR_FIT=0 (the
  * LZMA_GPU_PLAN_* flags below); DecodeBatchEx reads LZGPU_CLASS_STREAMS=0
  * (classes launched one after another on the caller's stream).
  * workspace_bytes includes the LDS launches' work counters at queue_offset
@@ -288,11 +296,6 @@ typedef struct LzmaGpuLdsClass {
 /* the class holds LZMA2 items: launched on the kernel build with the LZMA2 chunk
  * walker (without it the LZMA-only build runs, fewer registers) */
 #define LZMA_GPU_CLASS_HAS_LZMA2 1u
-/* bits 4-6: of every four one-lane waves of a latency class (placement 0x1BF,
- * lanes_per_group 1), how many run the decoder in scalar registers on the CU's
- * scalar ALU instead of the vector ALU (0-4; set by the planner, see
- * LzmaGpuPlanOptions.scalar_waves) */
-#define LZMA_GPU_CLASS_SCALAR_SHIFT 4
 
 typedef struct LzmaGpuPlan {
   uint64_t workspace_bytes;
@@ -317,9 +320,10 @@ SRes LzmaGpu_PlanBatchEx(LzmaGpuStreamDesc *descs, size_t n, uint32_t *order, Lz
  *               per wave -- the config-3 kernel, whatever the batch size;
  *   LATENCY     placement 0x1BF, one stream per wave (lanes_per_group may
  *               widen it);
- *   COOP        one stream per 32-lane wave, literal trees decided
- *               cooperatively (wave-speculation kernel); placement 0x7FF (all
- *               sections in LDS) where the whole table fits, else 0x1BF;
+ *   COOP        one stream per 32-lane wave, every lane holding the
+ *               stream's state (match copies and direct distance bits
+ *               spread over the lanes); placement 0x7FF (all sections in
+ *               LDS) where the whole table fits, else 0x1BF;
  *   GLOBAL      every stream on the generic kernel (tables in global memory).
  * A class whose latency-placement table exceeds the LDS limit keeps the
  * throughput placement.  cus: CUs to size the plan for (0 = the device's). */
@@ -338,9 +342,9 @@ typedef struct LzmaGpuPlanOptions {
   uint32_t coop;            /* AUTO only: 0 = by streams per CU, 1 = always, 2 = never */
   uint32_t one_class;       /* 1: all LDS-eligible streams in one launch */
   uint32_t flags;           /* LZMA_GPU_PLAN_* bits */
-  /* one-lane latency waves running the scalar-register decoder: 0 = planner
-   * default, 1 + k = k of every four (k = 0..4; LZGPU_SCALAR=k) */
-  uint32_t scalar_waves;
+  /* reserved, 0 (round 4's scalar-register share of one-lane waves, measured
+   * slower at every share and removed in round 5) */
+  uint32_t reserved;
 } LzmaGpuPlanOptions;
 /* per-lane LDS slices 8-byte aligned (default: an odd number of dwords, so that
  * 32 lanes reading the same cell index hit 32 different LDS banks) */
@@ -355,10 +359,6 @@ typedef struct LzmaGpuPlanOptions {
 /* one class per table-width bucket even when several land in the one-lane
  * latency regime (default: those are merged into one class, one launch) */
 #define LZMA_GPU_PLAN_NO_MERGE_LAT 8u
-/* throughput classes run the decision-level loop (round 4: one range-coder
- * decision per lane per iteration, the lane's phase choosing the cell; the
- * symbol loop otherwise) */
-#define LZMA_GPU_PLAN_STEP 0x80u
 /* throughput classes keep the probability sections that are not in LDS in
  * per-stream slices (the round-2 layout) instead of lane-interleaved -- cell i
  * of the 32 lanes of a lane group side by side -- in a slot area per class
@@ -475,7 +475,7 @@ SRes LzmaGpu_SessionDecodeBatch(LzmaGpuSession *d_sessions, size_t n, void *stre
  * LZMA items only (an LZMA2 item: SZ_ERROR_PARAM at plan time). */
 #define LZMA_GPU_SLICED_AUTO 0u
 #define LZMA_GPU_SLICED_LANE 1u   /* one stream per wave, its table staged in LDS per round */
-#define LZMA_GPU_SLICED_COOP 2u   /* one stream per 32-lane wave (literal trees by lane speculation) */
+#define LZMA_GPU_SLICED_COOP 2u   /* one stream per 32-lane wave (the wave-cooperative decoder) */
 #define LZMA_GPU_SLICED_GLOBAL 3u /* one stream per lane, table in the workspace (any lc/lp) */
 typedef struct LzmaGpuSlicedPlan {
   uint64_t workspace_bytes;

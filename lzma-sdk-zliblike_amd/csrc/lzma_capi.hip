@@ -151,18 +151,11 @@ size_t LzmaGpu_PlanBatch(LzmaGpuStreamDesc* descs, size_t n, uint32_t* order) {
   }
 }
 
-// Of every four one-lane latency waves, how many run the scalar-register
-// build (lzgpu_decode_one_kernel) by default: none -- config 2 / config 5 at
-// 0 / 1 / 2 / 3 / 4 quarters: 6.11 / 6.22 / 5.71 / 5.09 / 4.40 and 5.02 / 4.57
-// / 4.60 / 4.49 / 4.14 GB/s (profiles/r04_scalar/).
-constexpr uint32_t kScalarWavesDefault = 0;
-
 // Planner defaults with the experiment overrides of the environment, read at
 // call time (LZGPU_KERNEL=global|throughput|latency|coop, LZGPU_MASK=1|2,
 // LZGPU_COOP=0|1, LZGPU_CUS, LZGPU_LANES, LZGPU_GROUPS, LZGPU_OCC,
 // LZGPU_PERSIST=0, LZGPU_CLASSES=1, LZGPU_SLICE_ALIGN8=1, LZGPU_KERNEL_LZMA2=1,
-// LZGPU_COOP_LAT=1, LZGPU_MERGE_LAT=0, LZGPU_ILV=0, LZGPU_ILV_ANY=1, LZGPU_THR_FIT=0,
-// LZGPU_STEP=1, LZGPU_SCALAR=0..4).  Only LzmaGpu_PlanBatchEx reads them;
+// LZGPU_COOP_LAT=1, LZGPU_MERGE_LAT=0, LZGPU_ILV=0, LZGPU_ILV_ANY=1, LZGPU_THR_FIT=0).  Only LzmaGpu_PlanBatchEx reads them;
 // LzmaGpu_PlanBatchOpt takes its options from the caller alone.
 static LzmaGpuPlanOptions env_options() {
   LzmaGpuPlanOptions o;
@@ -194,10 +187,7 @@ static LzmaGpuPlanOptions env_options() {
             (env_int("LZGPU_MERGE_LAT", 1) ? 0u : LZMA_GPU_PLAN_NO_MERGE_LAT) |
             (env_int("LZGPU_ILV", 1) ? 0u : LZMA_GPU_PLAN_NO_ILV) |
             (env_int("LZGPU_ILV_ANY", 0) ? LZMA_GPU_PLAN_ILV_ANY : 0u) |
-            (env_int("LZGPU_THR_FIT", 1) ? 0u : LZMA_GPU_PLAN_NO_THR_FIT) |
-            (env_int("LZGPU_STEP", 0) ? LZMA_GPU_PLAN_STEP : 0u);
-  const int sc = env_int("LZGPU_SCALAR", -1);
-  o.scalar_waves = (sc >= 0 && sc <= 4) ? uint32_t(sc) + 1u : 0u;
+            (env_int("LZGPU_THR_FIT", 1) ? 0u : LZMA_GPU_PLAN_NO_THR_FIT);
   return o;
 }
 
@@ -352,10 +342,7 @@ static SRes plan_batch(LzmaGpuStreamDesc* descs, size_t n, uint32_t* order, Lzma
                          bool any_groups, bool allow_fit = false) -> LzmaGpuLdsClass {
     bool lat = false;
     const int regime = o.kernel == LZMA_GPU_KERNEL_THROUGHPUT ? 1 : 0;
-    // the decision-level loop keeps one spare LDS cell per lane (lz_run_step)
-    const uint32_t spare = (o.flags & LZMA_GPU_PLAN_STEP) ? 1u : 0u;
-    LzmaGpuLdsClass c = plan_lds_class(stride_lo + spare, idx.size(), LZGPU_LDS_MASK, cus, regime,
-                                       o, &lat);
+    LzmaGpuLdsClass c = plan_lds_class(stride_lo, idx.size(), LZGPU_LDS_MASK, cus, regime, o, &lat);
     const bool want_lat = o.kernel == LZMA_GPU_KERNEL_LATENCY || o.kernel == LZMA_GPU_KERNEL_COOP ||
                           (o.kernel == LZMA_GPU_KERNEL_AUTO && lat);
     if (!want_lat) return c;
@@ -366,7 +353,7 @@ static SRes plan_batch(LzmaGpuStreamDesc* descs, size_t n, uint32_t* order, Lzma
                        o.kernel == LZMA_GPU_KERNEL_AUTO ? 0 : 2, o, nullptr, any_groups,
                        allow_fit);
     // few streams per CU: the wave-cooperative kernel (all 32 lanes on one
-    // stream, literal trees decided by lane speculation) -- config 4
+    // stream, copies and direct bits spread over the lanes) -- config 4
     // 1.71 -> 2.85 GB/s and the xz leg 1.45 -> 2.36 at 4 streams per CU;
     // at 16 per CU (config 2) the single-lane waves are faster (5.9 vs 5.2)
     const uint64_t per_cu_batch = (idx.size() + cus - 1) / cus;
@@ -461,14 +448,6 @@ static SRes plan_batch(LzmaGpuStreamDesc* descs, size_t n, uint32_t* order, Lzma
       c.lds_mask |= lzgpu::kIlvBit;
       if (in_slots.empty()) in_slots.assign(n, 0);
       for (uint32_t i : bucket_idx[b]) in_slots[i] = 1;
-    }
-    if ((o.flags & LZMA_GPU_PLAN_STEP) && (c.lds_mask & ~lzgpu::kIlvBit) == LZGPU_LDS_MASK)
-      c.lds_mask |= lzgpu::kStepBit;
-    if (c.lds_mask == LZGPU_LDS_MASK_LAT && c.lanes_per_group == 1) {
-      // one-lane waves: this many of every four decode in scalar registers
-      const uint32_t q = (o.scalar_waves >= 1 && o.scalar_waves <= 5) ? o.scalar_waves - 1
-                                                                       : kScalarWavesDefault;
-      c.flags |= q << LZMA_GPU_CLASS_SCALAR_SHIFT;
     }
     plan->classes[plan->n_classes++] = c;
     plan->n_lds += c.n;

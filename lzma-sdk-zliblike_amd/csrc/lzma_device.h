@@ -192,11 +192,6 @@ typedef __attribute__((address_space(1))) uint32_t gu32;
 // to its column with cell arithmetic scaled by the row length.
 constexpr uint32_t kIlvBit = 0x40000000u;
 constexpr uint32_t kIlv = 32u;
-// Bit 28 of a placement mask (kStepBit, round 4): the bulk pass runs as the
-// decision-level loop lz_run_step (one range-coder decision per lane per
-// iteration) instead of the symbol loop lz_run; the sections and their
-// placement are those of the rest of the mask.
-constexpr uint32_t kStepBit = 0x10000000u;
 struct GS {
   gu16* p;
   __device__ __forceinline__ GS operator+(uint32_t k) const { return GS{p + kIlv * k}; }
@@ -209,8 +204,7 @@ constexpr uint32_t kIlvLaneCells = 1u;
 // different cells (tree nodes of diverging paths) fall in different LDS banks
 // -- bank = (16 i + l / 2) mod 64 -- instead of colliding at random between
 // per-lane slices (config 3: 79 M bank-conflict cycles per launch with slices).
-// Not under the decision-level loop (it indexes the slice directly) nor in the
-// host emulation.  -DLZGPU_LDS_ILV=0 (A/B only) keeps per-lane slices.
+// Not in the host emulation.  -DLZGPU_LDS_ILV=0 (A/B only) keeps per-lane slices.
 #ifndef LZGPU_LDS_ILV
 #define LZGPU_LDS_ILV 1
 #endif
@@ -255,9 +249,13 @@ struct LS {
 // the window covers is read from LDS instead of global memory -- where, in the
 // in-order vmcnt queue, every such load waited for the wave's earlier output
 // stores.  The window is a write-through cache of the
-// dictionary's last `av` bytes (<= mask + 1): slot = write counter & mask.
-// Every byte the decoder writes goes to both; reads it cannot serve fall back
-// to the dictionary, which is always complete.
+// dictionary's last `av` bytes: slot = write counter & mask.  `av` never
+// exceeds `lim` = min(window bytes, dicBufSize): a ring smaller than the window
+// (a caller's own dic under LzmaDec_AllocateProbs) holds only its last
+// dicBufSize bytes, and a match reaching further reads the ring slot the
+// reference reads (ring_back), overwritten or not.  Every byte the
+// decoder writes goes to both; reads it cannot serve fall back to the
+// dictionary, which is always complete.
 constexpr uint32_t kWinBit = 0x08000000u;
 #ifdef LZGPU_HOST_EMU
 typedef uint8_t lds_u8;
@@ -268,13 +266,57 @@ struct LzWin {
   lds_u8* b;
   uint32_t mask;  // window bytes - 1 (a power of two)
   uint32_t t;     // bytes written through the window
-  uint32_t av;    // of them, still held (the last av)
+  uint32_t av;    // of them, still held and served (the last av, <= lim)
   uint32_t fl;    // of them, not yet stored to the dictionary (deferred output)
+  uint32_t lim;   // av's cap: min(mask + 1, dicBufSize)
 };
+__host__ __device__ __forceinline__ LzWin win_make(lds_u8* b, uint32_t bytes, uint64_t cap) {
+  return LzWin{b, bytes - 1, 0, 0, 0, uint32_t(cap < bytes ? cap : bytes)};
+}
 __device__ __forceinline__ void win_put(LzWin& w, uint32_t v) {
   w.b[w.t & w.mask] = uint8_t(v);
   ++w.t;
-  w.av += (w.av <= w.mask) ? 1u : 0u;
+  w.av += (w.av < w.lim) ? 1u : 0u;
+}
+// the window after n more bytes were written through it
+__device__ __forceinline__ void win_adv(LzWin& w, uint32_t n) {
+  w.t += n;
+  w.av = (w.av + n > w.lim) ? w.lim : w.av + n;
+}
+// Eight window bytes from slot s on, and the low n (1..8) bytes of v to slots
+// s.. -- one unaligned LDS access (gfx950 runs LDS, like global memory, in
+// unaligned mode: ds_read_b64 / ds_write_b64 at any byte address) where the
+// bytes do not cross the window's end, byte by byte where they do.
+#ifdef LZGPU_HOST_EMU
+__device__ __forceinline__ uint64_t lds_ldu64(const lds_u8* p) {
+  uint64_t v;
+  __builtin_memcpy(&v, p, 8);
+  return v;
+}
+__device__ __forceinline__ void lds_stu64(lds_u8* p, uint64_t v) { __builtin_memcpy(p, &v, 8); }
+#else
+typedef uint64_t lz_lds_u64a1 __attribute__((aligned(1)));
+__device__ __forceinline__ uint64_t lds_ldu64(const lds_u8* p) {
+  return *(const __attribute__((address_space(3))) lz_lds_u64a1*)p;
+}
+__device__ __forceinline__ void lds_stu64(lds_u8* p, uint64_t v) {
+  *(__attribute__((address_space(3))) lz_lds_u64a1*)p = v;
+}
+#endif
+__device__ __forceinline__ uint64_t win_ld8(const LzWin& w, uint32_t s) {
+  const uint32_t i = s & w.mask;
+  if (i + 8u <= w.mask + 1u) return lds_ldu64(w.b + i);
+  uint64_t v = 0;
+  for (uint32_t k = 0; k < 8u; ++k) v |= uint64_t(w.b[(s + k) & w.mask]) << (8u * k);
+  return v;
+}
+__device__ __forceinline__ void win_stn(const LzWin& w, uint32_t s, uint64_t v, uint32_t n) {
+  const uint32_t i = s & w.mask;
+  if (n == 8u && i + 8u <= w.mask + 1u) {
+    lds_stu64(w.b + i, v);
+    return;
+  }
+  for (uint32_t k = 0; k < n; ++k) w.b[(s + k) & w.mask] = uint8_t(v >> (8u * k));
 }
 template <uint32_t M>
 __host__ __device__ constexpr bool win_on() {
@@ -299,12 +341,10 @@ constexpr uint32_t kDeferBytes = 64u;
 // state in registers (LzTmp below) the compiler proves that and moves the whole
 // serial decoder to the scalar unit -- measured slower there (config 4 3,060 ->
 // 2,607 MB/s: the scalar build spills hundreds of scalar registers to vector
-// lanes; profiles/r04_tmp/), so the cooperative state stays in vector registers.
-#ifndef LZGPU_COOP_VREG
-#define LZGPU_COOP_VREG 1  // 0: let the cooperative state go scalar (A/B only)
-#endif
+// lanes; profiles/r04_tmp/, the A/B switch retired in round 5), so the
+// cooperative state stays in vector registers.
 __device__ __forceinline__ uint32_t lz_vzero() {
-#if defined(LZGPU_HOST_EMU) || !LZGPU_COOP_VREG
+#if defined(LZGPU_HOST_EMU)
   return 0;
 #else
   uint32_t z;
@@ -318,18 +358,9 @@ __device__ __forceinline__ uint32_t lz_vzero() {
 // be a dynamically indexed private array inside the decoder state, and the
 // compiler keeps a structure that an unknown index reaches into in scratch
 // memory as a whole -- the range coder, positions and reps included -- with
-// every value read back from it a per-lane load; as words it is registers.
-// (-DLZGPU_TMP_BYTES=1: the byte array, A/B only.)
-#ifndef LZGPU_TMP_BYTES
-#define LZGPU_TMP_BYTES 0
-#endif
-#if LZGPU_TMP_BYTES
-struct LzTmp {
-  uint8_t b[kLookahead];
-  __device__ __forceinline__ uint32_t get(uint32_t i) const { return b[i]; }
-  __device__ __forceinline__ void set(uint32_t i, uint32_t v) { b[i] = uint8_t(v); }
-};
-#else
+// every value read back from it a per-lane load; as words it is registers
+// (round 4: config 3 +1.9 %, config 2 +2.3 %; the byte-array A/B build was
+// retired in round 5).
 struct LzTmp {
   uint64_t w0, w1, w2;
   __device__ __forceinline__ uint32_t get(uint32_t i) const {
@@ -344,7 +375,6 @@ struct LzTmp {
     w2 = i >= 16u ? ((w2 & m) | v) : w2;
   }
 };
-#endif
 // byte pointer over an LzTmp (the look-ahead probe of the tempBuf path)
 struct LzTmpIter {
   LzTmp t;
@@ -394,7 +424,7 @@ __host__ __device__ constexpr bool lds_ilv() {
 #ifdef LZGPU_HOST_EMU
   return false;
 #else
-  return LZGPU_LDS_ILV != 0 && (M & kIlvBit) != 0u && (M & kStepBit) == 0u;
+  return LZGPU_LDS_ILV != 0 && (M & kIlvBit) != 0u;
 #endif
 }
 
@@ -651,39 +681,30 @@ typedef GlobalReader16 PlainReader;
 // NORMALIZE fires in some lane almost every decision), the per-byte-checked
 // one elsewhere (one lane per wave: config 2 5.8 vs 5.2 GB/s).
 // Bit 31 of a placement mask marks the wave-cooperative kernel (kCoopBit: one
-// stream per wave, every lane holding the same state; lit8_coop).
+// stream per wave, every lane holding the same state).
 constexpr uint32_t kCoopBit = 0x80000000u;
 template <uint32_t M>
 __host__ __device__ constexpr bool def_on() {
   return LZGPU_WIN_DEFER != 0 && win_on<M>() && (M & kCoopBit) != 0u;
 }
-// (kStepBit, the decision-level loop's placement bit: with kIlvBit above)
 // every section in LDS (cooperative classes with few streams per CU)
 #ifndef LZGPU_LDS_MASK_ALL
 #define LZGPU_LDS_MASK_ALL 0x7FFu
 #endif
-// Windowed cooperative builds (kWinBit) take the per-byte reader and with it
-// the serial literal tree (lz_literal without lit8_coop): measured faster than
-// the checkpoint reader with the speculative stages once the window is there --
-// config 4 3,187 vs 3,060 MB/s, xz 2,834 vs 2,642, config 1 2.71 vs 2.49 MB/s
-// (profiles/r04_tmp/).  -DLZGPU_WIN_Q=1 (A/B only) keeps the checkpoint reader.
-#ifndef LZGPU_WIN_Q
-#define LZGPU_WIN_Q 0
-#endif
-// The cooperative kernels decide the plain literal tree one level at a time,
-// like every other kernel: the lane speculation of rounds 2-3 (lit8_coop, 5 + 3
-// levels per stage) measured slower on the round-4 build everywhere it ran --
-// 8 LZMA2 blocks per CU (no window, checkpoint reader) 5,146 vs 5,494 MB/s, the
-// windowed config 4 3,100 vs 3,318 MB/s (profiles/r04_coop8/, r04_qserial/).
-// -DLZGPU_COOP_SPEC=1 (A/B only) speculates again.
-#ifndef LZGPU_COOP_SPEC
-#define LZGPU_COOP_SPEC 0
-#endif
+// Windowed cooperative builds (kWinBit) take the per-byte reader: measured
+// faster than the checkpoint reader once the window is there -- config 4 3,187
+// vs 3,060 MB/s, xz 2,834 vs 2,642, config 1 2.71 vs 2.49 MB/s
+// (profiles/r04_tmp/, r04_qserial/).  Every kernel decides the plain literal
+// tree one level at a time: the lane speculation of rounds 2-3 (5 + 3 levels
+// per stage on the cooperative kernel) measured slower on the round-4 build
+// everywhere it ran -- 8 LZMA2 blocks per CU 5,146 vs 5,494 MB/s, the windowed
+// config 4 3,100 vs 3,318 MB/s (profiles/r04_coop8/, r04_qserial/) -- and was
+// removed in round 5 with the other rejected shapes.
 template <uint32_t M>
 struct BulkReaderFor {
-  static constexpr uint32_t m = M & ~(kIlvBit | kStepBit | (LZGPU_WIN_Q ? kWinBit : 0u));
+  static constexpr uint32_t m = M & ~kIlvBit;
   static constexpr bool q = m == LZGPU_LDS_MASK || m == (LZGPU_LDS_MASK_LAT | kCoopBit) ||
-                            m == (LZGPU_LDS_MASK_ALL | kCoopBit) || (M & kStepBit) != 0u;
+                            m == (LZGPU_LDS_MASK_ALL | kCoopBit);
   typedef typename std::conditional<q, GlobalReaderQ, PlainReader>::type type;
 };
 
@@ -695,7 +716,7 @@ struct BulkReaderFor {
 // within noise either way: profiles/r02_ilv/mbpf_latency_ab.log)
 template <uint32_t M>
 __host__ __device__ constexpr bool mb_pf_on() {
-  return ((M & kCoopBit) != 0u) || ((M & ~(kIlvBit | kStepBit)) == LZGPU_LDS_MASK);
+  return ((M & kCoopBit) != 0u) || ((M & ~kIlvBit) == LZGPU_LDS_MASK);
 }
 
 // checkpoint hooks for readers without them: every NORMALIZE checks
@@ -897,100 +918,12 @@ struct Rc {
   }
 };
 
-// ------------------------------------------------------------------ wave-cooperative tree stage
-//
-// Latency placement, cooperative kernel (one stream per wave, all lanes hold the
-// same decoder state): L levels of an MSB-first bit tree below node m0 decoded at
-// once.  Lane j assumes the path bits j (MSB first) and runs the L decisions of
-// that path on its own copy of (range, code, input window): with the bits assumed,
-// each level's new range/code follow from the assumption without waiting for the
-// comparison, and the L cells were read in one batch -- the comparisons only
-// verify the assumption.  Exactly one path is consistent with all L comparisons
-// (the one the serial decoder takes); its lane's state is broadcast and it alone
-// stores its L probability updates.  The reader must hold >= L bytes (a
-// checkpoint precedes the stage).  Returns the node reached (m0 << L | bits).
+// lane index within the wave (0 in the host emulation)
 #ifdef LZGPU_HOST_EMU
 __device__ __forceinline__ uint32_t lz_lane_id() { return 0; }
 #else
 __device__ __forceinline__ uint32_t lz_lane_id() { return __lane_id(); }
 #endif
-
-template <int L>
-struct SpecPath {
-  uint32_t range, code, nb;
-  uint64_t win;
-  uint32_t np[L];
-  bool ok;
-};
-
-template <int L, class P>
-__device__ __forceinline__ void spec_path(uint32_t j, uint32_t m0, P probs, uint32_t range,
-                                          uint32_t code, uint64_t win, uint32_t nb,
-                                          SpecPath<L>& o) {
-  uint32_t pv[L];
-#pragma unroll
-  for (int k = 0; k < L; ++k) pv[k] = probs[(m0 << k) | (j >> (L - k))];
-  bool ok = true;
-#pragma unroll
-  for (int k = 0; k < L; ++k) {
-    const bool n = range < kTop;  // NORMALIZE (LzmaDec.c:17), branch-free per lane
-    code = n ? ((code << 8) | uint32_t(win & 0xFFu)) : code;
-    range = n ? (range << 8) : range;
-    win = n ? (win >> 8) : win;
-    nb -= n ? 1u : 0u;
-    const uint32_t bound = (range >> 11) * pv[k];
-    const bool bk = ((j >> (L - 1 - k)) & 1u) != 0u;
-    ok = ok && ((code >= bound) == bk);
-    o.np[k] = uint32_t(int32_t(pv[k]) - ((int32_t(pv[k]) - (bk ? 0 : int32_t(kProbOne - 31))) >> 5));
-    range = bk ? range - bound : bound;
-    code = bk ? code - bound : code;
-  }
-  o.range = range;
-  o.code = code;
-  o.win = win;
-  o.nb = nb;
-  o.ok = ok;
-}
-
-template <int L, class Rd, class P>
-__device__ __forceinline__ uint32_t spec_stage(Rc<Rd>& rc, P probs, uint32_t m0) {
-  constexpr uint32_t kPaths = 1u << L;
-  SpecPath<L> o;
-  uint32_t w;
-#ifdef LZGPU_HOST_EMU
-  for (w = 0; w < kPaths; ++w) {
-    spec_path<L>(w, m0, probs, rc.range, rc.code, rc.rd->win, rc.rd->nb, o);
-    if (o.ok) break;
-  }
-#else
-  const uint32_t j = lz_lane_id() & (kPaths - 1u);
-  spec_path<L>(j, m0, probs, rc.range, rc.code, rc.rd->win, rc.rd->nb, o);
-  const uint64_t hits = __builtin_amdgcn_ballot_w64(o.ok);
-  const uint32_t wl = uint32_t(__builtin_ctzll(hits));  // wave-uniform winner lane
-  w = wl & (kPaths - 1u);
-  o.range = uint32_t(__builtin_amdgcn_readlane(int(o.range), int(wl)));
-  o.code = uint32_t(__builtin_amdgcn_readlane(int(o.code), int(wl)));
-  o.nb = uint32_t(__builtin_amdgcn_readlane(int(o.nb), int(wl)));
-  const uint32_t wlo = uint32_t(__builtin_amdgcn_readlane(int(uint32_t(o.win)), int(wl)));
-  const uint32_t whi = uint32_t(__builtin_amdgcn_readlane(int(uint32_t(o.win >> 32)), int(wl)));
-  o.win = uint64_t(wlo) | (uint64_t(whi) << 32);
-  // every lane stores the winner's updates (wave-uniform cells and values):
-  // no exec-mask region around the stores (round 3: config 4 -2.2 % time
-  // against the winner lane storing alone)
-#pragma unroll
-  for (int k = 0; k < L; ++k)
-    probs[(m0 << k) | (w >> (L - k))] =
-        uint16_t(__builtin_amdgcn_readlane(int(o.np[k]), int(wl)));
-#endif
-#ifdef LZGPU_HOST_EMU
-  for (int k = 0; k < L; ++k) probs[(m0 << k) | (w >> (L - k))] = uint16_t(o.np[k]);
-#endif
-  rc.range = o.range;
-  rc.code = o.code;
-  rc.rd->win = o.win;
-  rc.rd->nb = o.nb;
-  return (m0 << L) | w;
-}
 
 // Direct bits of a distance (LzmaDec.c:323-344), several per step, on the
 // wave-cooperative kernel (round 4).  A direct bit reads
@@ -1056,16 +989,6 @@ __device__ __forceinline__ void direct_coop(Rc<Rd>& rc, uint32_t& dist, uint32_t
     }
     left -= k;
   } while (left != 0);
-}
-
-// the plain literal tree in two cooperative stages (5 + 3 levels); the caller's
-// IsMatch checkpoint is followed by one here, and one between the stages
-template <class Rd, class P>
-__device__ __forceinline__ uint32_t lit8_coop(Rc<Rd>& rc, P probs) {
-  rc.rd->topup();
-  const uint32_t m = spec_stage<5>(rc, probs, 1u);
-  rc.rd->topup();
-  return spec_stage<3>(rc, probs, m);
 }
 
 // Copy n bytes of an LZ match: dic[pos..pos+n) = dic[from..], byte-serial
@@ -1260,8 +1183,7 @@ __device__ __forceinline__ uint32_t lz_copy_coop(gbyte* dic, uint64_t pos, uint6
     for (uint32_t j = 0; j < n; ++j) dic[pos + j] = v[j];
   if constexpr (WIN) {
     for (uint32_t j = 0; j < n; ++j) w->b[(w->t + j) & w->mask] = v[j];
-    w->t += n;
-    w->av = (w->av + n > w->mask + 1) ? w->mask + 1 : w->av + n;
+    win_adv(*w, n);
   }
   if constexpr (DEF) {
     w->fl += n;
@@ -1311,8 +1233,7 @@ __device__ __forceinline__ uint32_t lz_copy_coop(gbyte* dic, uint64_t pos, uint6
     my_mb = (j == n) ? v : my_mb;
   }
   if constexpr (WIN) {
-    w->t += n;
-    w->av = (w->av + n > w->mask + 1) ? w->mask + 1 : w->av + n;
+    win_adv(*w, n);
   }
   if constexpr (DEF) {
     // (the window bytes other lanes just wrote are seen by the flush's LDS
@@ -1323,6 +1244,163 @@ __device__ __forceinline__ uint32_t lz_copy_coop(gbyte* dic, uint64_t pos, uint6
   mb = uint32_t(__builtin_amdgcn_readlane(int(my_mb), int(n & (kCoopLanes - 1u))));
   return uint32_t(__builtin_amdgcn_readlane(int(my_last), int((n - 1) & (kCoopLanes - 1u))));
 #endif
+}
+
+// ------------------------------------------------------------------ one-lane window
+//
+// The LDS history window on the one-stream-per-wave latency kernel (round 5,
+// VERDICT r04 item 2; placement LZGPU_LDS_MASK_LAT | kWinBit, lwin_on): a
+// matched literal's byte (LzmaDec.c:176), a short rep's byte (:216) and a match
+// copy's source (:388-407) within the window's reach are LDS reads -- on the
+// one-lane kernel each such global load waited in the in-order vmcnt queue for
+// the lane's earlier output stores.  It runs on flat dictionaries only (batch
+// items: LzmaDecode's output window, LZMA2 ranges), where every byte the
+// decoder writes passes the window once in dictionary order, so window slot =
+// dictionary position & mask and a distance the window holds is simply one
+// <= its size (the decoder's own check keeps every distance <= the position):
+// no write counter or fill level to carry in registers.
+// ldef_on: deferred output, the cooperative kernels' idea (def_on) for a lane
+// alone -- decoded bytes go to the window only and reach the dictionary 16 at a
+// time (one aligned LDS read and one 16-byte global store per 16 output bytes,
+// instead of a byte store per literal and 8-byte stores per copy), the last
+// partial 16 before the bulk pass returns.  A read the window does not serve
+// (dist > its size >= 1 KiB) lies before every pending byte.
+// -DLZGPU_LANE_DEFER=0 writes through (A/B).
+#ifndef LZGPU_LANE_DEFER
+#define LZGPU_LANE_DEFER 1
+#endif
+template <uint32_t M>
+__host__ __device__ constexpr bool lwin_on() {
+  return win_on<M>() && (M & kCoopBit) == 0u;
+}
+template <uint32_t M>
+__host__ __device__ constexpr bool ldef_on() {
+  return LZGPU_LANE_DEFER != 0 && lwin_on<M>();
+}
+// the byte of dictionary position p to its window slot (one-lane window)
+__device__ __forceinline__ void win_put_at(const LzWin& w, uint64_t p, uint32_t v) {
+  w.b[uint32_t(p) & w.mask] = uint8_t(v);
+}
+#ifdef LZGPU_HOST_EMU
+__device__ __forceinline__ void win_store16(const LzWin& w, gbyte* dic, uint64_t c) {
+  __builtin_memcpy(dic + c - 16, w.b + ((uint32_t(c) - 16u) & w.mask), 16);
+}
+#else
+typedef unsigned int lz_w32x4 __attribute__((ext_vector_type(4)));
+typedef lz_w32x4 lz_w32x4a1 __attribute__((aligned(1)));
+// dictionary bytes [c - 16, c) (c a multiple of 16) from their window slots:
+// one aligned LDS read, one 16-byte global store
+__device__ __forceinline__ void win_store16(const LzWin& w, gbyte* dic, uint64_t c) {
+  const lz_w32x4 v =
+      *(const __attribute__((address_space(3))) lz_w32x4*)(w.b + ((uint32_t(c) - 16u) & w.mask));
+  *(__attribute__((address_space(1))) lz_w32x4a1*)(dic + c - 16) = v;
+#if LZGPU_SHADOW_OUT
+  *(__attribute__((address_space(1))) lz_w32x4a1*)(dic + c - 16 + LZGPU_SHADOW_OUT) = v;
+#endif
+}
+#endif
+// every 16-byte chunk that positions [p0, p1) completed, to the dictionary
+__device__ __forceinline__ void win_store_chunks(const LzWin& w, gbyte* dic, uint64_t p0,
+                                                 uint64_t p1) {
+  for (uint64_t c = (p0 + 16u) & ~uint64_t(15); c <= p1; c += 16u) win_store16(w, dic, c);
+}
+// the pending bytes of the last, partial chunk, [pos - (pos & 15), pos), to
+// the dictionary: it is complete again
+__device__ __forceinline__ void win_store_tail(const LzWin& w, gbyte* dic, uint64_t pos) {
+  const uint32_t k = uint32_t(pos) & 15u;
+  if (k == 0) return;
+  gbyte* d = dic + pos - k;
+  const uint32_t s0 = uint32_t(pos) - k;
+  const uint64_t lo = win_ld8(w, s0);
+  if (k >= 8) {
+    stu64(d, lo);
+    stu_tail(d + 8, win_ld8(w, s0 + 8), k - 8);
+  } else {
+    stu_tail(d, lo, k);
+  }
+}
+// one output byte at pos (literal / short rep), under every placement
+template <uint32_t M>
+__device__ __forceinline__ void lz_emit(gbyte* dic, uint64_t pos, uint32_t v, LzWin* w) {
+  if constexpr (ldef_on<M>()) {
+    win_put_at(*w, pos, v);
+    if (((uint32_t(pos) + 1u) & 15u) == 0) win_store16(*w, dic, pos + 1);
+  } else {
+    lz_put(dic + pos, v);
+    if constexpr (lwin_on<M>())
+      win_put_at(*w, pos, v);
+    else if constexpr (win_on<M>())
+      win_put(*w, v);
+  }
+}
+// the byte at distance dist before pos: from the one-lane window where it reaches
+template <uint32_t M>
+__device__ __forceinline__ uint32_t lz_back(const gbyte* dic, uint64_t pos, uint32_t dist,
+                                            uint64_t cap, const LzWin* w) {
+  if constexpr (lwin_on<M>()) {
+    if (dist <= w->mask + 1u) return w->b[(uint32_t(pos) - dist) & w->mask];
+  }
+  return dic[ring_back(pos, dist, cap)];
+}
+// LZ copy of the one-lane window kernel (flat dictionary: the source
+// dic[pos - dist, ...) never wraps): lz_copy's shapes -- 8 bytes per step,
+// the period of a distance < 8 built once in a register -- with the source
+// from the window when it reaches and every byte written to the window (and,
+// writing through, to the dictionary).  Returns the last byte copied.
+template <bool DEF>
+__device__ __forceinline__ uint32_t lz_copy_lw(gbyte* dic, uint64_t pos, uint32_t n, uint32_t dist,
+                                               const LzWin& w) {
+  const uint32_t t = uint32_t(pos);
+  const bool inwin = dist <= w.mask + 1u;
+  gbyte* d = dic + pos;
+  const gbyte* src = d - dist;
+  uint32_t last;
+  uint64_t v = 0;
+  if (dist >= 8) {
+    // source bytes [i, i + 8) of step i lie at least 8 bytes behind its
+    // destination: written before the step reads them
+    uint32_t i = 0;
+    for (; i + 8 <= n; i += 8) {
+      v = inwin ? win_ld8(w, t - dist + i) : ldu64(src + i);
+      win_stn(w, t + i, v, 8);
+      if constexpr (!DEF) stu64(d + i, v);
+    }
+    last = uint32_t(v >> 56);
+    if (i < n) {
+      v = inwin ? win_ld8(w, t - dist + i) : ldu64(src + i);
+      const uint32_t rem = n - i;
+      win_stn(w, t + i, v, rem);
+      if constexpr (!DEF) stu_tail(d + i, v, rem);
+      last = uint32_t(v >> (8 * (rem - 1))) & 0xFFu;
+    }
+  } else {
+    // dist < 8 (inside any window): the dist bytes before pos repeated
+    v = win_ld8(w, t - dist);
+    v &= ~0ull >> (64 - 8 * dist);
+    v |= v << (8 * dist);
+    if (dist < 4) v |= v << (16 * dist);
+    if (dist < 2) v |= v << 32;
+    const uint32_t ph = 8u % dist;  // phase advance per 8 bytes
+    for (uint32_t i = 0;; i += 8) {
+      const uint32_t rem = n - i;
+      if (rem <= 8) {
+        win_stn(w, t + i, v, rem);
+        if constexpr (!DEF) {
+          if (rem == 8)
+            stu64(d + i, v);
+          else
+            stu_tail(d + i, v, rem);
+        }
+        last = uint32_t(v >> (8 * (rem - 1))) & 0xFFu;
+        break;
+      }
+      win_stn(w, t + i, v, 8);
+      if constexpr (!DEF) stu64(d + i, v);
+      v = (v >> (8 * ph)) | (v << (8 * (dist - ph)));
+    }
+  }
+  if constexpr (DEF) win_store_chunks(w, dic, pos, pos + n);
+  return last;
 }
 
 // ------------------------------------------------------------------ symbol loop
@@ -1360,16 +1438,12 @@ __device__ __forceinline__ void lz_literal(Rc<Rd>& rc, const Tab<M, Lo>& T, uint
   if (full != 0 || total != 0) ctx = ((total & lp_mask) << lc) + (prev >> (8 - lc));
   if (st < 7) {
     st = (st < 4) ? 0 : st - 3;
-    if constexpr (((M & kCoopBit) != 0u) && kIsQ<Rd> && LZGPU_COOP_SPEC) {
-      sym = lit8_coop(rc, T.template at<S_LITP>(ctx << 8));
-    } else {
-      auto lp = T.template at<S_LITP>(ctx << 8);
-      const uint32_t m = rc.template tree_u<4>(lp, 1);
-      rd_topup(*rc.rd);
-      sym = rc.template tree_u<4>(lp, m);
-    }
+    auto lp = T.template at<S_LITP>(ctx << 8);
+    const uint32_t m = rc.template tree_u<4>(lp, 1);
+    rd_topup(*rc.rd);
+    sym = rc.template tree_u<4>(lp, m);
   } else {
-    uint32_t mbyte = mb_pf_on<M>() ? mb_pf : uint32_t(dic[ring_back(pos, r0, cap)]);
+    uint32_t mbyte = mb_pf_on<M>() ? mb_pf : lz_back<M>(dic, pos, r0, cap, w);
     st = (st < 10) ? st - 3 : st - 6;
     constexpr bool p_lds = ((M >> S_LITP) & 1u) != 0u, m_lds = ((M >> S_LITM) & 1u) != 0u;
     if constexpr (p_lds && !m_lds) {
@@ -1415,8 +1489,7 @@ __device__ __forceinline__ void lz_literal(Rc<Rd>& rc, const Tab<M, Lo>& T, uint
     win_put(*w, prev);
     if (++w->fl >= kDeferBytes) win_flush(*w, dic, pos + 1);
   } else {
-    lz_put(dic + pos, prev);
-    if constexpr (win_on<M>()) win_put(*w, prev);
+    lz_emit<M>(dic, pos, prev, w);
   }
   pos++;
   total++;
@@ -1446,361 +1519,12 @@ __device__ __forceinline__ bool lz_any(bool v) {
 }
 
 
-// ------------------------------------------------------------------ decision-level loop
-//
-// lz_run_step: the same contract as lz_run (one LzmaDec_DecodeReal pass,
-// LzmaDec.c:131-426: symbols until pos reaches `limit` or the reader reaches
-// `in_limit`, checked after each whole symbol; state written back only on
-// success), restructured for SIMT.  lz_run follows the reference's control
-// flow -- a symbol is a nest of branches, and the lanes of a wave sit in
-// different branches (literal runs of different lengths, plain vs matched
-// literals, the match path's kinds), so a wave executes the union of its
-// lanes' paths: 11.1 of 32 lanes active per VALU instruction on config 3
-// (profiles/r03_final/pmc_summary.json).  Here each lane is a small state
-// machine and every iteration of ONE loop makes exactly one range-coder
-// decision per lane: the lane's phase picks the probability cell (IsMatch, a
-// literal-tree node, a rep bit, a length / slot / SpecPos / align node) or a
-// direct bit, and the normalise / bound / compare / update sequence
-// (LzmaDec.c:8-45, 323-344) is shared by all lanes whatever their phase.  At
-// the end of a phase (a tree's last level, a single-bit decision) the lane
-// takes its transition -- the symbol grammar of LzmaDec.c:160-411 -- and
-// match copies run as their own (non-decision) phase.
-enum : uint32_t {
-  PH_LIT = 0,   // literal tree level (LzmaDec.c:161-196): plain, or matched while
-                // the decoded bits follow the match byte
-  PH_ISMATCH,   // IsMatch[state][posState] (:158-160)
-  PH_REP,       // IsRep / IsRepG0 / IsRepG1 / IsRepG2 [state] (:201-258): `aux` = which
-  PH_REP0L,     // IsRep0Long[state][posState] (:213-228)
-  PH_LCH,       // length choice (:263-268)
-  PH_LCH2,      // length choice2 (:270-285)
-  PH_LTREE,     // low / mid / high length tree; len = node + aux at its end
-  PH_SLOT,      // position slot tree (:295-300)
-  PH_SPEC,      // SpecPos reverse tree (:306-321), `aux` = its bits
-  PH_DIRECT,    // direct bits (:323-344), accumulated in `node`
-  PH_ALIGN,     // Align reverse tree (:345-353)
-  PH_COPY,      // the LZ copy of a match / rep / short rep (:373-408), no decision
-  PH_END        // pass over (`err` set on SZ_ERROR_DATA)
-};
-
-__host__ __device__ __forceinline__ uint32_t lz_bitrev(uint32_t v, uint32_t n) {
-#ifdef LZGPU_HOST_EMU
-  uint32_t r = 0;
-  for (uint32_t k = 0; k < n; ++k) r |= ((v >> k) & 1u) << (n - 1 - k);
-  return r;
-#else
-  return n ? (__builtin_bitreverse32(v) >> (32 - n)) : 0u;
-#endif
-}
-
-// Code shape (the second of two builds measured): lane
-// flags as integers (no lane-mask merges at every join), NORMALIZE as selects
-// on the checkpoint reader, the probability read from LDS for every lane (a
-// spare cell for lanes whose cell is global or who decode a direct bit) with
-// only the global read and store under a branch, and the literal path's
-// transitions (IsMatch -> literal -> IsMatch) ahead of the rest of the grammar.
-template <uint32_t M, class Lo, class Rd>
-__device__ __forceinline__ int lz_run_step(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
-                                           uint32_t in_limit) {
-  const Tab<M, Lo> T(s);
-  constexpr auto lds_of = [](uint32_t sec) { return ((M >> sec) & 1u) != 0u; };
-  constexpr uint32_t G_MATCH = lds_of(S_MATCH) ? 0u : 1u, G_REP = lds_of(S_REP) ? 0u : 1u,
-                     G_REP0L = lds_of(S_REP0L) ? 0u : 1u, G_LEN = lds_of(S_LEN) ? 0u : 1u,
-                     G_LENHI = lds_of(S_LENHI) ? 0u : 1u, G_SLOT = lds_of(S_SLOT) ? 0u : 1u,
-                     G_SPEC = lds_of(S_SPEC) ? 0u : 1u, G_ALIGN = lds_of(S_ALIGN) ? 0u : 1u,
-                     G_LITP = lds_of(S_LITP) ? 0u : 1u, G_LITM = lds_of(S_LITM) ? 0u : 1u;
-  static_assert(lds_of(S_LEN) == lds_of(S_REPLEN), "Len/RepLen placement");
-  const uint32_t pb = s.pb, lc = s.lc;
-  const uint32_t pb_mask = (1u << pb) - 1, lp_mask = (1u << s.lp) - 1;
-  gbyte* __restrict__ dic = s.dic;
-  const uint64_t cap = s.cap;
-  const uint32_t full = s.full;
-  uint64_t pos = s.pos;
-  uint32_t total = s.total, st = s.st;
-  uint32_t r0 = s.rep0, r1 = s.rep1, r2 = s.rep2, r3 = s.rep3;
-  uint32_t range = s.range, code = s.code;
-  uint32_t len = 0, prev = 0, mbp = 0;
-  if (full != 0 || total != 0) prev = dic[(pos == 0 ? cap : pos) - 1];
-  if (st >= 7) mbp = dic[ring_back(pos, r0, cap)];
-  const uint32_t o_match = T.L.o[S_MATCH], o_rep = T.L.o[S_REP], o_rep0l = T.L.o[S_REP0L];
-  const uint32_t o_len = T.L.o[S_LEN], o_replen = T.L.o[S_REPLEN], o_lenhi = T.L.o[S_LENHI];
-  const uint32_t o_slot = T.L.o[S_SLOT], o_spec = T.L.o[S_SPEC], o_align = T.L.o[S_ALIGN];
-  const uint32_t o_litp = T.L.o[S_LITP], o_litm = T.L.o[S_LITM];
-  // the lane's spare LDS cell (one past its sections; the planner reserves
-  // it): reads and stores of lanes whose cell is global, or who decode a
-  // direct bit, go there instead of behind a branch
-  const uint32_t spare = T.L.lds_cells;
-  uint32_t ph = PH_ISMATCH, node = 1, left = 1, aux = 0, dist = 0;
-  uint32_t cb = o_match + (st << pb) + (total & pb_mask) - 1, cg = G_MATCH;
-  uint32_t mlm = 0, lrep = 0, mb = 0, litm = 0, lcoff = o_len;
-  int err = kOk;
-  uint32_t it = 0;
-  while (lz_any(ph != PH_END)) {
-    // reader checkpoint every 4 iterations (one NORMALIZE each at most); a
-    // finished lane's reader keeps used() unchanged
-    if ((it++ & 3u) == 0u) rd_topup(rd);
-    if (ph < PH_COPY) {
-      const uint32_t mk = (mb >> 7) & 1u;
-      const uint32_t ci = mlm ? litm + (mk << 8) + node : cb + node;
-      const uint32_t g = mlm ? G_LITM : cg;
-      const uint32_t dir = ph == PH_DIRECT ? 1u : 0u;  // DIRECT lanes carry cg = 0
-      const uint32_t la = (g | dir) ? spare : ci;
-      uint32_t p = T.lo[la];
-      if (g) p = *T.g(ci);
-      // NORMALIZE (LzmaDec.c:17)
-      if constexpr (kIsQ<Rd>) {
-        const bool n = range < kTop;
-        code = n ? (code << 8) | uint32_t(rd.win & 0xFFu) : code;
-        range = n ? range << 8 : range;
-        rd.win = n ? rd.win >> 8 : rd.win;
-        rd.nb -= n ? 1u : 0u;
-      } else {
-        if (range < kTop) {
-          range <<= 8;
-          code = (code << 8) | rd.next();
-        }
-      }
-      const uint32_t bound = dir ? (range >> 1) : (range >> 11) * p;
-      const uint32_t bit = dir ? (int32_t(code - bound) >= 0 ? 1u : 0u) : (code >= bound ? 1u : 0u);
-      code = bit ? code - bound : code;
-      range = (dir | (bit ^ 1u)) ? bound : range - bound;
-      const int32_t m = bit ? 0 : int32_t(kProbOne - 31);
-      const uint32_t np = uint32_t(int32_t(p) - ((int32_t(p) - m) >> 5));
-      T.lo[la] = uint16_t(np);
-      if (g) *T.g(ci) = uint16_t(np);
-      node = 2 * node + bit;
-      mlm &= (bit == mk) ? 1u : 0u;
-      mb = (mb << 1) & 0xFFu;
-      --left;
-      if (left == 0) {
-        if (ph == PH_LIT) {
-          // ---- a literal is complete (LzmaDec.c:196-197)
-          prev = node & 0xFFu;
-          lz_put(dic + pos, prev);
-          ++pos;
-          ++total;
-          mlm = 0;
-          const bool more = pos < limit && rd.used() < in_limit;  // LzmaDec.c:410
-          ph = more ? PH_ISMATCH : PH_END;
-          cb = o_match + (st << pb) + (total & pb_mask) - 1;
-          cg = G_MATCH;
-          node = 1;
-          left = 1;
-        } else if (ph == PH_ISMATCH) {
-          if (!bit) {
-            // ---- a literal (LzmaDec.c:161-196)
-            const uint32_t ctx =
-                (full != 0 || total != 0) ? ((total & lp_mask) << lc) + (prev >> (8 - lc)) : 0u;
-            cb = o_litp + (ctx << 8);
-            cg = G_LITP;
-            mlm = st >= 7 ? 1u : 0u;
-            mb = mbp & 0xFFu;
-            litm = o_litm + (ctx << 9);
-            st = st < 4 ? 0u : (st < 10 ? st - 3 : st - 6);
-            ph = PH_LIT;
-            left = 8;
-          } else {
-            ph = PH_REP;
-            aux = 0;
-            cb = o_rep + st - 1;
-            cg = G_REP;
-            left = 1;
-          }
-          node = 1;
-        } else {
-          // ---- the rest of the grammar (LzmaDec.c:199-371)
-          switch (ph) {
-            case PH_REP:
-              if (aux == 0 && !bit) {  // a match: state + 12 marks it until the distance
-                st += 12;
-                lrep = 0;
-                ph = PH_LCH;
-              } else if (aux == 0 && full == 0 && total == 0) {
-                err = kErrData;
-                ph = PH_END;
-              } else if (aux == 1 && !bit) {
-                ph = PH_REP0L;
-                cb = o_rep0l + (st << pb) + (total & pb_mask) - 1;
-                cg = G_REP0L;
-              } else if (aux < 2 || (aux == 2 && bit)) {
-                ++aux;
-                cb = o_rep + 12 * aux + st - 1;
-              } else {
-                uint32_t d;
-                if (aux == 2) {
-                  d = r1;
-                } else {
-                  d = bit ? r3 : r2;
-                  r3 = bit ? r2 : r3;
-                  r2 = r1;
-                }
-                r1 = r0;
-                r0 = d;
-                st = st < 7 ? 8u : 11u;
-                lrep = 1;
-                ph = PH_LCH;
-              }
-              break;
-            case PH_REP0L:
-              if (!bit) {  // short rep: a one-byte copy (LzmaDec.c:213-228)
-                st = st < 7 ? 9u : 11u;
-                len = 1;
-                ph = PH_COPY;
-              } else {
-                st = st < 7 ? 8u : 11u;
-                lrep = 1;
-                ph = PH_LCH;
-              }
-              break;
-            case PH_LCH:
-              if (!bit) {
-                cb = lcoff + 2 + ((total & pb_mask) << 3);
-                left = 3;
-                aux = 0u - 8u;
-                ph = PH_LTREE;
-              } else {
-                cb = lcoff;
-                ph = PH_LCH2;
-              }
-              break;
-            case PH_LCH2:
-              if (!bit) {
-                cb = lcoff + 2 + (8u << pb) + ((total & pb_mask) << 3);
-                left = 3;
-                aux = 0;
-              } else {
-                cb = o_lenhi + (lrep ? 256u : 0u);
-                cg = G_LENHI;
-                left = 8;
-                aux = 16u - 256u;
-              }
-              ph = PH_LTREE;
-              break;
-            case PH_LTREE:
-              len = node + aux;
-              if (st >= 12) {
-                cb = o_slot + ((len < 4 ? len : 3u) << 6);
-                cg = G_SLOT;
-                left = 6;
-                ph = PH_SLOT;
-              } else {
-                len += 2;  // kMatchMinLen (LzmaDec.c:371)
-                ph = PH_COPY;
-              }
-              break;
-            case PH_SLOT: {
-              const uint32_t slot = node - 64;
-              const uint32_t nb = (slot >> 1) - 1;
-              dist = slot < 4 ? slot : (2u | (slot & 1u));
-              if (slot < 4) {
-                ph = PH_END + 1;
-              } else if (slot < 14) {
-                dist <<= nb;
-                cb = o_spec + dist - slot - 1;
-                cg = G_SPEC;
-                left = nb;
-                aux = nb;
-                ph = PH_SPEC;
-              } else {
-                left = nb - 4;
-                cg = 0;
-                ph = PH_DIRECT;
-              }
-              break;
-            }
-            case PH_SPEC:
-              dist |= lz_bitrev(node - (1u << aux), aux);
-              ph = PH_END + 1;
-              break;
-            case PH_DIRECT:
-              dist = node << 4;
-              cb = o_align;
-              cg = G_ALIGN;
-              left = 4;
-              ph = PH_ALIGN;
-              break;
-            case PH_ALIGN:
-              dist |= lz_bitrev(node - 16u, 4);
-              ph = PH_END + 1;
-              break;
-          }
-          if (ph == PH_LCH) {
-            lcoff = lrep ? o_replen : o_len;
-            cb = lcoff - 1;
-            cg = G_LEN;
-          }
-          left = left ? left : 1u;  // single-bit phases
-          // the direct bits accumulate under (2 | slot & 1) in node, MSB first
-          node = ph == PH_DIRECT ? dist : 1u;
-          if (ph == PH_END + 1) {  // the distance of a match (LzmaDec.c:354-371)
-            if (dist == 0xFFFFFFFFu) {  // end marker
-              len += kLenDone;
-              st -= 12;
-              ph = PH_END;
-            } else {
-              r3 = r2;
-              r2 = r1;
-              r1 = r0;
-              r0 = dist + 1;
-              if (full == 0 ? dist >= total : dist >= full) {
-                err = kErrData;
-                ph = PH_END;
-              } else {
-                st = st < 19 ? 7u : 10u;
-                len += 2;
-                ph = PH_COPY;
-              }
-            }
-          }
-        }
-      }
-    } else if (ph == PH_COPY) {
-      // ---- the LZ copy (LzmaDec.c:373-408)
-      if (limit == pos) {
-        err = kErrData;
-        ph = PH_END;
-      } else {
-        const uint64_t room = limit - pos;
-        const uint32_t n = (room < len) ? uint32_t(room) : len;
-        const uint64_t from = ring_back(pos, r0, cap);
-        total += n;
-        len -= n;
-        prev = lz_copy(dic, pos, from, n, r0, cap);
-        pos += n;
-        mbp = dic[ring_back(pos, r0, cap)];
-        const bool more = pos < limit && rd.used() < in_limit;
-        ph = more ? PH_ISMATCH : PH_END;
-        cb = o_match + (st << pb) + (total & pb_mask) - 1;
-        cg = G_MATCH;
-        node = 1;
-        left = 1;
-      }
-    }
-  }
-  if (err != kOk) return err;
-  if (range < kTop) {  // NORMALIZE after the loop (LzmaDec.c:411)
-    range <<= 8;
-    code = (code << 8) | rd.next();
-  }
-  s.range = range;
-  s.code = code;
-  s.pending = len;
-  s.pos = pos;
-  s.total = total;
-  s.rep0 = r0;
-  s.rep1 = r1;
-  s.rep2 = r2;
-  s.rep3 = r3;
-  s.st = st;
-  return kOk;
-}
-
 // Decode symbols until pos reaches `limit` or the reader index reaches
 // `in_limit` (checked after each whole symbol; the first is always decoded).
 // State is written back only on success, as LzmaDec_DecodeReal does.
 template <uint32_t M, class Lo, class Rd>
 __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
                                       uint32_t in_limit) {
-  if constexpr ((M & kStepBit) != 0u) return lz_run_step<M>(s, limit, rd, in_limit);
   const Tab<M, Lo> T(s);
   const uint32_t pb = s.pb;
   uint32_t st = s.st;
@@ -1934,8 +1658,9 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
                                                           r0, cap, mb_pf, &s.win);
             pos++;
           } else {
-            prev = dic[ring_back(pos, r0, cap)];
-            lz_put(dic + pos++, prev);
+            prev = lz_back<M>(dic, pos, r0, cap, &s.win);
+            lz_emit<M>(dic, pos, prev, &s.win);
+            pos++;
             if constexpr (mb_pf_on<M>()) mb_pf = dic[ring_back(pos, r0, cap)];
           }
           total++;
@@ -2143,7 +1868,10 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
         prev = lz_copy_coop<win_on<M>(), def_on<M>()>(dic, pos, from, n, r0, cap, mb_pf, &s.win);
         pos += n;
       } else {
-        prev = lz_copy(dic, pos, from, n, r0, cap);
+        if constexpr (lwin_on<M>())
+          prev = lz_copy_lw<ldef_on<M>()>(dic, pos, n, r0, s.win);
+        else
+          prev = lz_copy(dic, pos, from, n, r0, cap);
         pos += n;
         if constexpr (mb_pf_on<M>()) mb_pf = dic[ring_back(pos, r0, cap)];
       }
@@ -2152,6 +1880,7 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
   } while (pos < limit && rd.used() < in_limit);
 
   if constexpr (def_on<M>()) win_flush(s.win, dic, pos);  // the dictionary complete again
+  if constexpr (ldef_on<M>()) win_store_tail(s.win, dic, pos);
   rc.norm();
   s.range = rc.range;
   s.code = rc.code;
@@ -2177,7 +1906,10 @@ __device__ __forceinline__ void lz_flush_pending(LzStateT<Lo>& s, uint64_t limit
   while (n-- != 0) {
     const uint8_t b = s.dic[ring_back(s.pos, s.rep0, s.cap)];
     s.dic[s.pos] = b;
-    if constexpr (win_on<M>()) win_put(s.win, b);
+    if constexpr (lwin_on<M>())
+      win_put_at(s.win, s.pos, b);
+    else if constexpr (win_on<M>())
+      win_put(s.win, b);
     s.pos++;
   }
 }

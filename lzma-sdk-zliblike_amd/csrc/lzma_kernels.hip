@@ -16,6 +16,8 @@
 // The per-lane work is in lzma_lane.h.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cstdlib>
 #include <mutex>
 #include <set>
 #include <utility>
@@ -43,20 +45,6 @@ static int allow_full_lds(const void* kfn) {
 
 int lzgpu_allow_full_lds(const void* kfn) { return allow_full_lds(kfn); }
 
-// A second stream per device, for the scalar-register half of a split
-// latency launch (launch_lds); created once, never destroyed.
-static hipStream_t aux_stream() {
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kLzgpuMaxDevices) return nullptr;
-  static std::mutex mu;
-  static hipStream_t streams[kLzgpuMaxDevices] = {};
-  std::lock_guard<std::mutex> g(mu);
-  if (!streams[dev] && hipStreamCreateWithFlags(&streams[dev], hipStreamNonBlocking) != hipSuccess)
-    streams[dev] = nullptr;
-  return streams[dev];
-}
-
-
 __global__ void __launch_bounds__(64) lzgpu_decode_batch_kernel(
     const LzmaGpuStreamDesc* __restrict__ descs, const uint32_t* __restrict__ order, uint32_t n,
     const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, uint16_t* __restrict__ ws,
@@ -75,9 +63,8 @@ __global__ void __launch_bounds__(64) lzgpu_decode_batch_kernel(
 // that finishes its stream takes the next one from `queue` (a counter the
 // launcher zeroes), so no lane idles behind a slower neighbour in its wave
 // and the chip drains without a partial last round of workgroups.  Every
-// lane exits once the queue passes n.  Lane l starts on stream base + l and
-// then takes start + (queue ticket): start = the lanes of every launch that
-// shares the queue (a split class, lzgpu_decode_one_kernel).
+// lane exits once the queue passes n.  Lane l starts on stream l and then
+// takes start + (queue ticket): start = the lanes of the launch.
 // K2: the build carries the LZMA2 chunk walker (classes with LZMA2 items); the
 // LZMA-only build needs fewer registers (169 vs 202 VGPRs at W = 2, 21 vs 153
 // spilled at W = 4), so classes without LZMA2 items launch it.
@@ -86,13 +73,16 @@ __global__ void __launch_bounds__(64) lzgpu_decode_batch_kernel(
 // lane group g (32 lanes of one workgroup) owns rows of kIlv cells, `slot_cells`
 // rows, and lane l its column l; the lane keeps its column for every stream
 // it takes from the queue.
+// Windowed placements (M & kWinBit: the one-lane latency kernel, round 5):
+// the workgroup's single lane keeps its LDS history window of `win_bytes`
+// after its table slice (16-byte aligned).
 
 template <int W, uint32_t M, bool K2>
 __global__ void __launch_bounds__(64, W) lzgpu_decode_lds_kernel(
     const LzmaGpuStreamDesc* __restrict__ descs, const uint32_t* __restrict__ order, uint32_t n,
     const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, uint16_t* __restrict__ ws,
     LzmaGpuResult* __restrict__ results, uint32_t stride, uint32_t* __restrict__ queue,
-    uint64_t slot_off, uint32_t slot_cells, uint32_t base, uint32_t start) {
+    uint64_t slot_off, uint32_t slot_cells, uint32_t start, uint32_t win_bytes) {
   extern __shared__ uint32_t lz_smem[];
   // the lane's LDS slice; interleaved (lds_ilv): its column of its 32-lane
   // group's rows
@@ -101,7 +91,7 @@ __global__ void __launch_bounds__(64, W) lzgpu_decode_lds_kernel(
     lo += (threadIdx.x / kIlv) * (kIlv * stride) + (threadIdx.x % kIlv);
   else
     lo += threadIdx.x * stride;
-  uint32_t idx = base + blockIdx.x * blockDim.x + threadIdx.x;
+  uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x;
   gu16* gcol = nullptr;
   if constexpr ((M & kIlvBit) != 0u) {
     const uint32_t grp = blockIdx.x * ((blockDim.x + kIlv - 1) / kIlv) + threadIdx.x / kIlv;
@@ -110,55 +100,24 @@ __global__ void __launch_bounds__(64, W) lzgpu_decode_lds_kernel(
   }
   (void)slot_off;
   (void)slot_cells;
+  lds_u8* win = nullptr;
+  if constexpr (win_on<M>())
+    win = (lds_u8*)((uint8_t*)lz_smem) + ((size_t(stride) * 2 + 15) & ~size_t(15));
+  (void)win_bytes;
   while (idx < n) {
     const uint32_t id = order ? order[idx] : idx;
     const LzmaGpuStreamDesc d = descs[id];
-    results[id] = lane_decode_lds<M, K2>(d, src, dst, ws, lo, stride, gcol);
-    idx = start + atomicAdd(queue, 1u);
-  }
-}
-
-// Scalar-register waves (latency placement, one stream per one-lane wave,
-// round 4).  A one-lane wave of lzgpu_decode_lds_kernel spends a full
-// vector-ALU issue on every instruction of its single stream, and at 16 such
-// waves per CU the vector ALUs are the limit (config 2: VALU busy 78 % of the
-// kernel, the scalar ALU 33 %: profiles/r04_base/pmc_cfg2.json).  Built for a
-// workgroup of exactly one work-item, the same decoder compiles to scalar code
-// -- the compiler knows every value of a one-lane workgroup is wave-uniform,
-// so the range coder, probability updates, table indices and branches live in
-// scalar registers and run on the CU's scalar ALU (loaded values arrive by
-// readfirstlane; only the memory operations' addresses and store data touch
-// the vector unit).  The scalar ALU is one per CU against one vector ALU per
-// SIMD, so a launch can split a class between the two builds (`base` = this
-// launch's first stream index; both draw the rest from the same queue, whose
-// starting offset `start` is the two grids together).  Measured (round 4,
-// profiles/r04_scalar/): slower at every share -- config 2 6.11 GB/s on the
-// vector build, 4.40 with every wave scalar, 5.71 with half; the scalar build
-// needs more scalar instructions per decision than the CU's one scalar ALU
-// can issue for 16 waves -- so the planner's default share is zero and the
-// build stays selectable (LzmaGpuPlanOptions.scalar_waves, LZGPU_SCALAR).
-template <int W, uint32_t M, bool K2>
-__global__ void __launch_bounds__(1, W) lzgpu_decode_one_kernel(
-    const LzmaGpuStreamDesc* __restrict__ descs, const uint32_t* __restrict__ order, uint32_t n,
-    const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, uint16_t* __restrict__ ws,
-    LzmaGpuResult* __restrict__ results, uint32_t stride, uint32_t* __restrict__ queue,
-    uint32_t base, uint32_t start) {
-  extern __shared__ uint32_t lz_smem[];
-  lds_u16* lo = (lds_u16*)((uint16_t*)lz_smem);
-  uint32_t idx = base + blockIdx.x;
-  while (idx < n) {
-    const uint32_t id = order ? order[idx] : idx;
-    const LzmaGpuStreamDesc d = descs[id];
-    results[id] = lane_decode_lds<M, K2>(d, src, dst, ws, lo, stride, nullptr);
+    results[id] = lane_decode_lds<M, K2>(d, src, dst, ws, lo, stride, gcol, win, win_bytes);
     idx = start + atomicAdd(queue, 1u);
   }
 }
 
 // Wave-cooperative decode (latency regime): one stream per workgroup of one
 // 32-lane wave.  Every lane runs the same decoder on the same state, so control
-// flow and memory traffic are those of one lane -- except the literal tree,
-// whose levels are decided several at a time by speculating over the lanes
-// (spec_stage in lzma_device.h).  Lane 0 takes the next stream from the queue.
+// flow and memory traffic are those of one lane -- except match copies (byte j
+// by lane j mod 32, lz_copy_coop), the direct bits of a distance (several per
+// step, direct_coop) and table initialisation.  Lane 0 takes the next stream
+// from the queue.
 // Under kWinBit the workgroup's LDS holds, after the table (`stride` cells,
 // 16-byte aligned), the LDS history window of `win_bytes` (lzma_device.h):
 // match copies and matched bytes within its reach are LDS reads.
@@ -202,8 +161,8 @@ __global__ void __launch_bounds__(64) lzgpu_session_kernel(LzgpuSession* __restr
 // device-resident decoder (the drop-in LzmaDec_DecodeToDic / DecodeToBuf of a
 // host CLzmaDec, and small session batches): the wave-cooperative decoder with
 // the session's whole table staged in LDS for the call -- loaded from
-// q.probs, decoded on (literal trees by lane speculation, every other table
-// access an LDS round trip instead of a global one), written back.  Placement
+// q.probs, decoded on (every table access an LDS round trip instead of a
+// global one), written back.  Placement
 // 0x7FF keeps the all-global layout's offsets, so the copy is a straight one.
 // Dynamic LDS: the widest table of the batch's sessions (the launcher checks).
 // WIN: the LDS history window (win_bytes, after the table) is preloaded per
@@ -298,12 +257,30 @@ extern "C" int lzgpu_launch_decode_batch(const LzmaGpuStreamDesc* d_descs, const
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+// LDS history window of a one-lane latency launch (round 5): the largest
+// power of two, 1 KiB to 64 KiB, that fits beside the lane's table slice in the
+// workgroup's share of the CU (160 KiB / groups_per_cu); 0 = none fits, or
+// LZGPU_LANE_WIN=0 (A/B: the round-4 kernel).
+static uint32_t lane_window_bytes(uint32_t lanes, uint32_t stride, uint32_t groups_per_cu) {
+  static const bool off = [] {
+    const char* e = getenv("LZGPU_LANE_WIN");
+    return e && e[0] == '0';
+  }();
+  if (off || lanes != 1 || groups_per_cu == 0) return 0;
+  const size_t share = (size_t(160 * 1024) / groups_per_cu) & ~size_t(511);
+  const size_t tb = (size_t(stride) * 2 + 15) & ~size_t(15);
+  if (share < tb + 1024) return 0;
+  uint32_t w = 1u << 16;
+  while (w > share - tb) w >>= 1;
+  return w;
+}
+
 template <int W, uint32_t M, bool K2>
 static int launch_lds(const LzmaGpuStreamDesc* d_descs, const uint32_t* d_order, uint32_t n,
                       const uint8_t* d_src, uint8_t* d_dst, uint16_t* d_ws,
                       LzmaGpuResult* d_results, uint32_t lanes, uint32_t stride,
                       uint32_t groups_per_cu, uint32_t max_groups, uint32_t* d_queue,
-                      const LzgpuSlots& sl, hipStream_t stream, uint32_t uni_q = 0) {
+                      const LzgpuSlots& sl, hipStream_t stream) {
   if (allow_full_lds(reinterpret_cast<const void*>(lzgpu_decode_lds_kernel<W, M, K2>)) != 0)
     return -1;
   if (hipMemsetAsync(d_queue, 0, sizeof(uint32_t), stream) != hipSuccess) return -1;
@@ -327,51 +304,15 @@ static int launch_lds(const LzmaGpuStreamDesc* d_descs, const uint32_t* d_order,
     }
   }
   const uint32_t lanes_total = grid * lanes;
-  if constexpr (M == LZGPU_LDS_MASK_LAT) {
-    if (lanes == 1 && uni_q != 0) {
-      // uni_q of every four one-lane waves on the scalar-register build: the
-      // first grid * uni_q / 4 streams on a second stream of the device, the
-      // rest on the caller's, one queue (both launches resident together)
-      auto k1 = lzgpu_decode_one_kernel<W, M, K2>;
-      if (allow_full_lds(reinterpret_cast<const void*>(k1)) != 0) return -1;
-      const uint32_t g1 = uni_q >= 4 ? grid : uint32_t((uint64_t(grid) * uni_q) / 4);
-      if (g1 == grid) {
-        hipLaunchKernelGGL(k1, dim3(grid), dim3(1), lds, stream, d_descs, d_order, n, d_src,
-                           d_dst, d_ws, d_results, stride, d_queue, 0u, lanes_total);
-        return hipGetLastError() == hipSuccess ? 0 : -1;
-      }
-      if (g1 != 0) {
-        hipStream_t aux = aux_stream();
-        hipEvent_t e0 = nullptr, e1 = nullptr;
-        if (!aux || hipEventCreateWithFlags(&e0, hipEventDisableTiming) != hipSuccess) return -1;
-        if (hipEventCreateWithFlags(&e1, hipEventDisableTiming) != hipSuccess) {
-          hipEventDestroy(e0);
-          return -1;
-        }
-        bool ok = hipEventRecord(e0, stream) == hipSuccess &&
-                  hipStreamWaitEvent(aux, e0, 0) == hipSuccess;
-        if (ok) {
-          hipLaunchKernelGGL(k1, dim3(g1), dim3(1), lds, aux, d_descs, d_order, n, d_src, d_dst,
-                             d_ws, d_results, stride, d_queue, 0u, lanes_total);
-          ok = hipGetLastError() == hipSuccess && hipEventRecord(e1, aux) == hipSuccess;
-        }
-        if (ok) {
-          auto kv = lzgpu_decode_lds_kernel<W, M, K2>;
-          hipLaunchKernelGGL(kv, dim3(grid - g1), dim3(1), lds,
-                             stream, d_descs, d_order, n, d_src, d_dst, d_ws, d_results, stride,
-                             d_queue, sl.off, sl.cells, g1, lanes_total);
-          ok = hipGetLastError() == hipSuccess && hipStreamWaitEvent(stream, e1, 0) == hipSuccess;
-        }
-        hipEventDestroy(e0);
-        hipEventDestroy(e1);
-        return ok ? 0 : -1;
-      }
-    }
+  uint32_t win = 0;
+  if constexpr (win_on<M>()) {
+    win = lane_window_bytes(lanes, stride, groups_per_cu);
+    if (!win) return -1;  // the caller checked that one fits
+    lds = std::max(lds, ((size_t(stride) * 2 + 15) & ~size_t(15)) + win);
   }
-  (void)uni_q;
   auto kfn = lzgpu_decode_lds_kernel<W, M, K2>;
   hipLaunchKernelGGL(kfn, dim3(grid), dim3(lanes), lds, stream, d_descs, d_order, n, d_src, d_dst,
-                     d_ws, d_results, stride, d_queue, sl.off, sl.cells, 0u, lanes_total);
+                     d_ws, d_results, stride, d_queue, sl.off, sl.cells, lanes_total, win);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -405,16 +346,15 @@ static int launch_lds_w(const LzmaGpuStreamDesc* d_descs, const uint32_t* d_orde
                         const uint8_t* d_src, uint8_t* d_dst, uint16_t* d_ws,
                         LzmaGpuResult* d_results, uint32_t lanes, uint32_t stride,
                         uint32_t waves_per_simd, uint32_t groups_per_cu, uint32_t max_groups,
-                        uint32_t* d_queue, const LzgpuSlots& sl, hipStream_t stream,
-                        uint32_t uni_q = 0) {
+                        uint32_t* d_queue, const LzgpuSlots& sl, hipStream_t stream) {
   if (waves_per_simd <= 1)
     return launch_lds<1, M, K2>(d_descs, d_order, n, d_src, d_dst, d_ws, d_results, lanes, stride,
-                                groups_per_cu, max_groups, d_queue, sl, stream, uni_q);
+                                groups_per_cu, max_groups, d_queue, sl, stream);
   if (waves_per_simd == 2)
     return launch_lds<2, M, K2>(d_descs, d_order, n, d_src, d_dst, d_ws, d_results, lanes, stride,
-                                groups_per_cu, max_groups, d_queue, sl, stream, uni_q);
+                                groups_per_cu, max_groups, d_queue, sl, stream);
   return launch_lds<4, M, K2>(d_descs, d_order, n, d_src, d_dst, d_ws, d_results, lanes, stride,
-                              groups_per_cu, max_groups, d_queue, sl, stream, uni_q);
+                              groups_per_cu, max_groups, d_queue, sl, stream);
 }
 
 template <bool K2>
@@ -433,16 +373,6 @@ static int launch_class(const LzmaGpuStreamDesc* d_descs, const uint32_t* d_orde
                                                       d_results, lanes, stride, waves_per_simd,
                                                       groups_per_cu, max_groups, d_queue, sl,
                                                       stream);
-  // the decision-level loop (lz_run_step) on the throughput placement
-  if (lds_mask == (LZGPU_LDS_MASK | kIlvBit | kStepBit))
-    return launch_lds_w<LZGPU_LDS_MASK | kIlvBit | kStepBit, K2>(
-        d_descs, d_order, n, d_src, d_dst, d_ws, d_results, lanes, stride, waves_per_simd,
-        groups_per_cu, max_groups, d_queue, sl, stream);
-  if (lds_mask == (LZGPU_LDS_MASK | kStepBit))
-    return launch_lds_w<LZGPU_LDS_MASK | kStepBit, K2>(d_descs, d_order, n, d_src, d_dst, d_ws,
-                                                       d_results, lanes, stride, waves_per_simd,
-                                                       groups_per_cu, max_groups, d_queue, sl,
-                                                       stream);
   if (lds_mask == (LZGPU_LDS_MASK_LAT | kCoopBit)) {
     // one wave per workgroup: register budget by workgroups per SIMD
     constexpr uint32_t MC = LZGPU_LDS_MASK_LAT | kCoopBit;
@@ -465,11 +395,16 @@ static int launch_class(const LzmaGpuStreamDesc* d_descs, const uint32_t* d_orde
                                                 stride, groups_per_cu, max_groups, d_queue,
                                                 stream);
   }
-  if (lds_mask == LZGPU_LDS_MASK_LAT)
-    return launch_lds_w<LZGPU_LDS_MASK_LAT, K2>(
-        d_descs, d_order, n, d_src, d_dst, d_ws, d_results, lanes, stride, waves_per_simd,
-        groups_per_cu, max_groups, d_queue, sl, stream,
-        (class_flags >> LZMA_GPU_CLASS_SCALAR_SHIFT) & 7u);
+  if (lds_mask == LZGPU_LDS_MASK_LAT) {
+    // one stream per wave: with the LDS history window where it fits
+    if (lane_window_bytes(lanes, stride, groups_per_cu))
+      return launch_lds_w<LZGPU_LDS_MASK_LAT | kWinBit, K2>(
+          d_descs, d_order, n, d_src, d_dst, d_ws, d_results, lanes, stride, waves_per_simd,
+          groups_per_cu, max_groups, d_queue, sl, stream);
+    return launch_lds_w<LZGPU_LDS_MASK_LAT, K2>(d_descs, d_order, n, d_src, d_dst, d_ws,
+                                                d_results, lanes, stride, waves_per_simd,
+                                                groups_per_cu, max_groups, d_queue, sl, stream);
+  }
   return -1;  // no kernel built for this placement
 }
 

@@ -107,7 +107,7 @@ __device__ __forceinline__ LzmaGpuResult lane_decode_lds(const LzmaGpuStreamDesc
                                                          uint32_t lo_cap, gu16* gcol = nullptr,
                                                          lds_u8* win = nullptr,
                                                          uint32_t win_bytes = 0) {
-  const LzWin w0 = {win, win_bytes - 1, 0, 0};
+  const LzWin w0 = win_make(win, win_bytes, d.dst_cap);
   // global sections: the stream's own workspace slice, or under kIlvBit the
   // lane's column of its group's interleaved slot rows
   auto gtab = [&]() -> gu16* {
@@ -127,9 +127,7 @@ __device__ __forceinline__ LzmaGpuResult lane_decode_lds(const LzmaGpuStreamDesc
       return r;
     } else {
     // chunks may switch lc/lp/pb (lc + lp <= 4): the slice holds the widest layout
-    // (+1: the decision-level loop's spare cell, lz_run_step)
-    if (d.probs_off == LZMA_GPU_NO_WORKSPACE ||
-        lzma2_lds_cells(M) + ((M & kStepBit) ? 1u : 0u) > lo_cap) {
+    if (d.probs_off == LZMA_GPU_NO_WORKSPACE || lzma2_lds_cells(M) > lo_cap) {
       r.res = (d.props[0] > 40) ? kErrUnsupported : kErrMem;
       return r;
     }
@@ -166,7 +164,7 @@ __device__ __forceinline__ LzmaGpuResult lane_decode_lds(const LzmaGpuStreamDesc
   r.res = lz_props_parse(d.props, d.props_size, s.lc, s.lp, s.pb, s.dict_size);
   if (r.res != kOk) return r;
   if (d.probs_off == LZMA_GPU_NO_WORKSPACE ||
-      make_layout(s.lc, s.lp, s.pb, M).lds_cells + ((M & kStepBit) ? 1u : 0u) > lo_cap) {
+      make_layout(s.lc, s.lp, s.pb, M).lds_cells > lo_cap) {
     r.res = kErrMem;
     return r;
   }
@@ -280,7 +278,7 @@ template <uint32_t M = 0u, class Lo = gu16*>
 __device__ __forceinline__ void lane_session(LzgpuSession& q, Lo lo = Lo(), lds_u8* win = nullptr,
                                              uint32_t win_bytes = 0) {
   int status = kStNone;
-  LzWin w = {win, win_bytes - 1, 0, 0};
+  LzWin w = win_make(win, win_bytes, q.dic_buf_size);
   if constexpr (win_on<M>()) {
     uint64_t hv = q.check_dic_size != 0 ? q.dic_buf_size : q.processed_pos;
     if (hv > q.dic_buf_size) hv = q.dic_buf_size;

@@ -262,7 +262,7 @@ __global__ void __launch_bounds__(64, W) lzgpu_sliced_lane_kernel(SlicedRound a)
 }
 
 // Class 0, one stream per 32-lane wave, every lane holding its state: the
-// cooperative decoder (literal trees by lane speculation) on the whole table
+// cooperative decoder on the whole table
 // staged in LDS.
 constexpr uint32_t kSlicedCoopMask = kSlicedAll | kCoopBit;
 template <int W>

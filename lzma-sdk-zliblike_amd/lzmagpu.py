@@ -95,7 +95,7 @@ class PlanOptions(ctypes.Structure):
                 ("lanes_per_group", ctypes.c_uint32), ("groups_per_cu", ctypes.c_uint32),
                 ("waves_per_simd", ctypes.c_uint32), ("persistent", ctypes.c_uint32),
                 ("coop", ctypes.c_uint32), ("one_class", ctypes.c_uint32),
-                ("flags", ctypes.c_uint32), ("scalar_waves", ctypes.c_uint32)]
+                ("flags", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
 
 
 KERNELS = {"auto": 0, "throughput": 1, "latency": 2, "coop": 3, "global": 4}

@@ -10,11 +10,17 @@
  * so later LZMA chunks that match into stored bytes read what the host wrote:
  * the device mirror of the dictionary must notice (dropin_capi.hip).
  *
- *   lzma2_walker PROP STREAM_FILE OUT_SIZE IN_CHUNK DIC_CHUNK
+ *   lzma2_walker PROP STREAM_FILE OUT_SIZE IN_CHUNK DIC_CHUNK [OUT_CHUNK]
  *
  * 7zDec.c:181-202 (SzDecodeLzma2) shape: dic = the whole output buffer,
  * dicLimit advanced DIC_CHUNK bytes at a time (0: the whole output), input fed
  * IN_CHUNK bytes at a time.  Prints: res status dicPos inPos crc32 calls.
+ * OUT_CHUNK > 0 (round 5): the XzDec shape instead -- the
+ * decoder's own ring (Lzma2Dec_Allocate: dicBufSize = the dictionary size),
+ * Lzma2Dec_DecodeToBuf into the output OUT_CHUNK bytes at a time; stored
+ * chunks reach the ring in pieces on either side of its end (the walker wraps
+ * dicPos to 0 between the GPU decoder's calls).  Prints the output position
+ * in place of dicPos.
  */
 #include <stdio.h>
 #include <stdlib.h>
@@ -58,10 +64,12 @@ int main(int argc, char **argv) {
   CLzma2Dec dec;
   SRes r;
   ELzmaStatus st = LZMA_STATUS_NOT_SPECIFIED;
-  if (argc != 6) {
-    fprintf(stderr, "usage: %s PROP STREAM OUT_SIZE IN_CHUNK DIC_CHUNK\n", argv[0]);
+  size_t out_chunk = 0, out_pos = 0;
+  if (argc != 6 && argc != 7) {
+    fprintf(stderr, "usage: %s PROP STREAM OUT_SIZE IN_CHUNK DIC_CHUNK [OUT_CHUNK]\n", argv[0]);
     return 2;
   }
+  if (argc == 7) out_chunk = (size_t)strtoull(argv[6], NULL, 10);
   prop = (unsigned)strtoul(argv[1], NULL, 10);
   src = read_file(argv[2], &ns);
   out_size = (size_t)strtoull(argv[3], NULL, 10);
@@ -71,6 +79,32 @@ int main(int argc, char **argv) {
   out = (unsigned char *)malloc(out_size ? out_size : 1);
   memset(out, 0, out_size);
   Lzma2Dec_Construct(&dec);
+  if (out_chunk) {
+    r = Lzma2Dec_Allocate(&dec, (Byte)prop, &g_Alloc);
+    if (r == SZ_OK) {
+      Lzma2Dec_Init(&dec);
+      for (;;) {
+        SizeT sl = ns - in_pos, dl = out_size - out_pos;
+        ELzmaFinishMode fin = LZMA_FINISH_END;
+        if (sl > in_chunk) sl = in_chunk;
+        if (dl > out_chunk) {
+          dl = out_chunk;
+          fin = LZMA_FINISH_ANY;
+        }
+        r = Lzma2Dec_DecodeToBuf(&dec, out + out_pos, &dl, src + in_pos, &sl, fin, &st);
+        calls++;
+        in_pos += sl;
+        out_pos += dl;
+        if (r != SZ_OK || st == LZMA_STATUS_FINISHED_WITH_MARK || (sl == 0 && dl == 0)) break;
+      }
+      Lzma2Dec_Free(&dec, &g_Alloc);
+    }
+    printf("%d %d %zu %zu %08x %zu\n", (int)r, (int)st, out_pos, in_pos, crc32_of(out, out_pos),
+           calls);
+    free(out);
+    free(src);
+    return 0;
+  }
   r = Lzma2Dec_AllocateProbs(&dec, (Byte)prop, &g_Alloc);
   if (r == SZ_OK) {
     dec.decoder.dic = out;

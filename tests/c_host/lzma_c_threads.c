@@ -33,6 +33,8 @@
  * in the reference build */
 extern void LzmaGpu_CoalesceStats(uint64_t *batches, uint64_t *calls, uint64_t *max_batch,
                                   int reset) __attribute__((weak));
+extern void LzmaGpu_CoalesceTimes(uint64_t *ns, uint64_t *batches, int reset)
+    __attribute__((weak));
 
 static void *SzAlloc(void *p, size_t size) { (void)p; return malloc(size ? size : 1); }
 static void SzFree(void *p, void *address) { (void)p; free(address); }
@@ -173,15 +175,29 @@ int main(int argc, char **argv) {
     crc ^= w[t].crc;
   }
   {
-    uint64_t nb = 0, nc = 0, mx = 0;
+    uint64_t nb = 0, nc = 0, mx = 0, tns[8] = {0}, tb = 0;
+    char ph[256] = "null";
     if (LzmaGpu_CoalesceStats) LzmaGpu_CoalesceStats(&nb, &nc, &mx, 0);
+    if (LzmaGpu_CoalesceTimes) {
+      /* host microseconds per one-call batch by phase (plan, stage, upload,
+       * launch, wait, download, batch, call) */
+      int k;
+      size_t o = 0;
+      LzmaGpu_CoalesceTimes(tns, &tb, 0);
+      o += (size_t)snprintf(ph + o, sizeof ph - o, "[");
+      for (k = 0; k < 8; ++k)
+        o += (size_t)snprintf(ph + o, sizeof ph - o, "%s%.1f", k ? ", " : "",
+                              tb ? (double)tns[k] / 1e3 / (double)(k == 7 && nc ? nc : tb) : 0.0);
+      snprintf(ph + o, sizeof ph - o, "]");
+    }
     fprintf(stderr,
             "{\"mode\": \"%s\", \"threads\": %d, \"streams\": %zu, \"repeat\": %d, \"bytes\": %llu, "
             "\"seconds\": %.6f, \"MBps\": %.2f, \"fails\": %llu, \"crc_xor\": \"%08x\", "
+            "\"phase_us\": %s, "
             "\"batches\": %llu, \"batched_calls\": %llu, \"max_batch\": %llu}\n",
             (argc == 8 && strcmp(argv[7], "buf") == 0) ? "buf" : "one", T, n, repeat,
             (unsigned long long)bytes, sec, sec > 0 ? (double)bytes / sec / 1e6 : 0.0,
-            (unsigned long long)fails, crc, (unsigned long long)nb, (unsigned long long)nc,
+            (unsigned long long)fails, crc, ph, (unsigned long long)nb, (unsigned long long)nc,
             (unsigned long long)mx);
   }
   return 0;

@@ -34,7 +34,7 @@ void emu_decode_batch(const LzmaGpuStreamDesc* descs, size_t n, const uint8_t* s
 void emu_decode_batch_lds(const LzmaGpuStreamDesc* descs, size_t n, const uint8_t* src,
                           uint8_t* dst, uint16_t* ws, LzmaGpuResult* results, uint32_t stride) {
   uint16_t* slab = (uint16_t*)malloc(size_t(stride) * 2 + 16);
-#if defined(EMU_ILV) || defined(EMU_STEP_ILV)
+#if defined(EMU_ILV)
   // lane-interleaved global sections: 32 lane columns of the widest LZMA2
   // layout's global rows; stream i runs in column i % 32, its neighbours'
   // cells left as garbage (columns are reused stream after stream)
@@ -46,15 +46,7 @@ void emu_decode_batch_lds(const LzmaGpuStreamDesc* descs, size_t n, const uint8_
 #endif
   for (size_t i = 0; i < n; ++i) {
     memset(slab, 0xA5, size_t(stride) * 2);  // LDS is not zeroed between workgroups
-#if defined(EMU_STEP_ILV)
-    // the decision-level loop (lz_run_step) on the throughput placement with
-    // lane-interleaved global sections: the round-4 throughput instantiation
-    results[i] = lane_decode_lds<LZGPU_LDS_MASK | kIlvBit | kStepBit>(
-        descs[i], src, dst, ws, slab, stride, slots.data() + (i % kIlv) * kIlvLaneCells);
-#elif defined(EMU_STEP)
-    // the decision-level loop on the placement LZGPU_LDS_MASK (per-stream slices)
-    results[i] = lane_decode_lds<LZGPU_LDS_MASK | kStepBit>(descs[i], src, dst, ws, slab, stride);
-#elif defined(EMU_ILV)
+#if defined(EMU_ILV)
     results[i] = lane_decode_lds<LZGPU_LDS_MASK | kIlvBit>(descs[i], src, dst, ws, slab, stride,
                                                           slots.data() + (i % kIlv) * kIlvLaneCells);
 #elif defined(EMU_COOP_ALL_WIN)
@@ -66,14 +58,23 @@ void emu_decode_batch_lds(const LzmaGpuStreamDesc* descs, size_t n, const uint8_
       results[i] = lane_decode_lds<LZGPU_LDS_MASK_ALL | kCoopBit | kWinBit>(
           descs[i], src, dst, ws, slab, stride, nullptr, win.data(), EMU_WIN_BYTES);
     }
+#elif defined(EMU_LAT_WIN)
+    // the one-lane latency kernel with its LDS history window (round 5;
+    // deferred output unless -DLZGPU_LANE_DEFER=0)
+    {
+      static std::vector<uint8_t> win(EMU_WIN_BYTES);
+      memset(win.data(), 0x5C, win.size());  // stale LDS contents
+      results[i] = lane_decode_lds<LZGPU_LDS_MASK_LAT | kWinBit>(descs[i], src, dst, ws, slab,
+                                                                 stride, nullptr, win.data(),
+                                                                 EMU_WIN_BYTES);
+    }
 #elif defined(EMU_COOP_ALL)
     // the wave-cooperative kernel with every section in LDS (its default
     // placement where the whole table fits)
     results[i] = lane_decode_lds<LZGPU_LDS_MASK_ALL | kCoopBit>(descs[i], src, dst, ws, slab,
                                                                 stride);
 #elif defined(EMU_COOP)
-    // the wave-cooperative kernel's instantiation (speculative tree stages run
-    // their paths one after another here)
+    // the wave-cooperative kernel's instantiation on the latency placement
     results[i] = lane_decode_lds<LZGPU_LDS_MASK_LAT | kCoopBit>(descs[i], src, dst, ws, slab,
                                                                 stride);
 #elif defined(EMU_LAT_MASK)

@@ -216,25 +216,3 @@ def test_plan_options_force_each_instantiation():
     order = (ctypes.c_uint32 * len(items))()
     assert L.lib.LzmaGpu_PlanBatchOpt(descs, len(items), order, ctypes.byref(L.Plan()),
                                       ctypes.byref(bad)) == L.SZ_ERROR_PARAM
-
-
-def test_plan_scalar_waves_flag():
-    """One-lane latency classes carry the share of their waves that run the
-    scalar-register build (LZMA_GPU_CLASS_SCALAR_SHIFT, 0-4 of every four):
-    LzmaGpuPlanOptions.scalar_waves = 1 + k forces k, 0 takes the default;
-    other classes carry none."""
-    import lzmagpu as L
-    items = [dict(src_off=0, src_len=100, dst_off=65536 * i, dst_cap=65536, props=b"\x5d\x00\x00\x01\x00")
-             for i in range(256)]
-    descs = L.make_descs(items)
-    shares = {}
-    for sw in (0, 1, 2, 3, 4, 5):
-        p, _ = L.plan_ex(descs, L.plan_options("latency", cus=4, scalar_waves=sw))
-        cls = [p.classes[c] for c in range(p.n_classes)]
-        assert cls and all(c.lds_mask == 0x1BF and c.lanes_per_group == 1 for c in cls)
-        shares[sw] = {(c.flags >> 4) & 7 for c in cls}
-    assert [shares[sw] for sw in (1, 2, 3, 4, 5)] == [{0}, {1}, {2}, {3}, {4}]
-    assert shares[0] in ({0}, {1}, {2}, {3}, {4})  # the planner's default
-    for k in ("throughput", "coop"):
-        p, _ = L.plan_ex(descs, L.plan_options(k, cus=4, scalar_waves=5))
-        assert all((p.classes[c].flags >> 4) & 7 == 0 for c in range(p.n_classes))

@@ -245,7 +245,7 @@ def _lzma2_chunks(comp):
     return out
 
 
-def _stored_then_referenced(seed):
+def _stored_then_referenced(seed, dsz=1 << 20):
     """LZMA2 streams (liblzma) whose stored chunks (incompressible random blocks)
     are followed by LZMA chunks copying parts of them: a match into a stored
     chunk reads bytes only the host walker wrote."""
@@ -266,7 +266,6 @@ def _stored_then_referenced(seed):
             parts.append(b[o:o + rng.randrange(20, 300)])
             parts.append(text[:rng.randrange(1, 200)])
     data = b"".join(parts)
-    dsz = 1 << 20
     comp = lzma.compress(data, format=lzma.FORMAT_RAW,
                          filters=[{"id": lzma.FILTER_LZMA2, "dict_size": dsz}])
     return data, comp, _lzma2_prop(dsz)
@@ -308,3 +307,33 @@ def test_gpu_reference_lzma2_walker_over_dropin(tmp_path):
             assert r.returncode == 0, r.stderr
             got = r.stdout.split()
             assert " ".join(got[:5]) == want, (seed, in_chunk, dic_chunk, got, want)
+
+
+@pytest.mark.gpu
+@pytest.mark.skipif(not os.path.exists(WALKER), reason="oracle/_ref/lzma2_walker not built "
+                    "(built where /root/reference exists, travels with the tree)")
+def test_gpu_reference_lzma2_walker_ring_over_dropin(tmp_path):
+    """The reference's Lzma2Dec_DecodeToBuf (XzDec's shape) over the GPU
+    LzmaDec_*: the decoder's own 256 KiB ring under ~1 MB of output, so stored
+    chunks reach the ring in pieces on either side of its end and the device
+    mirror sees host-written spans across the wrap (dropin_capi.hip's two-piece
+    upload).  Output and {res, status, outPos, inPos} equal the
+    plaintext and the oracle's flat decode, for several input / output chunk
+    sizes."""
+    import native
+    orc = native.oracle()
+    for seed in (3, 4):
+        data, comp, prop = _stored_then_referenced(seed, dsz=1 << 18)
+        assert len(data) > 3 * (1 << 18)  # the ring wraps several times
+        res, st, dl, sl, dec = native.lzma2_decode(orc, "orc", comp, prop, len(data), 1)
+        assert (res, st, dl, sl) == (0, 1, len(data), len(comp)) and dec == data
+        want = "0 1 %d %d %08x" % (len(data), len(comp), zlib.crc32(data))
+        s = os.path.join(str(tmp_path), "r%d.bin" % seed)
+        open(s, "wb").write(comp)
+        for in_chunk, out_chunk in ((1 << 30, 1 << 30), (4096, 1 << 16), (100_000, 77_777)):
+            r = subprocess.run([WALKER, str(prop), s, str(len(data)), str(in_chunk), "0",
+                                str(out_chunk)], stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+                               text=True, timeout=300)
+            assert r.returncode == 0, r.stderr
+            got = r.stdout.split()
+            assert " ".join(got[:5]) == want, (seed, in_chunk, out_chunk, got, want)

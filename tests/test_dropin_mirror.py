@@ -129,3 +129,89 @@ def test_decode_to_buf_one_launch_per_call(L):
     assert ncalls == calls
     assert h2d <= sum(min(1 << 19, len(comp) - sum(x[2] for x in trace[:i]))
                       for i in range(len(trace))) + calls * 256 + 16384
+
+
+# ---------------------------------------------------------------- rings, host edits
+# Driven through the GPU library and through the reference's own LzmaDec.c
+# (oracle/_ref/libref_lzma.so, compiled in place) with the same host-side
+# actions; both must agree call by call.
+needs_ref = pytest.mark.skipif(not native.have_ref(), reason="oracle/_ref/libref_lzma.so not built")
+
+
+@needs_ref
+def test_ring_smaller_than_window_reads_the_ring_slot(L):
+    """A caller-owned ring (LzmaDec_AllocateProbs + a 4 KiB dic) smaller than
+    the dictionary size (64 KiB) and the session kernel's LDS window (up to
+    128 KiB): matches at distance 5,096 read the ring slot the reference reads
+    (dicPos - rep0 + dicBufSize: the byte 1,000 back), not the true history byte
+    the window would still hold -- the window serves distances up to
+    min(window, dicBufSize) only.  Hand-made streams (tests/lzmaenc_min.py)
+    keep every such read inside the ring."""
+    import lzmaenc_min as E
+    ref = native.ref()
+    for seed in (1, 2, 3):
+        comp, props, out = E.ring_reach_stream(seed)
+        for in_chunk, out_chunk in ((1 << 30, 3000), (700, 1000), (1 << 30, 1 << 30)):
+            want = E.ring_decode(ref, comp, props, 4096, len(out), in_chunk, out_chunk)
+            assert want[1] == out
+            got = E.ring_decode(L.lib, comp, props, 4096, len(out), in_chunk, out_chunk)
+            assert got == want, (seed, in_chunk, out_chunk, got[0][-3:], want[0][-3:])
+
+
+@needs_ref
+def test_host_edits_between_calls_match_the_reference(L):
+    """Host-side changes between DecodeToDic calls reach the device mirror:
+    every probability cell reset to 1024 by the host (the table hash check),
+    dicPos moved back (not a pure advance: the history is dropped and the whole
+    dictionary re-uploaded), and both at once; output and per-call results equal
+    the reference's LzmaDec.c given the same edits."""
+    import ctypes
+    import lzmaenc_min as E
+    ref = native.ref()
+    n = 300_000
+    data, comp, props = _stream(880011, n)
+
+    def reset_probs(k, d):
+        if k == 3:
+            cells = (ctypes.c_uint16 * d.numProbs).from_address(d.probs)
+            for i in range(d.numProbs):
+                cells[i] = 1024
+
+    def move_back(k, d):
+        if k == 4:
+            d.dicPos = d.dicPos - 1000
+
+    def both(k, d):
+        reset_probs(k, d)
+        move_back(k, d)
+
+    for edit in (None, reset_probs, move_back, both):
+        want = E.dic_calls(ref, comp, props, n, 9000, edit)
+        got = E.dic_calls(L.lib, comp, props, n, 9000, edit)
+        assert got[0] == want[0], (edit, got[0][-3:], want[0][-3:])
+        assert got[1] == want[1], edit
+        if edit is None:
+            assert want[1] == data
+
+
+def test_decoder_alternating_devices(L):
+    """A decoder used on one device, then another, then the first again decodes
+    on current state (its mirrors on the other devices are dropped)."""
+    import ctypes
+    if L.device_count() < 2:
+        pytest.skip("one visible device: the alternating-device case needs two")
+    n, win = 1 << 19, 1 << 14
+    data, comp, props = _stream(880012, n)
+    want = native.dic_decode(native.oracle(), "orc", comp, props, n, win)
+
+    hip = ctypes.CDLL("libamdhip64.so")
+
+    def hop(k, dec):  # the next call runs on the other device
+        assert hip.hipSetDevice((k + 1) % 2) == 0
+
+    try:
+        calls, trace, out, used = L.dic_decode(comp, props, n, win, between=hop)
+    finally:
+        hip.hipSetDevice(0)
+    assert [tuple(t) for t in trace] == [tuple(t) for t in want[1]]
+    assert out == data

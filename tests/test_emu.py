@@ -45,12 +45,11 @@ EMU_VARIANTS = {
     "coop_window_64k": "-DEMU_COOP_ALL_WIN -DEMU_WIN_BYTES=65536",
     "session_coop_window_4k": "-DEMU_SESS_COOP_WIN -DEMU_WIN_BYTES=4096",
     "session_coop_window_64k": "-DEMU_SESS_COOP_WIN -DEMU_WIN_BYTES=65536",
-    # round 4: the decision-level loop (lz_run_step) on the throughput
-    # instantiation and on other placements of the same code
-    "step_interleaved_instantiation": "-DEMU_STEP_ILV",
-    "step_latency_mask": "-DEMU_STEP -DLZGPU_LDS_MASK=0x1BF",
-    "step_all_lds": "-DEMU_STEP -DLZGPU_LDS_MASK=0x7FF",
-    "step_all_global": "-DEMU_STEP -DLZGPU_LDS_MASK=0",
+    # round 5: the one-lane latency kernel's window (1 KiB: most reads fall back
+    # to the dictionary; 4 KiB: config 2's; deferred output and write-through)
+    "lane_window_1k": "-DEMU_LAT_WIN -DEMU_WIN_BYTES=1024",
+    "lane_window_4k": "-DEMU_LAT_WIN -DEMU_WIN_BYTES=4096",
+    "lane_window_4k_write_through": "-DEMU_LAT_WIN -DEMU_WIN_BYTES=4096 -DLZGPU_LANE_DEFER=0",
 }
 
 

@@ -86,3 +86,20 @@ def test_oracle_vs_live_reference_fuzz(orc):
         a = native.decode(ref, "ref", bytes(c), pr, cap, fin)
         b = native.decode(orc, "orc", bytes(c), pr, cap, fin)
         assert a == b, (it, lc, lp, pb, d, n, kind, mode, cap, fin)
+
+
+@pytest.mark.skipif(not native.have_ref(), reason="oracle/_ref/libref_lzma.so not built")
+def test_symbol_encoder_pinned_by_reference_ring_decode():
+    """tests/lzmaenc_min.py writes the hand-made ring-reach streams of
+    tests/test_dropin_mirror.py.  The reference's own
+    LzmaDec_DecodeToBuf over a caller-owned 4 KiB ring reproduces the encoder's
+    model of the decoder output exactly; a flat LzmaDecode of the same stream
+    does not -- its matches at distance 5,096 read true history where the ring
+    decoder reads the slot 1,000 bytes back, which is what the GPU test pins."""
+    import lzmaenc_min as E
+    for seed in (1, 2, 3):
+        comp, props, out = E.ring_reach_stream(seed)
+        trace, got = E.ring_decode(native.ref(), comp, props, 4096, len(out), 1 << 30, 3000)
+        assert got == out and trace[-1][0] == 0
+        flat = native.decode(native.ref(), "ref", comp, props, len(out), 0)
+        assert flat[4] != out
