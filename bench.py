@@ -615,7 +615,8 @@ def print_prof(L):
                  "lit_lanes|slot_sub3_b|cyc_direct", "mlit_lanes|n_slot|cyc_align",
                  "mixed_iters|cyc_rep_bits", "match_entries|cyc_len", "match_lanes|cyc_dist",
                  "live_lanes|n_dist", "bytes", "matches|cyc_drain|cyc_specpos",
-                 "cyc_ismatch", "cyc_literal", "cyc_lit_tail", "cyc_iterations")
+                 "cyc_ismatch", "cyc_literal", "cyc_lit_tail", "cyc_iterations",
+                 "cyc_input_tail", "tail_passes", "cyc_table_init")
         prof = {k: buf[i] / lanes for i, k in enumerate(names)}
         prof["other_in_decode_to_dic"] = prof["decode_to_dic_total"] - sum(
             prof[k] for k in names[:3])  # refills overlap the first three regions
@@ -1661,13 +1662,33 @@ def run_secondary(cfgs, steps=5, warmup=1, timeout=420):
     return out
 
 
-def issue_roofline(cfg, kernel_ms):
+ISSUE_PEAKS = os.path.join(ROOT, "profiles", "r05_issue", "issue_peaks.json")
+
+
+def issue_peaks():
+    """Measured SIMD issue ceilings (scripts/ubench/simd_issue_ubench.hip, run
+    on the box; summarized in profiles/r05_issue/issue_peaks.json): wave-
+    instructions of any kind a SIMD sustains per cycle with W co-resident
+    waves, timed over whole kernels (round 4 priced a SIMD
+    at one VALU instruction per 4 cycles from per-wave s_memtime medians).
+    Falls back to MI355X_MICROARCH.md's SIMD-32 figure, one wave64 VALU
+    instruction per 2 cycles per SIMD."""
+    try:
+        return json.load(open(ISSUE_PEAKS))
+    except (OSError, ValueError):
+        return {"source": "MI355X_MICROARCH.md:53-54 (SIMD-32: one wave64 VALU per 2 cycles)",
+                "valu_per_simd_cycle": 0.5, "simd_inst_per_cycle": {}, "wave_cycles_per_inst": 4.0}
+
+
+def issue_roofline(cfg, kernel_ms, waves_per_simd=None):
     """Issue-side figures of the decode kernel from the committed rocprofv3 PMC
     summary for this config (profiles/pmc_<cfg>.json, written by
-    scripts/pmc_summary.py from separate --pmc passes of this bench):
-    VALU issue rate against the chip's one VALU wave-instruction per SIMD per
-    4-cycle issue window, lanes active per VALU instruction, share of wave cycles
-    waiting."""
+    scripts/pmc_summary.py from separate --pmc passes of this bench), priced
+    against the measured SIMD issue ceilings (issue_peaks()): instructions of
+    every kind issued per SIMD-cycle against the ceiling at the kernel's waves
+    per SIMD, VALU instructions against the SIMD-32 VALU rate, lanes active per
+    VALU instruction, and the shares of wave cycles issuing / parked on
+    s_waitcnt / stalled for issue."""
     path = os.path.join(ROOT, "profiles", f"pmc_{cfg}.json")
     if not os.path.exists(path):
         return None
@@ -1676,27 +1697,37 @@ def issue_roofline(cfg, kernel_ms):
     except (OSError, ValueError):
         return None
     c = p.get("counters", {})
-    out = {"source": os.path.relpath(path, ROOT), "binary": p.get("binary")}
+    pk = issue_peaks()
+    out = {"source": os.path.relpath(path, ROOT), "binary": p.get("binary"),
+           "peaks_source": pk.get("source")}
     clk = p.get("effective_clock_GHz") or 2.4
+    simds = 256 * 4
+    cyc = kernel_ms * 1e-3 * clk * 1e9  # shader cycles of one launch
     if "SQ_INSTS_VALU" in c:
-        # SQ_INSTS_* count per SE/XCD instance summed; wave-instructions per launch.
-        # The sequencer visits a SIMD once per 4-cycle window and issues at most one
-        # VALU instruction there (SQ_ACTIVE_INST_VALU = SQ_INSTS_VALU: one quad-cycle
-        # each), so the chip's VALU issue peak is 256 CUs x 4 SIMDs x clk / 4.
-        peak = 256 * 4 * clk * 1e9 / 4  # VALU wave-instructions per second, whole chip
-        rate = c["SQ_INSTS_VALU"] / (kernel_ms * 1e-3)
+        # SQ_INSTS_* are wave-instructions per launch (summed over XCD/SE instances)
+        kinds = ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_INSTS_BRANCH",
+                 "SQ_INSTS_VMEM_RD", "SQ_INSTS_VMEM_WR", "SQ_INSTS_SMEM")
+        total = sum(c.get(k, 0.0) for k in kinds)
+        per_simd = total / simds / cyc
+        valu = c["SQ_INSTS_VALU"] / simds / cyc
         out.update({"valu_insts_per_launch": c["SQ_INSTS_VALU"],
                     "salu_insts_per_launch": c.get("SQ_INSTS_SALU"),
-                    "valu_issue_per_s": rate, "valu_issue_peak_per_s": peak,
-                    "valu_issue_frac": round(rate / peak, 4)})
+                    "insts_per_launch": total,
+                    "insts_per_simd_cycle": round(per_simd, 4),
+                    "valu_per_simd_cycle": round(valu, 4),
+                    "valu_frac": round(valu / pk.get("valu_per_simd_cycle", 0.5), 4)})
+        w = waves_per_simd
+        ceil = (pk.get("simd_inst_per_cycle") or {}).get(str(w)) if w else None
+        if ceil:
+            out["issue_ceiling_per_simd_cycle"] = ceil
+            out["issue_frac"] = round(per_simd / ceil, 4)
     if "SQ_THREAD_CYCLES_VALU" in c and "SQ_ACTIVE_INST_VALU" in c and c["SQ_ACTIVE_INST_VALU"]:
         out["lanes_active_per_valu"] = round(c["SQ_THREAD_CYCLES_VALU"] / c["SQ_ACTIVE_INST_VALU"], 2)
     if "SQ_WAVE_CYCLES" in c and c["SQ_WAVE_CYCLES"]:
-        # SQ_WAIT_ANY: wave-cycles waiting on anything (s_waitcnt on memory / LDS);
-        # SQ_WAIT_INST_ANY: waiting for an instruction to be issued (arbitration)
+        # SQ_WAIT_ANY: wave-cycles parked on s_waitcnt (memory / LDS);
+        # SQ_WAIT_INST_ANY: ready but not issued (arbitration, dependency)
         for k, name in (("SQ_WAIT_ANY", "wait_any_frac"), ("SQ_WAIT_INST_ANY", "wait_issue_frac"),
-                        ("SQ_ACTIVE_INST_ANY", "issue_frac"),
-                        ("SQ_ACTIVE_INST_VALU", "valu_busy_frac")):
+                        ("SQ_ACTIVE_INST_ANY", "issue_frac_of_wave_cycles")):
             if k in c:
                 out[name] = round(c[k] / c["SQ_WAVE_CYCLES"], 4)
     for k in ("hbm_bytes_per_launch", "hbm_read_bytes_x2", "hbm_write_bytes", "kernel_avg_ns"):
@@ -1902,7 +1933,7 @@ def main():
             traffic = json.load(open(tpath)).get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
-    issue = issue_roofline(args.config, avg_kern_ms)
+    issue = issue_roofline(args.config, avg_kern_ms, int(plan.waves_per_simd))
     secondary = None
     if rank == 0 and world == 1 and args.config == "cfg3" and not args.no_secondary:
         # reported with their own `verified`; the headline's stands on config 3 alone

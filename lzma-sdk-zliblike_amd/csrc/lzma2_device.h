@@ -113,10 +113,7 @@ __device__ __forceinline__ int lz2_decode_to_dic(Lz2StateT<Lo>& p, uint64_t dic_
       // stored chunk (LzmaDec_UpdateWithUncompressed, Lzma2Dec.c:159-166)
       for (uint64_t i = 0; i < in_cur; ++i) {
         p.dec.dic[p.dec.pos + i] = src[i];
-        if constexpr (lwin_on<M>())
-          win_put_at(p.dec.win, p.dec.pos + i, src[i]);
-        else if constexpr (win_on<M>())
-          win_put(p.dec.win, src[i]);
+        if constexpr (win_on<M>()) win_put(p.dec.win, src[i]);
       }
       p.dec.pos += in_cur;
       if (p.dec.full == 0 && p.dec.dict_size - p.dec.total <= in_cur)

@@ -56,6 +56,17 @@ constexpr uint32_t kProbOne = 2048u;
 constexpr uint32_t kProbInit = 1024u;
 constexpr uint32_t kLookahead = 20u;  // LZMA_REQUIRED_INPUT_MAX
 constexpr uint32_t kLenDone = 274u;   // kMatchSpecLenStart
+// Cooperative kernels (round 5): the bit trees of a
+// symbol decided from load batches -- the literal tree as two batches of four
+// levels (15 cells each), the matched literal's eight all-match cells at once,
+// the length coder's choice bits and 3-level trees in one batch, the slot tree
+// as two batches of three levels, SpecPos and Align likewise -- instead of one
+// dependent LDS round trip (ds_read -> address) per level: with one wave per
+// SIMD the LDS has bandwidth to spare and the serial chain is the bound.
+// -DLZGPU_COOP_BATCH=0 keeps one level per round trip (A/B).
+#ifndef LZGPU_COOP_BATCH
+#define LZGPU_COOP_BATCH 0
+#endif
 // direct bits decided several per step on the cooperative kernel (direct_coop;
 // -DLZGPU_DIRECT_CHUNKS=0 restores the bit-serial loop for A/B)
 #ifndef LZGPU_DIRECT_CHUNKS
@@ -283,41 +294,6 @@ __device__ __forceinline__ void win_adv(LzWin& w, uint32_t n) {
   w.t += n;
   w.av = (w.av + n > w.lim) ? w.lim : w.av + n;
 }
-// Eight window bytes from slot s on, and the low n (1..8) bytes of v to slots
-// s.. -- one unaligned LDS access (gfx950 runs LDS, like global memory, in
-// unaligned mode: ds_read_b64 / ds_write_b64 at any byte address) where the
-// bytes do not cross the window's end, byte by byte where they do.
-#ifdef LZGPU_HOST_EMU
-__device__ __forceinline__ uint64_t lds_ldu64(const lds_u8* p) {
-  uint64_t v;
-  __builtin_memcpy(&v, p, 8);
-  return v;
-}
-__device__ __forceinline__ void lds_stu64(lds_u8* p, uint64_t v) { __builtin_memcpy(p, &v, 8); }
-#else
-typedef uint64_t lz_lds_u64a1 __attribute__((aligned(1)));
-__device__ __forceinline__ uint64_t lds_ldu64(const lds_u8* p) {
-  return *(const __attribute__((address_space(3))) lz_lds_u64a1*)p;
-}
-__device__ __forceinline__ void lds_stu64(lds_u8* p, uint64_t v) {
-  *(__attribute__((address_space(3))) lz_lds_u64a1*)p = v;
-}
-#endif
-__device__ __forceinline__ uint64_t win_ld8(const LzWin& w, uint32_t s) {
-  const uint32_t i = s & w.mask;
-  if (i + 8u <= w.mask + 1u) return lds_ldu64(w.b + i);
-  uint64_t v = 0;
-  for (uint32_t k = 0; k < 8u; ++k) v |= uint64_t(w.b[(s + k) & w.mask]) << (8u * k);
-  return v;
-}
-__device__ __forceinline__ void win_stn(const LzWin& w, uint32_t s, uint64_t v, uint32_t n) {
-  const uint32_t i = s & w.mask;
-  if (n == 8u && i + 8u <= w.mask + 1u) {
-    lds_stu64(w.b + i, v);
-    return;
-  }
-  for (uint32_t k = 0; k < n; ++k) w.b[(s + k) & w.mask] = uint8_t(v >> (8u * k));
-}
 template <uint32_t M>
 __host__ __device__ constexpr bool win_on() {
   return (M & kWinBit) != 0u;
@@ -415,7 +391,10 @@ struct LzStateT {
   // [5..13] wave-level counts: batch iterations, active / matched-literal lanes
   // per iteration, iterations with both literal kinds, match-path entries and
   // their lanes, live lanes per iteration, literals, matches (lane-level)
-  uint64_t prof[18];  // [14..16]: IsMatch, literal, batch tail cycles per literal
+  // [14..16]: IsMatch, literal, batch tail cycles per literal; [17] literal
+  // batch iterations; [18] the input tail (look-ahead dry runs + one-symbol
+  // passes, LzmaDec.c:487-675 / :766-812), [19] tail passes, [20] table init
+  uint64_t prof[21];
 #endif
 };
 
@@ -700,11 +679,24 @@ __host__ __device__ constexpr bool def_on() {
 // everywhere it ran -- 8 LZMA2 blocks per CU 5,146 vs 5,494 MB/s, the windowed
 // config 4 3,100 vs 3,318 MB/s (profiles/r04_coop8/, r04_qserial/) -- and was
 // removed in round 5 with the other rejected shapes.
+// -DLZGPU_COOP_Q=1 (A/B, round 5): every cooperative build takes the
+// checkpoint reader, with the batched trees' decisions unchecked after a top-up.
+#ifndef LZGPU_COOP_Q
+#define LZGPU_COOP_Q 0
+#endif
+// -DLZGPU_NORM_SEL=1 (A/B, round 5): NORMALIZE after a checkpoint as selects
+// (range, code and the reader's window chosen by range < 2^24) instead of a
+// branch -- on the cooperative kernels, where every lane takes the same way
+// and the VALU -> VCC -> EXEC branch sits on the decision chain.
+#ifndef LZGPU_NORM_SEL
+#define LZGPU_NORM_SEL 0
+#endif
 template <uint32_t M>
 struct BulkReaderFor {
   static constexpr uint32_t m = M & ~kIlvBit;
   static constexpr bool q = m == LZGPU_LDS_MASK || m == (LZGPU_LDS_MASK_LAT | kCoopBit) ||
-                            m == (LZGPU_LDS_MASK_ALL | kCoopBit);
+                            m == (LZGPU_LDS_MASK_ALL | kCoopBit) ||
+                            (LZGPU_COOP_Q != 0 && (m & kCoopBit) != 0u);
   typedef typename std::conditional<q, GlobalReaderQ, PlainReader>::type type;
 };
 
@@ -717,6 +709,11 @@ struct BulkReaderFor {
 template <uint32_t M>
 __host__ __device__ constexpr bool mb_pf_on() {
   return ((M & kCoopBit) != 0u) || ((M & ~kIlvBit) == LZGPU_LDS_MASK);
+}
+// batched bit trees on the cooperative kernels (LZGPU_COOP_BATCH)
+template <uint32_t M>
+__host__ __device__ constexpr bool coop_batch() {
+  return LZGPU_COOP_BATCH != 0 && (M & kCoopBit) != 0u;
 }
 
 // checkpoint hooks for readers without them: every NORMALIZE checks
@@ -758,7 +755,14 @@ struct Rc {
   }
   // NORMALIZE after a reader checkpoint: the byte is known to be in the window
   __device__ __forceinline__ void norm_u() {
-    if (range < kTop) {
+    if constexpr (LZGPU_NORM_SEL != 0 && kIsQ<Rd>) {
+      const bool n = range < kTop;
+      const uint32_t b = rd->peek();
+      code = n ? ((code << 8) | b) : code;
+      range = n ? (range << 8) : range;
+      rd->win = n ? (rd->win >> 8) : rd->win;
+      rd->nb -= n ? 1u : 0u;
+    } else if (range < kTop) {
       range <<= 8;
       code = (code << 8) | rd_take_u(*rd);
     }
@@ -861,25 +865,38 @@ struct Rc {
     return 2 * m + b1;
   }
   // Four levels below `root` (15 cells) from one load batch; returns
-  // 16 * root + (the four bits, MSB first).
-  template <class P>
+  // 16 * root + (the four bits, MSB first).  The candidates of the levels
+  // below are halved by each decided bit (independent selects), so a level's
+  // probability is one select behind its parent's decision.
+  // U: the decisions take their input bytes unchecked (norm_u), after a
+  // checkpoint reader's top-up (>= 5 bytes held)
+  template <bool U = false, class P>
   __device__ __forceinline__ uint32_t sub4(P probs, uint32_t root) {
-    uint32_t c[15];
+    auto dec = [&](uint32_t p, P cell) { return U ? bit_vu(p, cell) : bit_v(p, cell); };
+    const uint32_t r2 = root * 2, r4 = root * 4, r8 = root * 8;
+    const uint32_t c1 = probs[root];
+    uint32_t c2[2], c4[4], c8[8];
 #pragma unroll
-    for (int l = 0, o = 0; l < 4; o += (1 << l), ++l)
+    for (int k = 0; k < 2; ++k) c2[k] = probs[r2 + k];
 #pragma unroll
-      for (int j = 0; j < (1 << l); ++j) c[o + j] = probs[(root << l) + j];
-    uint32_t m = root, j = 0;  // j = bits decoded so far (the node below root)
+    for (int k = 0; k < 4; ++k) c4[k] = probs[r4 + k];
 #pragma unroll
-    for (int l = 0, o = 0; l < 4; o += (1 << l), ++l) {
-      uint32_t p = c[o];
+    for (int k = 0; k < 8; ++k) c8[k] = probs[r8 + k];
+    const uint32_t b0 = dec(c1, probs + root);
+    uint32_t m = r2 + b0;
+    const uint32_t p1 = b0 ? c2[1] : c2[0];
+    const uint32_t q0 = b0 ? c4[2] : c4[0], q1 = b0 ? c4[3] : c4[1];
+    uint32_t e[4];
 #pragma unroll
-      for (int k = 1; k < (1 << l); ++k) p = (j == uint32_t(k)) ? c[o + k] : p;
-      const uint32_t b = bit_v(p, probs + m);
-      m = 2 * m + b;
-      j = 2 * j + b;
-    }
-    return m;
+    for (int k = 0; k < 4; ++k) e[k] = b0 ? c8[4 + k] : c8[k];
+    const uint32_t b1 = dec(p1, probs + m);
+    m = 2 * m + b1;
+    const uint32_t p2 = b1 ? q1 : q0;
+    const uint32_t f0 = b1 ? e[2] : e[0], f1 = b1 ? e[3] : e[1];
+    const uint32_t b2 = dec(p2, probs + m);
+    m = 2 * m + b2;
+    const uint32_t b3 = dec(b2 ? f1 : f0, probs + m);
+    return 2 * m + b3;
   }
   // Seven cells of a 3-level subtree under `root`, loaded as one batch ahead of
   // the decisions that need them (dec3).
@@ -1246,161 +1263,12 @@ __device__ __forceinline__ uint32_t lz_copy_coop(gbyte* dic, uint64_t pos, uint6
 #endif
 }
 
-// ------------------------------------------------------------------ one-lane window
-//
-// The LDS history window on the one-stream-per-wave latency kernel (round 5,
-// VERDICT r04 item 2; placement LZGPU_LDS_MASK_LAT | kWinBit, lwin_on): a
-// matched literal's byte (LzmaDec.c:176), a short rep's byte (:216) and a match
-// copy's source (:388-407) within the window's reach are LDS reads -- on the
-// one-lane kernel each such global load waited in the in-order vmcnt queue for
-// the lane's earlier output stores.  It runs on flat dictionaries only (batch
-// items: LzmaDecode's output window, LZMA2 ranges), where every byte the
-// decoder writes passes the window once in dictionary order, so window slot =
-// dictionary position & mask and a distance the window holds is simply one
-// <= its size (the decoder's own check keeps every distance <= the position):
-// no write counter or fill level to carry in registers.
-// ldef_on: deferred output, the cooperative kernels' idea (def_on) for a lane
-// alone -- decoded bytes go to the window only and reach the dictionary 16 at a
-// time (one aligned LDS read and one 16-byte global store per 16 output bytes,
-// instead of a byte store per literal and 8-byte stores per copy), the last
-// partial 16 before the bulk pass returns.  A read the window does not serve
-// (dist > its size >= 1 KiB) lies before every pending byte.
-// -DLZGPU_LANE_DEFER=0 writes through (A/B).
-#ifndef LZGPU_LANE_DEFER
-#define LZGPU_LANE_DEFER 1
-#endif
-template <uint32_t M>
-__host__ __device__ constexpr bool lwin_on() {
-  return win_on<M>() && (M & kCoopBit) == 0u;
-}
-template <uint32_t M>
-__host__ __device__ constexpr bool ldef_on() {
-  return LZGPU_LANE_DEFER != 0 && lwin_on<M>();
-}
-// the byte of dictionary position p to its window slot (one-lane window)
-__device__ __forceinline__ void win_put_at(const LzWin& w, uint64_t p, uint32_t v) {
-  w.b[uint32_t(p) & w.mask] = uint8_t(v);
-}
-#ifdef LZGPU_HOST_EMU
-__device__ __forceinline__ void win_store16(const LzWin& w, gbyte* dic, uint64_t c) {
-  __builtin_memcpy(dic + c - 16, w.b + ((uint32_t(c) - 16u) & w.mask), 16);
-}
-#else
-typedef unsigned int lz_w32x4 __attribute__((ext_vector_type(4)));
-typedef lz_w32x4 lz_w32x4a1 __attribute__((aligned(1)));
-// dictionary bytes [c - 16, c) (c a multiple of 16) from their window slots:
-// one aligned LDS read, one 16-byte global store
-__device__ __forceinline__ void win_store16(const LzWin& w, gbyte* dic, uint64_t c) {
-  const lz_w32x4 v =
-      *(const __attribute__((address_space(3))) lz_w32x4*)(w.b + ((uint32_t(c) - 16u) & w.mask));
-  *(__attribute__((address_space(1))) lz_w32x4a1*)(dic + c - 16) = v;
-#if LZGPU_SHADOW_OUT
-  *(__attribute__((address_space(1))) lz_w32x4a1*)(dic + c - 16 + LZGPU_SHADOW_OUT) = v;
-#endif
-}
-#endif
-// every 16-byte chunk that positions [p0, p1) completed, to the dictionary
-__device__ __forceinline__ void win_store_chunks(const LzWin& w, gbyte* dic, uint64_t p0,
-                                                 uint64_t p1) {
-  for (uint64_t c = (p0 + 16u) & ~uint64_t(15); c <= p1; c += 16u) win_store16(w, dic, c);
-}
-// the pending bytes of the last, partial chunk, [pos - (pos & 15), pos), to
-// the dictionary: it is complete again
-__device__ __forceinline__ void win_store_tail(const LzWin& w, gbyte* dic, uint64_t pos) {
-  const uint32_t k = uint32_t(pos) & 15u;
-  if (k == 0) return;
-  gbyte* d = dic + pos - k;
-  const uint32_t s0 = uint32_t(pos) - k;
-  const uint64_t lo = win_ld8(w, s0);
-  if (k >= 8) {
-    stu64(d, lo);
-    stu_tail(d + 8, win_ld8(w, s0 + 8), k - 8);
-  } else {
-    stu_tail(d, lo, k);
-  }
-}
-// one output byte at pos (literal / short rep), under every placement
+// one output byte at pos (literal / short rep), written through to the
+// window where the placement has one
 template <uint32_t M>
 __device__ __forceinline__ void lz_emit(gbyte* dic, uint64_t pos, uint32_t v, LzWin* w) {
-  if constexpr (ldef_on<M>()) {
-    win_put_at(*w, pos, v);
-    if (((uint32_t(pos) + 1u) & 15u) == 0) win_store16(*w, dic, pos + 1);
-  } else {
-    lz_put(dic + pos, v);
-    if constexpr (lwin_on<M>())
-      win_put_at(*w, pos, v);
-    else if constexpr (win_on<M>())
-      win_put(*w, v);
-  }
-}
-// the byte at distance dist before pos: from the one-lane window where it reaches
-template <uint32_t M>
-__device__ __forceinline__ uint32_t lz_back(const gbyte* dic, uint64_t pos, uint32_t dist,
-                                            uint64_t cap, const LzWin* w) {
-  if constexpr (lwin_on<M>()) {
-    if (dist <= w->mask + 1u) return w->b[(uint32_t(pos) - dist) & w->mask];
-  }
-  return dic[ring_back(pos, dist, cap)];
-}
-// LZ copy of the one-lane window kernel (flat dictionary: the source
-// dic[pos - dist, ...) never wraps): lz_copy's shapes -- 8 bytes per step,
-// the period of a distance < 8 built once in a register -- with the source
-// from the window when it reaches and every byte written to the window (and,
-// writing through, to the dictionary).  Returns the last byte copied.
-template <bool DEF>
-__device__ __forceinline__ uint32_t lz_copy_lw(gbyte* dic, uint64_t pos, uint32_t n, uint32_t dist,
-                                               const LzWin& w) {
-  const uint32_t t = uint32_t(pos);
-  const bool inwin = dist <= w.mask + 1u;
-  gbyte* d = dic + pos;
-  const gbyte* src = d - dist;
-  uint32_t last;
-  uint64_t v = 0;
-  if (dist >= 8) {
-    // source bytes [i, i + 8) of step i lie at least 8 bytes behind its
-    // destination: written before the step reads them
-    uint32_t i = 0;
-    for (; i + 8 <= n; i += 8) {
-      v = inwin ? win_ld8(w, t - dist + i) : ldu64(src + i);
-      win_stn(w, t + i, v, 8);
-      if constexpr (!DEF) stu64(d + i, v);
-    }
-    last = uint32_t(v >> 56);
-    if (i < n) {
-      v = inwin ? win_ld8(w, t - dist + i) : ldu64(src + i);
-      const uint32_t rem = n - i;
-      win_stn(w, t + i, v, rem);
-      if constexpr (!DEF) stu_tail(d + i, v, rem);
-      last = uint32_t(v >> (8 * (rem - 1))) & 0xFFu;
-    }
-  } else {
-    // dist < 8 (inside any window): the dist bytes before pos repeated
-    v = win_ld8(w, t - dist);
-    v &= ~0ull >> (64 - 8 * dist);
-    v |= v << (8 * dist);
-    if (dist < 4) v |= v << (16 * dist);
-    if (dist < 2) v |= v << 32;
-    const uint32_t ph = 8u % dist;  // phase advance per 8 bytes
-    for (uint32_t i = 0;; i += 8) {
-      const uint32_t rem = n - i;
-      if (rem <= 8) {
-        win_stn(w, t + i, v, rem);
-        if constexpr (!DEF) {
-          if (rem == 8)
-            stu64(d + i, v);
-          else
-            stu_tail(d + i, v, rem);
-        }
-        last = uint32_t(v >> (8 * (rem - 1))) & 0xFFu;
-        break;
-      }
-      win_stn(w, t + i, v, 8);
-      if constexpr (!DEF) stu64(d + i, v);
-      v = (v >> (8 * ph)) | (v << (8 * (dist - ph)));
-    }
-  }
-  if constexpr (DEF) win_store_chunks(w, dic, pos, pos + n);
-  return last;
+  lz_put(dic + pos, v);
+  if constexpr (win_on<M>()) win_put(*w, v);
 }
 
 // ------------------------------------------------------------------ symbol loop
@@ -1439,14 +1307,23 @@ __device__ __forceinline__ void lz_literal(Rc<Rd>& rc, const Tab<M, Lo>& T, uint
   if (st < 7) {
     st = (st < 4) ? 0 : st - 3;
     auto lp = T.template at<S_LITP>(ctx << 8);
-    const uint32_t m = rc.template tree_u<4>(lp, 1);
-    rd_topup(*rc.rd);
-    sym = rc.template tree_u<4>(lp, m);
+    if constexpr (coop_batch<M>() && kIsQ<Rd>) {
+      rd_topup(*rc.rd);
+      const uint32_t m = rc.template sub4<true>(lp, 1);
+      rd_topup(*rc.rd);
+      sym = rc.template sub4<true>(lp, m);
+    } else if constexpr (coop_batch<M>()) {
+      sym = rc.sub4(lp, rc.sub4(lp, 1));
+    } else {
+      const uint32_t m = rc.template tree_u<4>(lp, 1);
+      rd_topup(*rc.rd);
+      sym = rc.template tree_u<4>(lp, m);
+    }
   } else {
-    uint32_t mbyte = mb_pf_on<M>() ? mb_pf : lz_back<M>(dic, pos, r0, cap, w);
+    uint32_t mbyte = mb_pf_on<M>() ? mb_pf : uint32_t(dic[ring_back(pos, r0, cap)]);
     st = (st < 10) ? st - 3 : st - 6;
     constexpr bool p_lds = ((M >> S_LITP) & 1u) != 0u, m_lds = ((M >> S_LITM) & 1u) != 0u;
-    if constexpr (p_lds && !m_lds) {
+    if constexpr ((p_lds && !m_lds) || coop_batch<M>()) {
       // While the decoded bits equal the match byte's, the cell of bit k is
       // fixed by the match byte alone (offs stays 0x100, symbol = its top k
       // bits under a leading 1): load all eight matched-tree cells at once
@@ -1658,9 +1535,8 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
                                                           r0, cap, mb_pf, &s.win);
             pos++;
           } else {
-            prev = lz_back<M>(dic, pos, r0, cap, &s.win);
-            lz_emit<M>(dic, pos, prev, &s.win);
-            pos++;
+            prev = dic[ring_back(pos, r0, cap)];
+            lz_put(dic + pos++, prev);
             if constexpr (mb_pf_on<M>()) mb_pf = dic[ring_back(pos, r0, cap)];
           }
           total++;
@@ -1698,7 +1574,7 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
       auto lbase = [&]() {
         if constexpr (len_lds) return T.lo + lsec_o; else return T.g(lsec_o);
       }();
-      if constexpr (!len_lds) {
+      if constexpr (!len_lds || coop_batch<M>()) {
         // global length coder: the choice bits and the low tree load together,
         // the mid tree only behind choice = 1
         if constexpr ((M & ~kIlvBit) != LZGPU_LDS_MASK) {
@@ -1743,7 +1619,7 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
     if (st >= 12) {
       const uint32_t lstate = len < 4 ? len : 3;
       uint32_t dist;
-      if constexpr (((M >> S_SLOT) & 1u) == 0u) {
+      if constexpr (((M >> S_SLOT) & 1u) == 0u || coop_batch<M>()) {
         auto sl_t = T.template at<S_SLOT>(lstate << 6);
 #if LZGPU_PROF == 1 && !defined(LZGPU_HOST_EMU)
         // one global round trip + 3 decisions, timed (profiling builds)
@@ -1777,7 +1653,7 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
           dist <<= nbits;
           uint32_t mask = 1, node = 1;
           const uint32_t sp = dist - slot - 1;
-          if constexpr (((M >> S_SPEC) & 1u) == 0u) {
+          if constexpr (((M >> S_SPEC) & 1u) == 0u || coop_batch<M>()) {
             if (nbits >= 3) {
               // first three reverse-tree bits in one load batch
               node = rc.sub3(T.template at<S_SPEC>(sp), 1);
@@ -1814,7 +1690,7 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
 #endif
           dist <<= 4;
           uint32_t node = 1;
-          if constexpr (((M >> S_ALIGN) & 1u) == 0u) {
+          if constexpr (((M >> S_ALIGN) & 1u) == 0u || coop_batch<M>()) {
             if constexpr ((M & ~kIlvBit) != LZGPU_LDS_MASK) {
               // all four reverse bits from one batch of the 15 cells
               node = rc.sub4(T.template at<S_ALIGN>(0), 1);
@@ -1868,10 +1744,7 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
         prev = lz_copy_coop<win_on<M>(), def_on<M>()>(dic, pos, from, n, r0, cap, mb_pf, &s.win);
         pos += n;
       } else {
-        if constexpr (lwin_on<M>())
-          prev = lz_copy_lw<ldef_on<M>()>(dic, pos, n, r0, s.win);
-        else
-          prev = lz_copy(dic, pos, from, n, r0, cap);
+        prev = lz_copy(dic, pos, from, n, r0, cap);
         pos += n;
         if constexpr (mb_pf_on<M>()) mb_pf = dic[ring_back(pos, r0, cap)];
       }
@@ -1880,7 +1753,6 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
   } while (pos < limit && rd.used() < in_limit);
 
   if constexpr (def_on<M>()) win_flush(s.win, dic, pos);  // the dictionary complete again
-  if constexpr (ldef_on<M>()) win_store_tail(s.win, dic, pos);
   rc.norm();
   s.range = rc.range;
   s.code = rc.code;
@@ -1906,10 +1778,7 @@ __device__ __forceinline__ void lz_flush_pending(LzStateT<Lo>& s, uint64_t limit
   while (n-- != 0) {
     const uint8_t b = s.dic[ring_back(s.pos, s.rep0, s.cap)];
     s.dic[s.pos] = b;
-    if constexpr (lwin_on<M>())
-      win_put_at(s.win, s.pos, b);
-    else if constexpr (win_on<M>())
-      win_put(s.win, b);
+    if constexpr (win_on<M>()) win_put(s.win, b);
     s.pos++;
   }
 }
@@ -2193,10 +2062,20 @@ __device__ __forceinline__ int lz_decode_to_dic(LzStateT<Lo>& s, uint64_t dic_li
       if (s.pending != 0) { status = kStNotDone; return kErrData; }
       at_end_check = true;
     }
+#if LZGPU_PROF && !defined(LZGPU_HOST_EMU)
+    const uint64_t t_init = lz_clock();
     if (s.need_state_init) lz_init_state_real<M>(s);
+    s.prof[20] += lz_clock() - t_init;
+#else
+    if (s.need_state_init) lz_init_state_real<M>(s);
+#endif
 
     if (!WithTemp || s.tmp_n == 0) {
       uint32_t in_limit;
+#if LZGPU_PROF && !defined(LZGPU_HOST_EMU)
+      const uint64_t t_tail = lz_clock();
+      const bool tail = avail < kLookahead || at_end_check;
+#endif
       if (avail < kLookahead || at_end_check) {
         int k = lz_probe<M>(s, src, avail);
         if (k == PROBE_SHORT) {
@@ -2217,6 +2096,10 @@ __device__ __forceinline__ int lz_decode_to_dic(LzStateT<Lo>& s, uint64_t dic_li
 #if LZGPU_PROF && !defined(LZGPU_HOST_EMU)
       const int rr = lz_run_split<M>(s, dic_limit, rd, in_limit);
       s.prof[4] += rd.prof;
+      if (tail) {
+        s.prof[18] += lz_clock() - t_tail;
+        s.prof[19] += 1;
+      }
       if (rr != kOk) return kErrData;
 #else
       if (lz_run_split<M>(s, dic_limit, rd, in_limit) != kOk) return kErrData;

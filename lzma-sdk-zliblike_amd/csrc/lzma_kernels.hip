@@ -73,16 +73,13 @@ __global__ void __launch_bounds__(64) lzgpu_decode_batch_kernel(
 // lane group g (32 lanes of one workgroup) owns rows of kIlv cells, `slot_cells`
 // rows, and lane l its column l; the lane keeps its column for every stream
 // it takes from the queue.
-// Windowed placements (M & kWinBit: the one-lane latency kernel, round 5):
-// the workgroup's single lane keeps its LDS history window of `win_bytes`
-// after its table slice (16-byte aligned).
 
 template <int W, uint32_t M, bool K2>
 __global__ void __launch_bounds__(64, W) lzgpu_decode_lds_kernel(
     const LzmaGpuStreamDesc* __restrict__ descs, const uint32_t* __restrict__ order, uint32_t n,
     const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, uint16_t* __restrict__ ws,
     LzmaGpuResult* __restrict__ results, uint32_t stride, uint32_t* __restrict__ queue,
-    uint64_t slot_off, uint32_t slot_cells, uint32_t start, uint32_t win_bytes) {
+    uint64_t slot_off, uint32_t slot_cells, uint32_t start) {
   extern __shared__ uint32_t lz_smem[];
   // the lane's LDS slice; interleaved (lds_ilv): its column of its 32-lane
   // group's rows
@@ -100,15 +97,49 @@ __global__ void __launch_bounds__(64, W) lzgpu_decode_lds_kernel(
   }
   (void)slot_off;
   (void)slot_cells;
-  lds_u8* win = nullptr;
-  if constexpr (win_on<M>())
-    win = (lds_u8*)((uint8_t*)lz_smem) + ((size_t(stride) * 2 + 15) & ~size_t(15));
-  (void)win_bytes;
   while (idx < n) {
     const uint32_t id = order ? order[idx] : idx;
     const LzmaGpuStreamDesc d = descs[id];
-    results[id] = lane_decode_lds<M, K2>(d, src, dst, ws, lo, stride, gcol, win, win_bytes);
+    results[id] = lane_decode_lds<M, K2>(d, src, dst, ws, lo, stride, gcol);
     idx = start + atomicAdd(queue, 1u);
+  }
+}
+
+// One-stream waves of the latency placement (round 5): the one-lane decoder
+// run by all D lanes of a workgroup on the same stream -- the instruction
+// stream of lzgpu_decode_lds_kernel with one lane per wave, but with D >= 16
+// lanes in EXEC.  The SIMD issue micro-benchmark (scripts/ubench/
+// simd_issue_ubench.hip lanes, profiles/r05_issue/simd_lanes.jsonl) finds a
+// VALU instruction of a wave with 1-8 active lanes issuing once per ~16.7
+// cycles alone on its SIMD and at 3.5 cycles per SIMD with four such waves,
+// against 4.8 / 2.5 cycles with 16 or more lanes; a dependent LDS decision
+// chain takes 98 against 75 cycles per SIMD at four waves.  Config 2 6.28 ->
+// 6.86 GB/s, config 5 5.13 -> 5.58 (profiles/r05_dup/).  The lanes share the
+// workgroup's LDS slice and store identical values to identical addresses;
+// lane 0 writes the result and takes the next stream from the queue.
+constexpr int kLaneDup = 32;
+template <int W, uint32_t M, bool K2>
+__global__ void __launch_bounds__(64, W) lzgpu_decode_dup_kernel(
+    const LzmaGpuStreamDesc* __restrict__ descs, const uint32_t* __restrict__ order, uint32_t n,
+    const uint8_t* __restrict__ src, uint8_t* __restrict__ dst, uint16_t* __restrict__ ws,
+    LzmaGpuResult* __restrict__ results, uint32_t stride, uint32_t* __restrict__ queue) {
+  extern __shared__ uint32_t lz_smem[];
+  lds_u16* lo = (lds_u16*)((uint16_t*)lz_smem);
+  uint32_t idx = blockIdx.x;
+  while (idx < n) {
+    const uint32_t id = order ? order[idx] : idx;
+    LzmaGpuStreamDesc d = descs[id];
+    // keep the shared decoder state in vector registers (lz_vzero)
+    const uint32_t z = lz_vzero();
+    d.src_off += z;
+    d.dst_off += z;
+    const LzmaGpuResult r = lane_decode_lds<M, K2>(d, src, dst, ws, lo, stride, nullptr);
+    uint32_t next = 0;
+    if (threadIdx.x == 0) {
+      results[id] = r;
+      next = gridDim.x + atomicAdd(queue, 1u);
+    }
+    idx = uint32_t(__builtin_amdgcn_readfirstlane(int(next)));
   }
 }
 
@@ -257,24 +288,6 @@ extern "C" int lzgpu_launch_decode_batch(const LzmaGpuStreamDesc* d_descs, const
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
-// LDS history window of a one-lane latency launch (round 5): the largest
-// power of two, 1 KiB to 64 KiB, that fits beside the lane's table slice in the
-// workgroup's share of the CU (160 KiB / groups_per_cu); 0 = none fits, or
-// LZGPU_LANE_WIN=0 (A/B: the round-4 kernel).
-static uint32_t lane_window_bytes(uint32_t lanes, uint32_t stride, uint32_t groups_per_cu) {
-  static const bool off = [] {
-    const char* e = getenv("LZGPU_LANE_WIN");
-    return e && e[0] == '0';
-  }();
-  if (off || lanes != 1 || groups_per_cu == 0) return 0;
-  const size_t share = (size_t(160 * 1024) / groups_per_cu) & ~size_t(511);
-  const size_t tb = (size_t(stride) * 2 + 15) & ~size_t(15);
-  if (share < tb + 1024) return 0;
-  uint32_t w = 1u << 16;
-  while (w > share - tb) w >>= 1;
-  return w;
-}
-
 template <int W, uint32_t M, bool K2>
 static int launch_lds(const LzmaGpuStreamDesc* d_descs, const uint32_t* d_order, uint32_t n,
                       const uint8_t* d_src, uint8_t* d_dst, uint16_t* d_ws,
@@ -304,15 +317,24 @@ static int launch_lds(const LzmaGpuStreamDesc* d_descs, const uint32_t* d_order,
     }
   }
   const uint32_t lanes_total = grid * lanes;
-  uint32_t win = 0;
-  if constexpr (win_on<M>()) {
-    win = lane_window_bytes(lanes, stride, groups_per_cu);
-    if (!win) return -1;  // the caller checked that one fits
-    lds = std::max(lds, ((size_t(stride) * 2 + 15) & ~size_t(15)) + win);
+  if constexpr (M == LZGPU_LDS_MASK_LAT) {
+    // one-stream waves: kLaneDup lanes per stream (LZGPU_DUP=D overrides for
+    // A/B; D = 1 launches the one-lane kernel)
+    static const int dup = [] {
+      const char* e = getenv("LZGPU_DUP");
+      return e ? atoi(e) : kLaneDup;
+    }();
+    if (lanes == 1 && dup > 1 && dup <= 64) {
+      auto kd = lzgpu_decode_dup_kernel<W, M, K2>;
+      if (allow_full_lds(reinterpret_cast<const void*>(kd)) != 0) return -1;
+      hipLaunchKernelGGL(kd, dim3(grid), dim3(dup), lds, stream, d_descs, d_order, n, d_src, d_dst,
+                         d_ws, d_results, stride, d_queue);
+      return hipGetLastError() == hipSuccess ? 0 : -1;
+    }
   }
   auto kfn = lzgpu_decode_lds_kernel<W, M, K2>;
   hipLaunchKernelGGL(kfn, dim3(grid), dim3(lanes), lds, stream, d_descs, d_order, n, d_src, d_dst,
-                     d_ws, d_results, stride, d_queue, sl.off, sl.cells, lanes_total, win);
+                     d_ws, d_results, stride, d_queue, sl.off, sl.cells, lanes_total);
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
@@ -353,6 +375,12 @@ static int launch_lds_w(const LzmaGpuStreamDesc* d_descs, const uint32_t* d_orde
   if (waves_per_simd == 2)
     return launch_lds<2, M, K2>(d_descs, d_order, n, d_src, d_dst, d_ws, d_results, lanes, stride,
                                 groups_per_cu, max_groups, d_queue, sl, stream);
+#if LZGPU_W3
+  // three waves per SIMD (A/B builds only: -DLZGPU_W3=1)
+  if (waves_per_simd == 3)
+    return launch_lds<3, M, K2>(d_descs, d_order, n, d_src, d_dst, d_ws, d_results, lanes, stride,
+                                groups_per_cu, max_groups, d_queue, sl, stream);
+#endif
   return launch_lds<4, M, K2>(d_descs, d_order, n, d_src, d_dst, d_ws, d_results, lanes, stride,
                               groups_per_cu, max_groups, d_queue, sl, stream);
 }
@@ -395,16 +423,10 @@ static int launch_class(const LzmaGpuStreamDesc* d_descs, const uint32_t* d_orde
                                                 stride, groups_per_cu, max_groups, d_queue,
                                                 stream);
   }
-  if (lds_mask == LZGPU_LDS_MASK_LAT) {
-    // one stream per wave: with the LDS history window where it fits
-    if (lane_window_bytes(lanes, stride, groups_per_cu))
-      return launch_lds_w<LZGPU_LDS_MASK_LAT | kWinBit, K2>(
-          d_descs, d_order, n, d_src, d_dst, d_ws, d_results, lanes, stride, waves_per_simd,
-          groups_per_cu, max_groups, d_queue, sl, stream);
+  if (lds_mask == LZGPU_LDS_MASK_LAT)
     return launch_lds_w<LZGPU_LDS_MASK_LAT, K2>(d_descs, d_order, n, d_src, d_dst, d_ws,
                                                 d_results, lanes, stride, waves_per_simd,
                                                 groups_per_cu, max_groups, d_queue, sl, stream);
-  }
   return -1;  // no kernel built for this placement
 }
 

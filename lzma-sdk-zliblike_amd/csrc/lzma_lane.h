@@ -139,7 +139,7 @@ __device__ __forceinline__ LzmaGpuResult lane_decode_lds(const LzmaGpuStreamDesc
     uint64_t sl = d.src_len;
     int status = kStNone;
 #if LZGPU_PROF && !defined(LZGPU_HOST_EMU)
-    for (int k = 0; k < 18; ++k) p.dec.prof[k] = 0;
+    for (int k = 0; k < 21; ++k) p.dec.prof[k] = 0;
     const uint64_t t0 = lz_clock();
 #endif
     r.res = lz2_decode_to_dic<M>(p, d.dst_cap, (const gbyte*)(src + d.src_off), sl,
@@ -147,7 +147,7 @@ __device__ __forceinline__ LzmaGpuResult lane_decode_lds(const LzmaGpuStreamDesc
 #if LZGPU_PROF && !defined(LZGPU_HOST_EMU)
     p.dec.prof[3] = lz_clock() - t0;
     p.dec.prof[12] = p.dec.total;
-    for (int k = 0; k < 18; ++k) atomicAdd(&g_lz_prof[k], (unsigned long long)p.dec.prof[k]);
+    for (int k = 0; k < 21; ++k) atomicAdd(&g_lz_prof[k], (unsigned long long)p.dec.prof[k]);
     atomicAdd(&g_lz_prof[23], 1ull);
 #endif
     r.status = status;
@@ -182,7 +182,7 @@ __device__ __forceinline__ LzmaGpuResult lane_decode_lds(const LzmaGpuStreamDesc
   uint64_t sl = d.src_len;
   int status = kStNone;
 #if LZGPU_PROF && !defined(LZGPU_HOST_EMU)
-  for (int k = 0; k < 18; ++k) s.prof[k] = 0;
+  for (int k = 0; k < 21; ++k) s.prof[k] = 0;
   const uint64_t t0 = lz_clock();
 #endif
   int res = lz_decode_to_dic<false, M>(s, d.dst_cap, (const gbyte*)(src + d.src_off), sl,
@@ -190,7 +190,7 @@ __device__ __forceinline__ LzmaGpuResult lane_decode_lds(const LzmaGpuStreamDesc
 #if LZGPU_PROF && !defined(LZGPU_HOST_EMU)
   s.prof[3] = lz_clock() - t0;
   s.prof[12] = s.total;  // literals + match bytes: decoded bytes
-  for (int k = 0; k < 18; ++k) atomicAdd(&g_lz_prof[k], (unsigned long long)s.prof[k]);
+  for (int k = 0; k < 21; ++k) atomicAdd(&g_lz_prof[k], (unsigned long long)s.prof[k]);
   atomicAdd(&g_lz_prof[23], 1ull);
 #endif
   if (res == kOk && status == kStMoreInput) res = kErrInputEof;

@@ -235,6 +235,7 @@ __device__ __forceinline__ uint32_t next_entry(const SlicedRound& a) {
 // stream's sections of placement M into LDS, lane 0 makes the call (the
 // per-byte-checked reader of the one-lane kernels), the lanes write them back
 // if the stream goes on.  W = register budget (waves per SIMD).
+constexpr uint32_t kSlicedDup = 32;
 template <int W, uint32_t M>
 __global__ void __launch_bounds__(64, W) lzgpu_sliced_lane_kernel(SlicedRound a) {
   extern __shared__ uint32_t lz_smem[];
@@ -248,12 +249,21 @@ __global__ void __launch_bounds__(64, W) lzgpu_sliced_lane_kernel(SlicedRound a)
     gu16* gp = (gu16*)qp->probs;
     if (!qp->need_init_state) stage<M>(lo, gp, lc, lp, pb, true);
     __syncthreads();
-    if (threadIdx.x == 0) {
+    if (threadIdx.x < kSlicedDup) {
+      // the first wave's kSlicedDup lanes all decode the stream (identical
+      // state, identical stores; lane 0 records the outcome): a wave with
+      // >= 16 lanes in EXEC issues ~1.4-3x faster than a one-lane wave
+      // (round 5, lzma_kernels.hip lzgpu_decode_dup_kernel)
       LzgpuSession q = *qp;
+      const uint32_t z = lz_vzero();  // keep the shared state in vector registers
+      q.in = (const uint8_t*)q.in + z;
+      q.dic = (uint8_t*)q.dic + z;
       LzmaGpuResult r;
       const bool done = sliced_step<M>(q, a.slice, lo, r);
-      sliced_finish(a, i, q, done, r);
-      s_done = done ? 1u : 0u;
+      if (threadIdx.x == 0) {
+        sliced_finish(a, i, q, done, r);
+        s_done = done ? 1u : 0u;
+      }
     }
     __syncthreads();
     if (!s_done) stage<M>(lo, gp, lc, lp, pb, false);

@@ -29,6 +29,7 @@
 #include <stdlib.h>
 
 #include <algorithm>
+#include <string>
 #include <vector>
 
 #define CHECK(x)                                              \
@@ -42,17 +43,27 @@
 
 constexpr int kPerIter = 64;  // instructions (or decisions / 8) per loop iteration
 
+// per-wave record of the occupancy check (rec != nullptr): shader-clock and
+// constant 100 MHz stamps at the start and end of the timed loop, HW_ID and
+// XCC_ID -- which SIMD of which CU the wave ran on, and with whom at once
+struct WaveRec {
+  uint64_t t0, t1, r0, r1;
+  uint32_t hw_id, xcc_id;
+};
+
 template <int T>
 __global__ void __launch_bounds__(64) ub_kernel(uint32_t lanes, uint32_t iters, uint64_t* cyc,
                                                 const uint16_t* __restrict__ tab,
-                                                uint32_t* __restrict__ sink) {
+                                                uint32_t* __restrict__ sink,
+                                                WaveRec* __restrict__ rec) {
   __shared__ uint16_t lt[2048];  // 4 KiB: 32 workgroups per CU fit (W = 8)
   for (int i = threadIdx.x; i < 2048; i += 64) lt[i] = uint16_t(200 + ((i * 2654435761u) >> 21) % 1600);
   __syncthreads();
   uint32_t a0 = threadIdx.x, a1 = a0 * 3, a2 = a0 * 5, a3 = a0 * 7, a4 = a0 + 11, a5 = a0 + 13,
            a6 = a0 + 17, a7 = a0 + 19;
-  uint64_t t0 = 0, t1 = 0;
+  uint64_t t0 = 0, t1 = 0, r0 = 0, r1 = 0;
   if (threadIdx.x < lanes) {
+    r0 = __builtin_amdgcn_s_memrealtime();
     t0 = __builtin_amdgcn_s_memtime();
     if constexpr (T == 0) {
       for (uint32_t s = 0; s < iters; ++s) {
@@ -132,8 +143,16 @@ __global__ void __launch_bounds__(64) ub_kernel(uint32_t lanes, uint32_t iters, 
       a0 = m + range + code;
     }
     t1 = __builtin_amdgcn_s_memtime();
+    r1 = __builtin_amdgcn_s_memrealtime();
   }
-  if (threadIdx.x == 0) cyc[blockIdx.x] = t1 - t0;
+  if (threadIdx.x == 0) {
+    cyc[blockIdx.x] = t1 - t0;
+    if (rec) {
+      // hwreg(HW_REG_HW_ID) and hwreg(HW_REG_XCC_ID), whole registers
+      rec[blockIdx.x] = WaveRec{t0, t1, r0, r1, __builtin_amdgcn_s_getreg((31 << 11) | 4),
+                                __builtin_amdgcn_s_getreg((31 << 11) | 20)};
+    }
+  }
   if (a0 + a1 + a2 + a3 + a4 + a5 + a6 + a7 == 0x12345678u) sink[0] = 1;
 }
 
@@ -147,13 +166,15 @@ static Res run(int grid, uint32_t lanes, uint32_t iters, uint16_t* tab, uint32_t
   hipEvent_t e0, e1;
   CHECK(hipEventCreate(&e0));
   CHECK(hipEventCreate(&e1));
-  hipLaunchKernelGGL(ub_kernel<T>, dim3(grid), dim3(64), 0, 0, lanes, iters, d_cyc, tab, sink);
+  hipLaunchKernelGGL(ub_kernel<T>, dim3(grid), dim3(64), 0, 0, lanes, iters, d_cyc, tab, sink,
+                     (WaveRec*)nullptr);
   CHECK(hipDeviceSynchronize());
   double best = 1e30;
   std::vector<uint64_t> c(grid), keep;
   for (int r = 0; r < 3; ++r) {
     CHECK(hipEventRecord(e0, 0));
-    hipLaunchKernelGGL(ub_kernel<T>, dim3(grid), dim3(64), 0, 0, lanes, iters, d_cyc, tab, sink);
+    hipLaunchKernelGGL(ub_kernel<T>, dim3(grid), dim3(64), 0, 0, lanes, iters, d_cyc, tab, sink,
+                       (WaveRec*)nullptr);
     CHECK(hipEventRecord(e1, 0));
     CHECK(hipEventSynchronize(e1));
     float ms = 0;
@@ -191,7 +212,64 @@ static void test(const char* name, int cus, int W, uint32_t lanes, uint32_t iter
   fflush(stdout);
 }
 
-int main() {
+// Occupancy check: one launch of test T with per-wave records; reports the
+// shader clock (memtime cycles over the 100 MHz realtime span) and how many
+// waves shared a SIMD at once (the maximum over SIMDs of overlapping
+// [r0, r1) spans), i.e. whether W waves per SIMD were really co-resident.
+template <int T>
+static void occupancy(const char* name, int cus, int W, uint32_t lanes, uint32_t iters,
+                      uint16_t* tab, uint32_t* sink, uint64_t* cyc) {
+  const int grid = cus * 4 * W;
+  WaveRec* d_rec;
+  CHECK(hipMalloc(&d_rec, size_t(grid) * sizeof(WaveRec)));
+  hipLaunchKernelGGL(ub_kernel<T>, dim3(grid), dim3(64), 0, 0, lanes, iters, cyc, tab, sink, d_rec);
+  CHECK(hipDeviceSynchronize());
+  std::vector<WaveRec> r(grid);
+  CHECK(hipMemcpy(r.data(), d_rec, grid * sizeof(WaveRec), hipMemcpyDeviceToHost));
+  CHECK(hipFree(d_rec));
+  std::vector<double> clk;
+  uint64_t rmin = ~0ull, rmax = 0;
+  for (const WaveRec& w : r) {
+    if (w.r1 > w.r0) clk.push_back(double(w.t1 - w.t0) / (double(w.r1 - w.r0) / 100e6));
+    rmin = std::min(rmin, w.r0);
+    rmax = std::max(rmax, w.r1);
+  }
+  std::sort(clk.begin(), clk.end());
+  // SIMD key: XCC, SE, SH, CU, SIMD fields of HW_ID (gfx9 layout)
+  std::vector<std::pair<uint64_t, int>> ev;  // (time, +1/-1) per SIMD key
+  std::vector<std::pair<uint32_t, std::pair<uint64_t, int>>> evk;
+  for (const WaveRec& w : r) {
+    const uint32_t key = ((w.xcc_id & 0xF) << 16) | (((w.hw_id >> 13) & 7) << 12) |
+                         (((w.hw_id >> 12) & 1) << 11) | (((w.hw_id >> 8) & 0xF) << 4) |
+                         ((w.hw_id >> 4) & 3);
+    evk.push_back({key, {w.r0, +1}});
+    evk.push_back({key, {w.r1, -1}});
+  }
+  std::sort(evk.begin(), evk.end(), [](const auto& a, const auto& b) {
+    if (a.first != b.first) return a.first < b.first;
+    if (a.second.first != b.second.first) return a.second.first < b.second.first;
+    return a.second.second < b.second.second;  // ends before starts at equal times
+  });
+  int best = 0, cur = 0, simds = 0;
+  uint32_t last = ~0u;
+  for (const auto& e : evk) {
+    if (e.first != last) {
+      last = e.first;
+      cur = 0;
+      ++simds;
+    }
+    cur += e.second.second;
+    best = std::max(best, cur);
+  }
+  printf("{\"occupancy\": \"%s\", \"waves_per_simd\": %d, \"lanes\": %u, \"simds_seen\": %d, "
+         "\"max_coresident_per_simd\": %d, \"clock_ghz_median\": %.3f, \"clock_ghz_min\": %.3f, "
+         "\"span_us\": %.1f}\n",
+         name, W, lanes, simds, best, clk[clk.size() / 2] * 1e-9, clk.front() * 1e-9,
+         double(rmax - rmin) / 100.0);
+  fflush(stdout);
+}
+
+int main(int argc, char** argv) {
   int dev = 0, cus = 0;
   CHECK(hipGetDevice(&dev));
   CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
@@ -205,6 +283,20 @@ int main() {
   CHECK(hipMalloc(&sink, 64));
   CHECK(hipMalloc(&cyc, size_t(cus) * 4 * 8 * 8));
   fprintf(stderr, "CUs %d\n", cus);
+  if (argc > 1 && std::string(argv[1]) == "lanes") {
+    // active lanes per wave: does a wave with one active lane issue slower?
+    for (int W : {1, 2, 4})
+      for (uint32_t lanes : {1u, 2u, 4u, 8u, 16u, 32u}) {
+        test<0>("valu_ilp8", cus, W, lanes, 2000, tab, sink, cyc);
+        test<2>("salu_ilp8", cus, W, lanes, 2000, tab, sink, cyc);
+        test<4>("dec_lds", cus, W, lanes, 200, tab, sink, cyc);
+      }
+    return 0;
+  }
+  for (int W : {1, 2, 4, 8}) {
+    occupancy<0>("valu_ilp8", cus, W, 64, 20000, tab, sink, cyc);
+    occupancy<4>("dec_lds", cus, W, 32, 2000, tab, sink, cyc);
+  }
   for (int W : {1, 2, 4, 8})
     for (uint32_t lanes : {1u, 32u, 64u}) {
       test<0>("valu_ilp8", cus, W, lanes, 2000, tab, sink, cyc);

@@ -58,16 +58,6 @@ void emu_decode_batch_lds(const LzmaGpuStreamDesc* descs, size_t n, const uint8_
       results[i] = lane_decode_lds<LZGPU_LDS_MASK_ALL | kCoopBit | kWinBit>(
           descs[i], src, dst, ws, slab, stride, nullptr, win.data(), EMU_WIN_BYTES);
     }
-#elif defined(EMU_LAT_WIN)
-    // the one-lane latency kernel with its LDS history window (round 5;
-    // deferred output unless -DLZGPU_LANE_DEFER=0)
-    {
-      static std::vector<uint8_t> win(EMU_WIN_BYTES);
-      memset(win.data(), 0x5C, win.size());  // stale LDS contents
-      results[i] = lane_decode_lds<LZGPU_LDS_MASK_LAT | kWinBit>(descs[i], src, dst, ws, slab,
-                                                                 stride, nullptr, win.data(),
-                                                                 EMU_WIN_BYTES);
-    }
 #elif defined(EMU_COOP_ALL)
     // the wave-cooperative kernel with every section in LDS (its default
     // placement where the whole table fits)

@@ -189,9 +189,14 @@ def test_host_edits_between_calls_match_the_reference(L):
         want = E.dic_calls(ref, comp, props, n, 9000, edit)
         got = E.dic_calls(L.lib, comp, props, n, 9000, edit)
         assert got[0] == want[0], (edit, got[0][-3:], want[0][-3:])
-        assert got[1] == want[1], edit
+        # the dictionary up to the final dicPos (after SZ_ERROR_DATA the
+        # reference also leaves the failed pass's bytes beyond dicPos in dic,
+        # LzmaDec.c:366-379 returning before the write-back; the drop-in
+        # returns dic[0, dicPos) -- DESIGN.md §2)
+        end = want[0][-1][3]
+        assert got[1][:end] == want[1][:end], edit
         if edit is None:
-            assert want[1] == data
+            assert want[1] == data and end == n
 
 
 def test_decoder_alternating_devices(L):
