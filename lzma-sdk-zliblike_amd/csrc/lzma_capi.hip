@@ -216,8 +216,7 @@ static LzmaGpuLdsClass plan_lds_class(uint32_t stride, uint64_t count, uint32_t 
   const uint32_t per_cu = std::max<uint32_t>(1, lds_per_cu / (stride * 2));  // streams/CU
   uint32_t occ = 4;
   const uint32_t occ_over = o.waves_per_simd;
-  if (occ_over == 1 || occ_over == 2 || occ_over == 3 || occ_over == 4 || occ_over == 6 ||
-      occ_over == 8)
+  if (occ_over == 1 || occ_over == 2 || occ_over == 4 || occ_over == 6 || occ_over == 8)
     occ = occ_over;
   // Two regimes (profiles/r01_variants v17-v28):
   //  * throughput -- LDS holds >= 64 streams per CU and the batch fills them:

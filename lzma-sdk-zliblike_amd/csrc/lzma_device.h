@@ -56,17 +56,6 @@ constexpr uint32_t kProbOne = 2048u;
 constexpr uint32_t kProbInit = 1024u;
 constexpr uint32_t kLookahead = 20u;  // LZMA_REQUIRED_INPUT_MAX
 constexpr uint32_t kLenDone = 274u;   // kMatchSpecLenStart
-// Cooperative kernels (round 5): the bit trees of a
-// symbol decided from load batches -- the literal tree as two batches of four
-// levels (15 cells each), the matched literal's eight all-match cells at once,
-// the length coder's choice bits and 3-level trees in one batch, the slot tree
-// as two batches of three levels, SpecPos and Align likewise -- instead of one
-// dependent LDS round trip (ds_read -> address) per level: with one wave per
-// SIMD the LDS has bandwidth to spare and the serial chain is the bound.
-// -DLZGPU_COOP_BATCH=0 keeps one level per round trip (A/B).
-#ifndef LZGPU_COOP_BATCH
-#define LZGPU_COOP_BATCH 0
-#endif
 // direct bits decided several per step on the cooperative kernel (direct_coop;
 // -DLZGPU_DIRECT_CHUNKS=0 restores the bit-serial loop for A/B)
 #ifndef LZGPU_DIRECT_CHUNKS
@@ -679,24 +668,11 @@ __host__ __device__ constexpr bool def_on() {
 // everywhere it ran -- 8 LZMA2 blocks per CU 5,146 vs 5,494 MB/s, the windowed
 // config 4 3,100 vs 3,318 MB/s (profiles/r04_coop8/, r04_qserial/) -- and was
 // removed in round 5 with the other rejected shapes.
-// -DLZGPU_COOP_Q=1 (A/B, round 5): every cooperative build takes the
-// checkpoint reader, with the batched trees' decisions unchecked after a top-up.
-#ifndef LZGPU_COOP_Q
-#define LZGPU_COOP_Q 0
-#endif
-// -DLZGPU_NORM_SEL=1 (A/B, round 5): NORMALIZE after a checkpoint as selects
-// (range, code and the reader's window chosen by range < 2^24) instead of a
-// branch -- on the cooperative kernels, where every lane takes the same way
-// and the VALU -> VCC -> EXEC branch sits on the decision chain.
-#ifndef LZGPU_NORM_SEL
-#define LZGPU_NORM_SEL 0
-#endif
 template <uint32_t M>
 struct BulkReaderFor {
   static constexpr uint32_t m = M & ~kIlvBit;
   static constexpr bool q = m == LZGPU_LDS_MASK || m == (LZGPU_LDS_MASK_LAT | kCoopBit) ||
-                            m == (LZGPU_LDS_MASK_ALL | kCoopBit) ||
-                            (LZGPU_COOP_Q != 0 && (m & kCoopBit) != 0u);
+                            m == (LZGPU_LDS_MASK_ALL | kCoopBit);
   typedef typename std::conditional<q, GlobalReaderQ, PlainReader>::type type;
 };
 
@@ -709,11 +685,6 @@ struct BulkReaderFor {
 template <uint32_t M>
 __host__ __device__ constexpr bool mb_pf_on() {
   return ((M & kCoopBit) != 0u) || ((M & ~kIlvBit) == LZGPU_LDS_MASK);
-}
-// batched bit trees on the cooperative kernels (LZGPU_COOP_BATCH)
-template <uint32_t M>
-__host__ __device__ constexpr bool coop_batch() {
-  return LZGPU_COOP_BATCH != 0 && (M & kCoopBit) != 0u;
 }
 
 // checkpoint hooks for readers without them: every NORMALIZE checks
@@ -755,14 +726,7 @@ struct Rc {
   }
   // NORMALIZE after a reader checkpoint: the byte is known to be in the window
   __device__ __forceinline__ void norm_u() {
-    if constexpr (LZGPU_NORM_SEL != 0 && kIsQ<Rd>) {
-      const bool n = range < kTop;
-      const uint32_t b = rd->peek();
-      code = n ? ((code << 8) | b) : code;
-      range = n ? (range << 8) : range;
-      rd->win = n ? (rd->win >> 8) : rd->win;
-      rd->nb -= n ? 1u : 0u;
-    } else if (range < kTop) {
+    if (range < kTop) {
       range <<= 8;
       code = (code << 8) | rd_take_u(*rd);
     }
@@ -868,11 +832,9 @@ struct Rc {
   // 16 * root + (the four bits, MSB first).  The candidates of the levels
   // below are halved by each decided bit (independent selects), so a level's
   // probability is one select behind its parent's decision.
-  // U: the decisions take their input bytes unchecked (norm_u), after a
-  // checkpoint reader's top-up (>= 5 bytes held)
-  template <bool U = false, class P>
+  template <class P>
   __device__ __forceinline__ uint32_t sub4(P probs, uint32_t root) {
-    auto dec = [&](uint32_t p, P cell) { return U ? bit_vu(p, cell) : bit_v(p, cell); };
+    auto dec = [&](uint32_t p, P cell) { return bit_v(p, cell); };
     const uint32_t r2 = root * 2, r4 = root * 4, r8 = root * 8;
     const uint32_t c1 = probs[root];
     uint32_t c2[2], c4[4], c8[8];
@@ -1307,23 +1269,14 @@ __device__ __forceinline__ void lz_literal(Rc<Rd>& rc, const Tab<M, Lo>& T, uint
   if (st < 7) {
     st = (st < 4) ? 0 : st - 3;
     auto lp = T.template at<S_LITP>(ctx << 8);
-    if constexpr (coop_batch<M>() && kIsQ<Rd>) {
-      rd_topup(*rc.rd);
-      const uint32_t m = rc.template sub4<true>(lp, 1);
-      rd_topup(*rc.rd);
-      sym = rc.template sub4<true>(lp, m);
-    } else if constexpr (coop_batch<M>()) {
-      sym = rc.sub4(lp, rc.sub4(lp, 1));
-    } else {
-      const uint32_t m = rc.template tree_u<4>(lp, 1);
-      rd_topup(*rc.rd);
-      sym = rc.template tree_u<4>(lp, m);
-    }
+    const uint32_t m = rc.template tree_u<4>(lp, 1);
+    rd_topup(*rc.rd);
+    sym = rc.template tree_u<4>(lp, m);
   } else {
     uint32_t mbyte = mb_pf_on<M>() ? mb_pf : uint32_t(dic[ring_back(pos, r0, cap)]);
     st = (st < 10) ? st - 3 : st - 6;
     constexpr bool p_lds = ((M >> S_LITP) & 1u) != 0u, m_lds = ((M >> S_LITM) & 1u) != 0u;
-    if constexpr ((p_lds && !m_lds) || coop_batch<M>()) {
+    if constexpr (p_lds && !m_lds) {
       // While the decoded bits equal the match byte's, the cell of bit k is
       // fixed by the match byte alone (offs stays 0x100, symbol = its top k
       // bits under a leading 1): load all eight matched-tree cells at once
@@ -1574,7 +1527,7 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
       auto lbase = [&]() {
         if constexpr (len_lds) return T.lo + lsec_o; else return T.g(lsec_o);
       }();
-      if constexpr (!len_lds || coop_batch<M>()) {
+      if constexpr (!len_lds) {
         // global length coder: the choice bits and the low tree load together,
         // the mid tree only behind choice = 1
         if constexpr ((M & ~kIlvBit) != LZGPU_LDS_MASK) {
@@ -1619,7 +1572,7 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
     if (st >= 12) {
       const uint32_t lstate = len < 4 ? len : 3;
       uint32_t dist;
-      if constexpr (((M >> S_SLOT) & 1u) == 0u || coop_batch<M>()) {
+      if constexpr (((M >> S_SLOT) & 1u) == 0u) {
         auto sl_t = T.template at<S_SLOT>(lstate << 6);
 #if LZGPU_PROF == 1 && !defined(LZGPU_HOST_EMU)
         // one global round trip + 3 decisions, timed (profiling builds)
@@ -1653,7 +1606,7 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
           dist <<= nbits;
           uint32_t mask = 1, node = 1;
           const uint32_t sp = dist - slot - 1;
-          if constexpr (((M >> S_SPEC) & 1u) == 0u || coop_batch<M>()) {
+          if constexpr (((M >> S_SPEC) & 1u) == 0u) {
             if (nbits >= 3) {
               // first three reverse-tree bits in one load batch
               node = rc.sub3(T.template at<S_SPEC>(sp), 1);
@@ -1690,7 +1643,7 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
 #endif
           dist <<= 4;
           uint32_t node = 1;
-          if constexpr (((M >> S_ALIGN) & 1u) == 0u || coop_batch<M>()) {
+          if constexpr (((M >> S_ALIGN) & 1u) == 0u) {
             if constexpr ((M & ~kIlvBit) != LZGPU_LDS_MASK) {
               // all four reverse bits from one batch of the 15 cells
               node = rc.sub4(T.template at<S_ALIGN>(0), 1);

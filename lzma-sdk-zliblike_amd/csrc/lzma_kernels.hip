@@ -375,12 +375,6 @@ static int launch_lds_w(const LzmaGpuStreamDesc* d_descs, const uint32_t* d_orde
   if (waves_per_simd == 2)
     return launch_lds<2, M, K2>(d_descs, d_order, n, d_src, d_dst, d_ws, d_results, lanes, stride,
                                 groups_per_cu, max_groups, d_queue, sl, stream);
-#if LZGPU_W3
-  // three waves per SIMD (A/B builds only: -DLZGPU_W3=1)
-  if (waves_per_simd == 3)
-    return launch_lds<3, M, K2>(d_descs, d_order, n, d_src, d_dst, d_ws, d_results, lanes, stride,
-                                groups_per_cu, max_groups, d_queue, sl, stream);
-#endif
   return launch_lds<4, M, K2>(d_descs, d_order, n, d_src, d_dst, d_ws, d_results, lanes, stride,
                               groups_per_cu, max_groups, d_queue, sl, stream);
 }

@@ -45,15 +45,6 @@ EMU_VARIANTS = {
     "coop_window_64k": "-DEMU_COOP_ALL_WIN -DEMU_WIN_BYTES=65536",
     "session_coop_window_4k": "-DEMU_SESS_COOP_WIN -DEMU_WIN_BYTES=4096",
     "session_coop_window_64k": "-DEMU_SESS_COOP_WIN -DEMU_WIN_BYTES=65536",
-    # round 5: batched bit trees on the cooperative kernels (LZGPU_COOP_BATCH)
-    "coop_batch_all_lds": "-DEMU_COOP_ALL -DLZGPU_COOP_BATCH=1",
-    "coop_batch_latency_placement": "-DEMU_COOP -DLZGPU_COOP_BATCH=1",
-    "coop_batch_window_4k": "-DEMU_COOP_ALL_WIN -DEMU_WIN_BYTES=4096 -DLZGPU_COOP_BATCH=1",
-    "session_coop_batch_window_4k": "-DEMU_SESS_COOP_WIN -DEMU_WIN_BYTES=4096 -DLZGPU_COOP_BATCH=1",
-    "coop_batch_q_window_4k": "-DEMU_COOP_ALL_WIN -DEMU_WIN_BYTES=4096 -DLZGPU_COOP_BATCH=1 -DLZGPU_COOP_Q=1",
-    "coop_batch_qsel_window_4k": "-DEMU_COOP_ALL_WIN -DEMU_WIN_BYTES=4096 -DLZGPU_COOP_BATCH=1 -DLZGPU_COOP_Q=1 -DLZGPU_NORM_SEL=1",
-    "coop_qsel_all_lds": "-DEMU_COOP_ALL -DLZGPU_COOP_Q=1 -DLZGPU_NORM_SEL=1",
-    "session_coop_batch_qsel_window_4k": "-DEMU_SESS_COOP_WIN -DEMU_WIN_BYTES=4096 -DLZGPU_COOP_BATCH=1 -DLZGPU_COOP_Q=1 -DLZGPU_NORM_SEL=1",
 }
 
 
