@@ -294,7 +294,14 @@ def plan_kernels(plan):
     for c in list(plan.classes)[:int(plan.n_classes)]:
         if int(c.n) == 0:
             continue
-        k = "lzgpu_decode_coop_kernel" if int(c.lds_mask) & 0x80000000 else "lzgpu_decode_lds_kernel"
+        m = int(c.lds_mask)
+        dup = int(os.environ.get("LZGPU_DUP", "32") or 0)  # lzma_kernels.hip kLaneDup
+        if m & 0x80000000:
+            k = "lzgpu_decode_coop_kernel"
+        elif m == 0x1BF and int(c.lanes_per_group) == 1 and 1 < dup <= 64:
+            k = "lzgpu_decode_dup_kernel"  # one-stream waves on all 32 lanes
+        else:
+            k = "lzgpu_decode_lds_kernel"
         if k not in names:
             names.append(k)
     if int(plan.n) > int(plan.n_lds):

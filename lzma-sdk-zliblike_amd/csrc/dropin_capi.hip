@@ -95,10 +95,11 @@ struct ScratchLease {
 //
 // One-call decodes (LzmaDecode, LzmaUncompress, Lzma2Decode) made by several
 // host threads at once share launches -- group commit: a call joins its
-// device's pending list; if no batch is running on that device it takes the
-// whole list and runs it as ONE batch (inputs packed into pinned staging, one
-// upload, one plan + launch, one download of results and outputs), otherwise it
-// waits, and the calls that arrive while a batch runs form the next one.  An
+// device's pending list; if one of the device's batch sets is free it takes
+// the whole list and runs it as ONE batch (inputs packed into pinned staging,
+// one upload, one plan + launch, one download of results and outputs),
+// otherwise it waits, and the calls that arrive while the sets are busy form
+// the next batch.  An
 // unchanged multi-threaded caller (the reference's LzmaDecode / LzmaUncompress
 // are reentrant, LzmaDec.c:972-1002, LzmaLib.c:41-46) therefore reaches the
 // batch planner and its throughput / latency kernels; a lone caller pays
@@ -117,19 +118,41 @@ struct OneCall {
   LzmaGpuResult r = {};
   SRes err = SZ_OK;       // infrastructure failure of the batch (else r.res)
   const char* msg = "";   // its message (static text)
+  bool taken = false;     // in a batch (running or done)
   bool done = false;
 };
+
+// The resources of one batch in flight: pinned staging (inputs | descriptors +
+// order | results | outputs), device buffers and a stream of its own.
+struct BatchSet {
+  uint8_t* pin = nullptr;
+  size_t pin_cap = 0;
+  DevBuf io, ws, meta;
+  hipStream_t stream = nullptr;
+  bool busy = false;
+};
+
+// Batches in flight per device at once (LZGPU_COALESCE_INFLIGHT=1..8, default
+// 4: GPU_MAX_HW_QUEUES is 4).  A lone 4 KiB call is one wave's serial decode
+// (2.3 ms of its 2.4, profiles/r05_coalesce/), so with one batch at a time the
+// callers that arrive during it all wait for it to end; with several sets the
+// next leader launches at once and the batches share the chip (a one-wave
+// batch leaves the rest of every CU idle).
+constexpr int kMaxInFlight = 8;
+int in_flight_limit() {
+  static const int n = [] {
+    const char* e = getenv("LZGPU_COALESCE_INFLIGHT");
+    const int v = e ? atoi(e) : 4;
+    return v < 1 ? 1 : (v > kMaxInFlight ? kMaxInFlight : v);
+  }();
+  return n;
+}
 
 struct Coalescer {
   std::mutex mu;
   std::condition_variable cv;
   std::vector<OneCall*> pending;
-  bool running = false;
-  // the running leader's resources
-  uint8_t* pin = nullptr;  // pinned staging: inputs | descriptors + order | results
-  size_t pin_cap = 0;
-  DevBuf io, ws, meta;
-  hipStream_t stream = nullptr;
+  BatchSet sets[kMaxInFlight];
   std::atomic<uint64_t> batches{0}, items{0}, max_items{0};
 };
 
@@ -179,8 +202,14 @@ struct PhaseClock {
   }
 };
 
+// Outputs of a batch up to this many bytes of capacity come back in one
+// transfer into the pinned staging and are copied to the callers' buffers on
+// the host; a larger batch downloads each call's decoded bytes on its own
+// (one pageable transfer per call: ~7 us each, 1.9 ms of a 255-call batch).
+constexpr size_t kBulkOutMax = size_t(64) << 20;
+
 // One batch of calls on the current device (the leader, C.mu not held).
-void run_batch(Coalescer& C, const std::vector<OneCall*>& b) {
+void run_batch(BatchSet& C, const std::vector<OneCall*>& b) {
   PhaseClock pc;
   const size_t k = b.size();
   auto fail_all = [&](SRes e, const char* what) {
@@ -219,8 +248,9 @@ void run_batch(Coalescer& C, const std::vector<OneCall*>& b) {
   }
   pc.mark(kTPlan);
   const size_t meta_bytes = align16(k * sizeof(LzmaGpuStreamDesc)) + align16(k * sizeof(uint32_t));
-  const size_t res_bytes = k * sizeof(LzmaGpuResult);
-  const size_t pin_need = in_total + meta_bytes + res_bytes + 64;
+  const size_t res_bytes = align16(k * sizeof(LzmaGpuResult));
+  const bool bulk_out = out_total <= kBulkOutMax;
+  const size_t pin_need = in_total + meta_bytes + res_bytes + (bulk_out ? out_total : 0) + 64;
   if (C.pin_cap < pin_need) {
     // grow geometrically: a run of slightly larger batches reallocates (and
     // synchronises the device, hipHostFree / hipHostMalloc) O(log) times
@@ -260,11 +290,15 @@ void run_batch(Coalescer& C, const std::vector<OneCall*>& b) {
     return fail_all(SZ_ERROR_FAIL, "LzmaDecode: batch launch failed");
   }
   pc.mark(kTLaunch);
+  // results (and, for a bulk batch, every output) in one synchronisation
+  uint8_t* pin_out = reinterpret_cast<uint8_t*>(pin_res) + align16(res_bytes);
   if (xfer(pin_res, d_res, res_bytes, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      (bulk_out && out_total &&
+       xfer(pin_out, d_io + in_total, out_total, hipMemcpyDeviceToHost, st) != hipSuccess) ||
       hipStreamSynchronize(st) != hipSuccess)
     return fail_all(SZ_ERROR_FAIL, "LzmaDecode: decode kernel failed");
   pc.mark(kTWait);
-  // outputs: straight into each caller's buffer (only the bytes decoded)
+  // outputs: only the bytes decoded, into each caller's buffer
   for (size_t i = 0; i < k; ++i) {
     OneCall& c = *b[i];
     c.r = pin_res[i];
@@ -273,14 +307,17 @@ void run_batch(Coalescer& C, const std::vector<OneCall*>& b) {
       c.msg = "LzmaDecode: kernel reported more output than its capacity";
       continue;
     }
-    if (c.r.dest_len &&
-        xfer(c.dest, d_io + in_total + d[i].dst_off, c.r.dest_len, hipMemcpyDeviceToHost, st) !=
-            hipSuccess) {
+    if (!c.r.dest_len) continue;
+    if (bulk_out) {
+      memcpy(c.dest, pin_out + d[i].dst_off, size_t(c.r.dest_len));
+    } else if (xfer(c.dest, d_io + in_total + d[i].dst_off, c.r.dest_len,
+                    hipMemcpyDeviceToHost, st) != hipSuccess) {
       c.err = SZ_ERROR_FAIL;
       c.msg = "LzmaDecode: download output failed";
     }
   }
-  if (hipStreamSynchronize(st) != hipSuccess) fail_all(SZ_ERROR_FAIL, "LzmaDecode: download output");
+  if (!bulk_out && hipStreamSynchronize(st) != hipSuccess)
+    fail_all(SZ_ERROR_FAIL, "LzmaDecode: download output");
   pc.mark(kTDownload);
 }
 
@@ -293,7 +330,7 @@ constexpr size_t kCoalesceItemMax = size_t(256) << 20;
 // batch of several calls that fails as a whole (an allocation, upload or
 // launch of the batch) is retried call by call, so a call fails only when it
 // would have failed alone.
-void run_calls(Coalescer& C, const std::vector<OneCall*>& batch) {
+void run_calls(BatchSet& C, const std::vector<OneCall*>& batch) {
   std::vector<OneCall*> small;
   std::vector<std::vector<OneCall*>> runs;
   for (OneCall* c : batch) {
@@ -325,21 +362,28 @@ void coalesced(OneCall& me, int dev) {
   }
   Coalescer& C = *Cp;
   std::unique_lock<std::mutex> lk(C.mu);
-  if (!C.stream && hipStreamCreateWithFlags(&C.stream, hipStreamNonBlocking) != hipSuccess) {
-    (void)hipGetLastError();
-    C.stream = nullptr;
-    me.err = SZ_ERROR_FAIL;
-    me.msg = "LzmaDecode: stream creation failed";
-    return;
-  }
   C.pending.push_back(&me);
   while (!me.done) {
-    if (C.running) {
+    // lead when this call is still pending and a batch set is free
+    BatchSet* R = nullptr;
+    if (!me.taken)
+      for (int i = 0; i < in_flight_limit() && !R; ++i)
+        if (!C.sets[i].busy) R = &C.sets[i];
+    if (!R) {
       C.cv.wait(lk);
       continue;
     }
-    // lead: take everything pending (this call included) as one batch
-    C.running = true;
+    if (!R->stream && hipStreamCreateWithFlags(&R->stream, hipStreamNonBlocking) != hipSuccess) {
+      (void)hipGetLastError();
+      R->stream = nullptr;
+      C.pending.erase(std::find(C.pending.begin(), C.pending.end(), &me));
+      me.err = SZ_ERROR_FAIL;
+      me.msg = "LzmaDecode: stream creation failed";
+      me.taken = me.done = true;
+      return;
+    }
+    // take everything pending (this call included) as one batch
+    R->busy = true;
     std::vector<OneCall*> batch;
     batch.swap(C.pending);
     if (!coalesce_on() && batch.size() > 1) {  // one launch per call: this one now
@@ -347,9 +391,10 @@ void coalesced(OneCall& me, int dev) {
         if (c != &me) C.pending.push_back(c);
       batch.assign(1, &me);
     }
+    for (OneCall* c : batch) c->taken = true;
     lk.unlock();
     try {
-      run_calls(C, batch);
+      run_calls(*R, batch);
     } catch (const std::exception&) {
       for (OneCall* c : batch) {
         c->err = SZ_ERROR_MEM;
@@ -363,7 +408,7 @@ void coalesced(OneCall& me, int dev) {
     }
     lk.lock();
     for (OneCall* c : batch) c->done = true;
-    C.running = false;
+    R->busy = false;
     C.cv.notify_all();
   }
 }
@@ -535,24 +580,31 @@ void mirror_drop(const CLzmaDec* p) {
 // by several host threads at once, each on its own decoder, share launches the
 // same way one-call decodes do: each call prepares its mirror (uploads its
 // input, table and history on its own stream) and hands the device session
-// state to its device's session queue; the call that finds no launch running
-// takes the whole queue as ONE launch of the session kernels (one 32-lane wave
-// per decoder) and every caller then downloads its own table and bytes.
+// state to its device's session queue; a call that finds a free session set
+// (up to in_flight_limit() launches at once) takes the whole queue as ONE
+// launch of the session kernels (one 32-lane wave per decoder) and every
+// caller then downloads its own table and bytes.
 struct SessCall {
   LzgpuSession q;  // in: the call; out: the state after it
   uint32_t cells = 0;
   int err = 0;     // launch failure
+  bool taken = false;  // in a launch (running or done)
   bool done = false;
+};
+
+// One session launch in flight: its LzgpuSession array, host copy and stream.
+struct SessSet {
+  DevBuf arr;                   // the batch's LzgpuSession array
+  std::vector<LzgpuSession> h;  // its host copy
+  hipStream_t stream = nullptr;
+  bool busy = false;
 };
 
 struct SessCoalescer {
   std::mutex mu;
   std::condition_variable cv;
   std::vector<SessCall*> pending;
-  bool running = false;
-  DevBuf arr;                  // the batch's LzgpuSession array
-  std::vector<LzgpuSession> h;  // its host copy
-  hipStream_t stream = nullptr;
+  SessSet sets[kMaxInFlight];  // up to in_flight_limit() launches at once
   std::atomic<uint64_t> batches{0}, items{0}, max_items{0};
 };
 
@@ -568,7 +620,7 @@ SessCoalescer* sess_coalescer(int dev) {
 // One launch for a batch of session calls (the leader, C.mu not held):
 // wave-cooperative sessions in one launch, tables wider than 64 KiB on the
 // one-lane global session kernel.
-void run_sess_batch(SessCoalescer& C, const std::vector<SessCall*>& b) {
+void run_sess_batch(SessSet& C, const std::vector<SessCall*>& b) {
   const size_t k = b.size();
   std::vector<size_t> coop, glob;
   uint32_t lds_cells = 0;
@@ -614,19 +666,25 @@ void sess_coalesced(SessCall& me, int dev) {
   }
   SessCoalescer& C = *Cp;
   std::unique_lock<std::mutex> lk(C.mu);
-  if (!C.stream && hipStreamCreateWithFlags(&C.stream, hipStreamNonBlocking) != hipSuccess) {
-    (void)hipGetLastError();
-    C.stream = nullptr;
-    me.err = 1;
-    return;
-  }
   C.pending.push_back(&me);
   while (!me.done) {
-    if (C.running) {
+    SessSet* R = nullptr;
+    if (!me.taken)
+      for (int i = 0; i < in_flight_limit() && !R; ++i)
+        if (!C.sets[i].busy) R = &C.sets[i];
+    if (!R) {
       C.cv.wait(lk);
       continue;
     }
-    C.running = true;
+    if (!R->stream && hipStreamCreateWithFlags(&R->stream, hipStreamNonBlocking) != hipSuccess) {
+      (void)hipGetLastError();
+      R->stream = nullptr;
+      C.pending.erase(std::find(C.pending.begin(), C.pending.end(), &me));
+      me.err = 1;
+      me.taken = me.done = true;
+      return;
+    }
+    R->busy = true;
     std::vector<SessCall*> batch;
     batch.swap(C.pending);
     if (!coalesce_on() && batch.size() > 1) {
@@ -634,9 +692,10 @@ void sess_coalesced(SessCall& me, int dev) {
         if (c != &me) C.pending.push_back(c);
       batch.assign(1, &me);
     }
+    for (SessCall* c : batch) c->taken = true;
     lk.unlock();
     try {
-      run_sess_batch(C, batch);
+      run_sess_batch(*R, batch);
     } catch (const std::exception&) {
       for (SessCall* c : batch) c->err = 1;
     }
@@ -647,7 +706,7 @@ void sess_coalesced(SessCall& me, int dev) {
     }
     lk.lock();
     for (SessCall* c : batch) c->done = true;
-    C.running = false;
+    R->busy = false;
     C.cv.notify_all();
   }
 }
@@ -784,24 +843,23 @@ SRes gpu_session_call(CLzmaDec* p, int mode, SizeT dicLimit, const Byte* src, Si
     set_error("LzmaDec: host allocation failed");
     return SZ_ERROR_MEM;
   }
-  if (xfer(back.data() + kSessBytes, d_probs, size_t(cells) * 2, hipMemcpyDeviceToHost, st) !=
-          hipSuccess ||
-      hipStreamSynchronize(st) != hipSuccess)
-    return fail("LzmaDec: download probs");
-  // the decoded bytes: DecodeToDic's new dictionary bytes, DecodeToBuf's output
+  // the table and the decoded bytes (DecodeToDic's new dictionary bytes,
+  // DecodeToBuf's output) in one synchronisation
   if (mode == 0) {
     if (q.dic_pos < pos0 || q.dic_pos > p->dicBufSize) return fail("LzmaDec: bad session state");
-    if (q.dic_pos > pos0 &&
-        (xfer(p->dic + pos0, d_dic + pos0, q.dic_pos - pos0, hipMemcpyDeviceToHost, st) !=
-             hipSuccess ||
-         hipStreamSynchronize(st) != hipSuccess))
-      return fail("LzmaDec: download dictionary");
-  } else {
-    if (q.out_len > out_room || q.dic_pos > p->dicBufSize) return fail("LzmaDec: bad session state");
-    if (q.out_len &&
-        (xfer(dest, d_io + in_pad, q.out_len, hipMemcpyDeviceToHost, st) != hipSuccess ||
-         hipStreamSynchronize(st) != hipSuccess))
-      return fail("LzmaDec: download output");
+  } else if (q.out_len > out_room || q.dic_pos > p->dicBufSize) {
+    return fail("LzmaDec: bad session state");
+  }
+  if (xfer(back.data() + kSessBytes, d_probs, size_t(cells) * 2, hipMemcpyDeviceToHost, st) !=
+          hipSuccess ||
+      (mode == 0 && q.dic_pos > pos0 &&
+       xfer(p->dic + pos0, d_dic + pos0, q.dic_pos - pos0, hipMemcpyDeviceToHost, st) !=
+           hipSuccess) ||
+      (mode == 1 && q.out_len &&
+       xfer(dest, d_io + in_pad, q.out_len, hipMemcpyDeviceToHost, st) != hipSuccess) ||
+      hipStreamSynchronize(st) != hipSuccess)
+    return fail("LzmaDec: download probs / decoded bytes");
+  if (mode == 1) {
     // the host ring gets the same bytes the device ring got (LzmaDec.c:849-866:
     // each pass writes from dicPos, wrapping to 0 at dicBufSize)
     SizeT pos = pos0, left = q.out_len;

@@ -3,7 +3,7 @@
 # rocprofv3 kernel trace of one- and 16-caller LzmaDecode runs.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
-O=gpurun_out/r05_run3
+O=${RUN3_OUT:-gpurun_out/r05_run3}
 mkdir -p $O
 sha256sum lzma-sdk-zliblike_amd/lib/liblzmagpu.so > $O/binary.sha256
 timeout -k 10 600 python -u bench.py --config coalesce > $O/coalesce.json 2> $O/coalesce.err

@@ -20,4 +20,4 @@ plain, comp, lens, props = bench.build_workload("cfg3", 0, count, 8)
 offs = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
 comps = [comp[offs[i]:offs[i + 1]].tobytes() for i in range(count)]
 f = TC.write_stream_set(d, comps, [props] * count, [4096] * count)
-print(" ".join(f[k] for k in ("src", "lens", "props", "outs")))
+print(" ".join(os.path.abspath(f[k]) for k in ("src", "lens", "props", "outs")))
