@@ -120,6 +120,7 @@ struct OneCall {
   const char* msg = "";   // its message (static text)
   bool taken = false;     // in a batch (running or done)
   bool done = false;
+  std::condition_variable cv;  // its caller sleeps here (group_commit)
 };
 
 // The resources of one batch in flight: pinned staging (inputs | descriptors +
@@ -150,11 +151,91 @@ int in_flight_limit() {
 
 struct Coalescer {
   std::mutex mu;
-  std::condition_variable cv;
   std::vector<OneCall*> pending;
   BatchSet sets[kMaxInFlight];
+  uint32_t in_flight = 0;  // calls in running batches
   std::atomic<uint64_t> batches{0}, items{0}, max_items{0};
 };
+
+// Group commit, shared by the one-call and the session coalescers (C: mu,
+// pending, sets[], in_flight and the counters; Call: taken, done, cv).  A
+// pending call leads when a batch set is free and no batch runs, or the
+// running ones hold fewer than budget / 2 calls (budget: one call per CU; a
+// lone call's stream is one wave, so small batches leave the chip idle and
+// run side by side, while a large one already fills it); it takes the
+// pending calls in arrival order, up to budget minus those in flight, runs them
+// (run(set, batch)) and marks them done.  Every caller sleeps on its own
+// condition variable: a finished batch wakes its own callers and, when calls
+// are pending, the oldest one to lead next -- not all the threads (256
+// callers on 16 host cores: the wake-up storm alone cost milliseconds per
+// batch).
+bool coalesce_on();
+
+template <class Set, class Coal>
+Set* free_set(Coal& C, uint32_t budget) {
+  // a second batch only while the running ones fill less than half the
+  // budget: 256 callers ran 124 MB/s one batch at a time and 86 MB/s with
+  // concurrent batches (each a fraction of the callers), 16 callers 12.9 vs
+  // 17.2 MB/s the other way round (profiles/r05_coalesce/)
+  if (C.in_flight != 0 && C.in_flight >= budget / 2) return nullptr;
+  for (int i = 0; i < in_flight_limit(); ++i)
+    if (!C.sets[i].busy) return &C.sets[i];
+  return nullptr;
+}
+template <class Coal, class Set>
+void wake_next(Coal& C, uint32_t budget) {
+  if (!C.pending.empty() && free_set<Set>(C, budget))
+    C.pending.front()->cv.notify_one();
+}
+template <class Coal, class Set, class Call, class Run, class Fail>
+void group_commit(Coal& C, Call& me, uint32_t budget, Run run, Fail stream_failed) {
+  std::unique_lock<std::mutex> lk(C.mu);
+  C.pending.push_back(&me);
+  while (!me.done) {
+    Set* R = me.taken ? nullptr : free_set<Set>(C, budget);
+    if (!R) {
+      me.cv.wait(lk);
+      continue;
+    }
+    if (!R->stream && hipStreamCreateWithFlags(&R->stream, hipStreamNonBlocking) != hipSuccess) {
+      (void)hipGetLastError();
+      R->stream = nullptr;
+      C.pending.erase(std::find(C.pending.begin(), C.pending.end(), &me));
+      stream_failed(me);
+      me.taken = me.done = true;
+      return;
+    }
+    std::vector<Call*> batch;
+    if (!coalesce_on()) {  // one launch per call: this one now
+      C.pending.erase(std::find(C.pending.begin(), C.pending.end(), &me));
+      batch.assign(1, &me);
+    } else {
+      const size_t room = budget > C.in_flight ? budget - C.in_flight : 1;
+      const size_t take = std::min(C.pending.size(), room);
+      batch.assign(C.pending.begin(), C.pending.begin() + take);
+      C.pending.erase(C.pending.begin(), C.pending.begin() + take);
+    }
+    for (Call* c : batch) c->taken = true;
+    R->busy = true;
+    C.in_flight += uint32_t(batch.size());
+    wake_next<Coal, Set>(C, budget);  // more pending and room: a concurrent batch
+    lk.unlock();
+    run(*R, batch);
+    C.batches++;
+    C.items += batch.size();
+    uint64_t mx = C.max_items.load();
+    while (batch.size() > mx && !C.max_items.compare_exchange_weak(mx, batch.size())) {
+    }
+    lk.lock();
+    for (Call* c : batch) {
+      c->done = true;
+      if (c != &me) c->cv.notify_one();
+    }
+    R->busy = false;
+    C.in_flight -= uint32_t(batch.size());
+    wake_next<Coal, Set>(C, budget);
+  }
+}
 
 std::atomic<Coalescer*> g_coal[kLzgpuMaxDevices];
 Coalescer* coalescer(int dev) {
@@ -207,6 +288,10 @@ struct PhaseClock {
 // the host; a larger batch downloads each call's decoded bytes on its own
 // (one pageable transfer per call: ~7 us each, 1.9 ms of a 255-call batch).
 constexpr size_t kBulkOutMax = size_t(64) << 20;
+// First allocation of a batch set's pinned staging and device I/O buffer (the
+// workspace and metadata take a quarter): 256 coalesced 4 KiB calls need
+// ~1.6 MB, so steady traffic never regrows them.
+constexpr size_t kSetFloor = size_t(4) << 20;
 
 // One batch of calls on the current device (the leader, C.mu not held).
 void run_batch(BatchSet& C, const std::vector<OneCall*>& b) {
@@ -252,9 +337,10 @@ void run_batch(BatchSet& C, const std::vector<OneCall*>& b) {
   const bool bulk_out = out_total <= kBulkOutMax;
   const size_t pin_need = in_total + meta_bytes + res_bytes + (bulk_out ? out_total : 0) + 64;
   if (C.pin_cap < pin_need) {
-    // grow geometrically: a run of slightly larger batches reallocates (and
-    // synchronises the device, hipHostFree / hipHostMalloc) O(log) times
-    const size_t want = std::max(pin_need, C.pin_cap * 2);
+    // grow geometrically from 4 MiB: a run of slightly larger batches
+    // reallocates (and synchronises the device, hipHostFree / hipHostMalloc,
+    // stalling the other sets' batches) O(log) times
+    const size_t want = std::max({pin_need, C.pin_cap * 2, kSetFloor});
     if (C.pin) (void)hipHostFree(C.pin);
     C.pin = nullptr;
     C.pin_cap = 0;
@@ -265,9 +351,9 @@ void run_batch(BatchSet& C, const std::vector<OneCall*>& b) {
     }
     C.pin_cap = want;
   }
-  uint8_t* d_io = static_cast<uint8_t*>(C.io.get(in_total + out_total + 16));
-  void* d_ws = C.ws.get(size_t(plan.workspace_bytes));
-  uint8_t* d_meta = static_cast<uint8_t*>(C.meta.get(meta_bytes + res_bytes + 16));
+  uint8_t* d_io = static_cast<uint8_t*>(C.io.get(std::max(in_total + out_total + 16, kSetFloor)));
+  void* d_ws = C.ws.get(std::max(size_t(plan.workspace_bytes), kSetFloor / 4));
+  uint8_t* d_meta = static_cast<uint8_t*>(C.meta.get(std::max(meta_bytes + res_bytes + 16, kSetFloor / 4)));
   if (!d_io || !d_ws || !d_meta) return fail_all(SZ_ERROR_MEM, "LzmaDecode: device allocation failed");
   // pack inputs and metadata, one upload each
   uint8_t* pin_meta = C.pin + in_total;
@@ -360,57 +446,22 @@ void coalesced(OneCall& me, int dev) {
     me.msg = "LzmaDecode: host allocation failed";
     return;
   }
-  Coalescer& C = *Cp;
-  std::unique_lock<std::mutex> lk(C.mu);
-  C.pending.push_back(&me);
-  while (!me.done) {
-    // lead when this call is still pending and a batch set is free
-    BatchSet* R = nullptr;
-    if (!me.taken)
-      for (int i = 0; i < in_flight_limit() && !R; ++i)
-        if (!C.sets[i].busy) R = &C.sets[i];
-    if (!R) {
-      C.cv.wait(lk);
-      continue;
-    }
-    if (!R->stream && hipStreamCreateWithFlags(&R->stream, hipStreamNonBlocking) != hipSuccess) {
-      (void)hipGetLastError();
-      R->stream = nullptr;
-      C.pending.erase(std::find(C.pending.begin(), C.pending.end(), &me));
-      me.err = SZ_ERROR_FAIL;
-      me.msg = "LzmaDecode: stream creation failed";
-      me.taken = me.done = true;
-      return;
-    }
-    // take everything pending (this call included) as one batch
-    R->busy = true;
-    std::vector<OneCall*> batch;
-    batch.swap(C.pending);
-    if (!coalesce_on() && batch.size() > 1) {  // one launch per call: this one now
-      for (OneCall* c : batch)
-        if (c != &me) C.pending.push_back(c);
-      batch.assign(1, &me);
-    }
-    for (OneCall* c : batch) c->taken = true;
-    lk.unlock();
-    try {
-      run_calls(*R, batch);
-    } catch (const std::exception&) {
-      for (OneCall* c : batch) {
-        c->err = SZ_ERROR_MEM;
-        c->msg = "LzmaDecode: host allocation failed";
-      }
-    }
-    C.batches++;
-    C.items += batch.size();
-    uint64_t mx = C.max_items.load();
-    while (batch.size() > mx && !C.max_items.compare_exchange_weak(mx, batch.size())) {
-    }
-    lk.lock();
-    for (OneCall* c : batch) c->done = true;
-    R->busy = false;
-    C.cv.notify_all();
-  }
+  group_commit<Coalescer, BatchSet>(
+      *Cp, me, std::max(1u, lzgpu_host::device_cus()),
+      [](BatchSet& R, std::vector<OneCall*>& batch) {
+        try {
+          run_calls(R, batch);
+        } catch (const std::exception&) {
+          for (OneCall* c : batch) {
+            c->err = SZ_ERROR_MEM;
+            c->msg = "LzmaDecode: host allocation failed";
+          }
+        }
+      },
+      [](OneCall& c) {
+        c.err = SZ_ERROR_FAIL;
+        c.msg = "LzmaDecode: stream creation failed";
+      });
 }
 
 // LzmaDecode-style one call over host buffers through the device's coalescer.
@@ -448,7 +499,70 @@ SRes gpu_one_call(uint8_t kind, Byte* dest, SizeT* destLen, const Byte* src, Siz
 
 // ------------------------------------------------------------------ dictionary mirrors
 
+// Device buffers of retired mirrors, kept for the next decoder instead of
+// freed: hipFree synchronises the whole device, and a DecodeToBuf caller that
+// creates and frees a decoder per stream (7zDec.c:567-648) would otherwise
+// stall every other caller's launch once per stream.  Bounded; beyond it the
+// oldest buffer is freed.
+struct BufPool {
+  struct Ent {
+    void* p;
+    size_t cap;
+    int dev;
+  };
+  std::mutex mu;
+  std::vector<Ent> v;
+  size_t bytes = 0;
+};
+constexpr size_t kBufPoolMaxBytes = size_t(1) << 30;
+constexpr size_t kBufPoolMaxCount = 512;
+BufPool& buf_pool() {
+  static BufPool* p = new BufPool();  // process lifetime (HIP teardown order)
+  return *p;
+}
+void pool_put(DevBuf& b, int dev) {
+  if (!b.p) return;
+  std::vector<void*> drop;
+  {
+    BufPool& P = buf_pool();
+    std::lock_guard<std::mutex> g(P.mu);
+    try {
+      P.v.push_back({b.p, b.cap, dev});
+    } catch (const std::exception&) {
+      drop.push_back(b.p);
+    }
+    if (drop.empty()) P.bytes += b.cap;
+    while (P.v.size() > kBufPoolMaxCount || P.bytes > kBufPoolMaxBytes) {
+      P.bytes -= P.v.front().cap;
+      drop.push_back(P.v.front().p);
+      P.v.erase(P.v.begin());
+    }
+  }
+  b.p = nullptr;
+  b.cap = 0;
+  for (void* q : drop) (void)hipFree(q);  // outside the pool lock
+}
+// an empty DevBuf takes the smallest pooled buffer of at least n bytes
+void pool_take(DevBuf& b, size_t n, int dev) {
+  if (b.p) return;
+  BufPool& P = buf_pool();
+  std::lock_guard<std::mutex> g(P.mu);
+  size_t best = P.v.size();
+  for (size_t i = 0; i < P.v.size(); ++i)
+    if (P.v[i].dev == dev && P.v[i].cap >= n && (best == P.v.size() || P.v[i].cap < P.v[best].cap))
+      best = i;
+  if (best == P.v.size()) return;
+  b.p = P.v[best].p;
+  b.cap = P.v[best].cap;
+  P.bytes -= b.cap;
+  P.v.erase(P.v.begin() + ptrdiff_t(best));
+}
+
 struct Mirror {
+  ~Mirror() {
+    pool_put(block, dev);
+    pool_put(io, dev);
+  }
   const CLzmaDec* key = nullptr;
   int dev = 0;
   const Byte* dic = nullptr;
@@ -567,11 +681,17 @@ uint64_t probs_hash(const CLzmaProb* t, uint32_t cells) {
 }
 
 void mirror_drop(const CLzmaDec* p) {
+  std::vector<std::shared_ptr<Mirror>> dead;  // released after the registry lock
   Registry& R = registry();
   std::lock_guard<std::mutex> g(R.mu);
-  R.v.erase(std::remove_if(R.v.begin(), R.v.end(),
-                           [&](const std::shared_ptr<Mirror>& e) { return e->key == p; }),
-            R.v.end());
+  for (size_t i = 0; i < R.v.size();) {
+    if (R.v[i]->key == p) {
+      dead.push_back(std::move(R.v[i]));
+      R.v.erase(R.v.begin() + ptrdiff_t(i));
+    } else {
+      ++i;
+    }
+  }
 }
 
 // ------------------------------------------------------------------ coalesced session calls
@@ -590,6 +710,7 @@ struct SessCall {
   int err = 0;     // launch failure
   bool taken = false;  // in a launch (running or done)
   bool done = false;
+  std::condition_variable cv;  // its caller sleeps here (group_commit)
 };
 
 // One session launch in flight: its LzgpuSession array, host copy and stream.
@@ -602,9 +723,9 @@ struct SessSet {
 
 struct SessCoalescer {
   std::mutex mu;
-  std::condition_variable cv;
   std::vector<SessCall*> pending;
   SessSet sets[kMaxInFlight];  // up to in_flight_limit() launches at once
+  uint32_t in_flight = 0;      // calls in running launches
   std::atomic<uint64_t> batches{0}, items{0}, max_items{0};
 };
 
@@ -636,7 +757,7 @@ void run_sess_batch(SessSet& C, const std::vector<SessCall*>& b) {
   size_t j = 0;
   for (size_t i : coop) C.h[j++] = b[i]->q;
   for (size_t i : glob) C.h[j++] = b[i]->q;
-  LzgpuSession* d = static_cast<LzgpuSession*>(C.arr.get(k * sizeof(LzgpuSession)));
+  LzgpuSession* d = static_cast<LzgpuSession*>(C.arr.get(std::max(k * sizeof(LzgpuSession), kSetFloor / 4)));
   const hipStream_t st = C.stream;
   int e = (d && xfer(d, C.h.data(), k * sizeof(LzgpuSession), hipMemcpyHostToDevice, st) ==
                     hipSuccess) ? 0 : 1;
@@ -664,51 +785,16 @@ void sess_coalesced(SessCall& me, int dev) {
     me.err = 1;
     return;
   }
-  SessCoalescer& C = *Cp;
-  std::unique_lock<std::mutex> lk(C.mu);
-  C.pending.push_back(&me);
-  while (!me.done) {
-    SessSet* R = nullptr;
-    if (!me.taken)
-      for (int i = 0; i < in_flight_limit() && !R; ++i)
-        if (!C.sets[i].busy) R = &C.sets[i];
-    if (!R) {
-      C.cv.wait(lk);
-      continue;
-    }
-    if (!R->stream && hipStreamCreateWithFlags(&R->stream, hipStreamNonBlocking) != hipSuccess) {
-      (void)hipGetLastError();
-      R->stream = nullptr;
-      C.pending.erase(std::find(C.pending.begin(), C.pending.end(), &me));
-      me.err = 1;
-      me.taken = me.done = true;
-      return;
-    }
-    R->busy = true;
-    std::vector<SessCall*> batch;
-    batch.swap(C.pending);
-    if (!coalesce_on() && batch.size() > 1) {
-      for (SessCall* c : batch)
-        if (c != &me) C.pending.push_back(c);
-      batch.assign(1, &me);
-    }
-    for (SessCall* c : batch) c->taken = true;
-    lk.unlock();
-    try {
-      run_sess_batch(*R, batch);
-    } catch (const std::exception&) {
-      for (SessCall* c : batch) c->err = 1;
-    }
-    C.batches++;
-    C.items += batch.size();
-    uint64_t mx = C.max_items.load();
-    while (batch.size() > mx && !C.max_items.compare_exchange_weak(mx, batch.size())) {
-    }
-    lk.lock();
-    for (SessCall* c : batch) c->done = true;
-    R->busy = false;
-    C.cv.notify_all();
-  }
+  group_commit<SessCoalescer, SessSet>(
+      *Cp, me, std::max(1u, lzgpu_host::device_cus()),
+      [](SessSet& R, std::vector<SessCall*>& batch) {
+        try {
+          run_sess_batch(R, batch);
+        } catch (const std::exception&) {
+          for (SessCall* c : batch) c->err = 1;
+        }
+      },
+      [](SessCall& c) { c.err = 1; });
 }
 
 // One LzmaDec_DecodeToDic (mode 0) or LzmaDec_DecodeToBuf (mode 1) call on the
@@ -741,8 +827,10 @@ SRes gpu_session_call(CLzmaDec* p, int mode, SizeT dicLimit, const Byte* src, Si
   const hipStream_t st = L.s->stream;
   const size_t out_room = mode == 1 ? size_t(*destLen) : 0;
   const void* blk_before = m->block.p;
+  pool_take(m->block, kSessBytes + pa + p->dicBufSize + 16, dev);
   uint8_t* blk = static_cast<uint8_t*>(m->block.get(kSessBytes + pa + p->dicBufSize + 16));
   const size_t in_pad = (size_t(in_size) + 15) & ~size_t(15);
+  pool_take(m->io, in_pad + out_room + 16, dev);
   uint8_t* d_io = static_cast<uint8_t*>(m->io.get(in_pad + out_room + 16));
   if (!blk || !d_io) {
     m->history = m->probs_dev = false;
@@ -780,10 +868,21 @@ SRes gpu_session_call(CLzmaDec* p, int mode, SizeT dicLimit, const Byte* src, Si
   }
   if (m->probs_dev && (m->probs_cells != cells || probs_hash(p->probs, cells) != m->probs_hash))
     m->probs_dev = false;
+  // small transfers go through the scratch's pinned staging (layout: input |
+  // table up; after the launch: table down | decoded bytes)
+  const size_t tab_bytes = size_t(cells) * 2, tab_pad = (tab_bytes + 15) & ~size_t(15);
+  const size_t down_max = tab_pad + (mode == 1 ? out_room : size_t(p->dicBufSize));
+  uint8_t* pin = lzgpu_host::scratch_pinned(L.s, std::max(in_pad + tab_pad, down_max));
   // the table: the device copy is current after every successful call
-  if (!m->probs_dev &&
-      xfer(d_probs, p->probs, size_t(cells) * 2, hipMemcpyHostToDevice, st) != hipSuccess)
-    return fail("LzmaDec: upload probs");
+  if (!m->probs_dev) {
+    const void* from = p->probs;
+    if (pin) {
+      memcpy(pin + in_pad, p->probs, tab_bytes);
+      from = pin + in_pad;
+    }
+    if (xfer(d_probs, from, tab_bytes, hipMemcpyHostToDevice, st) != hipSuccess)
+      return fail("LzmaDec: upload probs");
+  }
   // history: only a decoder continuing a dictionary reads bytes it did not
   // write in this call (LzmaDec.c:165-166,176,216,376-408 read dic only when
   // processedPos or checkDicSize is non-zero); uploaded once per mirror
@@ -791,7 +890,8 @@ SRes gpu_session_call(CLzmaDec* p, int mode, SizeT dicLimit, const Byte* src, Si
   if (need_hist && !m->history && p->dicBufSize &&
       xfer(d_dic, p->dic, p->dicBufSize, hipMemcpyHostToDevice, st) != hipSuccess)
     return fail("LzmaDec: upload dictionary");
-  if (in_size && xfer(d_io, src, in_size, hipMemcpyHostToDevice, st) != hipSuccess)
+  if (in_size && pin) memcpy(pin, src, in_size);
+  if (in_size && xfer(d_io, pin ? pin : src, in_size, hipMemcpyHostToDevice, st) != hipSuccess)
     return fail("LzmaDec: upload src");
 
   LzgpuSession q;
@@ -834,31 +934,35 @@ SRes gpu_session_call(CLzmaDec* p, int mode, SizeT dicLimit, const Byte* src, Si
   sess_coalesced(call, dev);
   if (call.err) return fail("LzmaDec: session kernel");
   q = call.q;
-  // the table back (the kernel wrote it to the mirror's device copy)
-  std::vector<uint8_t> back;
-  try {
-    back.resize(kSessBytes + size_t(cells) * 2);
-  } catch (const std::exception&) {
-    m->history = m->probs_dev = false;
-    set_error("LzmaDec: host allocation failed");
-    return SZ_ERROR_MEM;
-  }
-  // the table and the decoded bytes (DecodeToDic's new dictionary bytes,
-  // DecodeToBuf's output) in one synchronisation
+  // the table back (the kernel wrote it to the mirror's device copy) and the
+  // decoded bytes (DecodeToDic's new dictionary bytes, DecodeToBuf's output),
+  // in one synchronisation, into the pinned staging when there is one
   if (mode == 0) {
     if (q.dic_pos < pos0 || q.dic_pos > p->dicBufSize) return fail("LzmaDec: bad session state");
   } else if (q.out_len > out_room || q.dic_pos > p->dicBufSize) {
     return fail("LzmaDec: bad session state");
   }
-  if (xfer(back.data() + kSessBytes, d_probs, size_t(cells) * 2, hipMemcpyDeviceToHost, st) !=
-          hipSuccess ||
-      (mode == 0 && q.dic_pos > pos0 &&
-       xfer(p->dic + pos0, d_dic + pos0, q.dic_pos - pos0, hipMemcpyDeviceToHost, st) !=
-           hipSuccess) ||
-      (mode == 1 && q.out_len &&
-       xfer(dest, d_io + in_pad, q.out_len, hipMemcpyDeviceToHost, st) != hipSuccess) ||
+  const size_t nbytes = mode == 0 ? size_t(q.dic_pos - pos0) : size_t(q.out_len);
+  const uint8_t* d_bytes = mode == 0 ? d_dic + pos0 : d_io + in_pad;
+  Byte* h_bytes = mode == 0 ? p->dic + pos0 : dest;
+  std::vector<uint8_t> back;
+  uint8_t* tab_to = pin;
+  if (!pin) {
+    try {
+      back.resize(tab_bytes);
+    } catch (const std::exception&) {
+      m->history = m->probs_dev = false;
+      set_error("LzmaDec: host allocation failed");
+      return SZ_ERROR_MEM;
+    }
+    tab_to = back.data();
+  }
+  if (xfer(tab_to, d_probs, tab_bytes, hipMemcpyDeviceToHost, st) != hipSuccess ||
+      (nbytes && xfer(pin ? pin + tab_pad : h_bytes, d_bytes, nbytes, hipMemcpyDeviceToHost, st) !=
+                     hipSuccess) ||
       hipStreamSynchronize(st) != hipSuccess)
     return fail("LzmaDec: download probs / decoded bytes");
+  if (pin && nbytes) memcpy(h_bytes, pin + tab_pad, nbytes);
   if (mode == 1) {
     // the host ring gets the same bytes the device ring got (LzmaDec.c:849-866:
     // each pass writes from dicPos, wrapping to 0 at dicBufSize)
@@ -874,7 +978,7 @@ SRes gpu_session_call(CLzmaDec* p, int mode, SizeT dicLimit, const Byte* src, Si
     }
     *destLen = q.out_len;
   }
-  memcpy(p->probs, back.data() + kSessBytes, size_t(cells) * 2);
+  memcpy(p->probs, tab_to, tab_bytes);
   p->dicPos = q.dic_pos;
   p->range = q.range;
   p->code = q.code;

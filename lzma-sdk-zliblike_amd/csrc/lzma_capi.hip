@@ -989,6 +989,22 @@ CallScratch* scratch_acquire() {
   return s;
 }
 
+uint8_t* scratch_pinned(CallScratch* s, size_t n) {
+  if (!s || n > kPinnedStageMax) return nullptr;
+  if (s->pin_cap >= n) return s->pin;
+  const size_t want = std::min(kPinnedStageMax, std::max({n, s->pin_cap * 2, size_t(1) << 20}));
+  if (s->pin) (void)hipHostFree(s->pin);
+  s->pin = nullptr;
+  s->pin_cap = 0;
+  if (hipHostMalloc(reinterpret_cast<void**>(&s->pin), want, hipHostMallocDefault) != hipSuccess) {
+    (void)hipGetLastError();
+    s->pin = nullptr;
+    return nullptr;
+  }
+  s->pin_cap = want;
+  return s->pin;
+}
+
 void scratch_release(CallScratch* s) {
   if (!s) return;
   ScratchPool& P = scratch_pool();
@@ -997,6 +1013,7 @@ void scratch_release(CallScratch* s) {
     P.free_sets[s->dev].push_back(s);
   } catch (const std::exception&) {
     (void)hipStreamDestroy(s->stream);
+    if (s->pin) (void)hipHostFree(s->pin);
     delete s;
   }
 }

@@ -134,9 +134,18 @@ struct CallScratch {
   DevBuf buf[4];
   hipStream_t stream = nullptr;
   int dev = 0;
+  uint8_t* pin = nullptr;  // pinned host staging (scratch_pinned)
+  size_t pin_cap = 0;
 };
 CallScratch* scratch_acquire();  // current device; nullptr (error set) on failure
 void scratch_release(CallScratch* s);
+// The scratch's pinned host staging, at least n bytes (grown geometrically from
+// 1 MiB, at most kPinnedStageMax); nullptr when n is larger or the allocation
+// fails -- the caller then copies from / to pageable memory directly.  A
+// pageable hipMemcpyAsync goes through the runtime's own staging buffer, one
+// per device, so concurrent callers' small copies queue behind each other.
+constexpr size_t kPinnedStageMax = size_t(8) << 20;
+uint8_t* scratch_pinned(CallScratch* s, size_t n);
 
 // owning device array for the container drivers' per-call buffers
 template <class T>

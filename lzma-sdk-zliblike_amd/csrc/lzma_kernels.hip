@@ -379,6 +379,18 @@ static int launch_lds_w(const LzmaGpuStreamDesc* d_descs, const uint32_t* d_orde
                               groups_per_cu, max_groups, d_queue, sl, stream);
 }
 
+// Workgroups a CU actually holds at once: the launch's workgroups spread over
+// the CUs, so at most min(groups_per_cu, ceil(n / cus)).  The register budget
+// (the W of __launch_bounds__) follows it: a plan for 16 narrow-table
+// cooperative waves per CU that gets one stream (a lone drop-in call) would
+// otherwise run the W = 4 build, 128 VGPRs and 46-218 spilled, instead of the
+// W = 2 build without spills.
+static uint32_t resident_waves_per_simd(uint32_t n, uint32_t groups_per_cu) {
+  const uint32_t cus = std::max(1u, lzgpu_host::device_cus());
+  const uint32_t per_cu = std::max(1u, std::min(groups_per_cu, (n + cus - 1) / cus));
+  return (per_cu + 3) / 4;
+}
+
 template <bool K2>
 static int launch_class(const LzmaGpuStreamDesc* d_descs, const uint32_t* d_order, uint32_t n,
                         const uint8_t* d_src, uint8_t* d_dst, uint16_t* d_ws,
@@ -398,7 +410,7 @@ static int launch_class(const LzmaGpuStreamDesc* d_descs, const uint32_t* d_orde
   if (lds_mask == (LZGPU_LDS_MASK_LAT | kCoopBit)) {
     // one wave per workgroup: register budget by workgroups per SIMD
     constexpr uint32_t MC = LZGPU_LDS_MASK_LAT | kCoopBit;
-    const uint32_t w = (groups_per_cu + 3) / 4;
+    const uint32_t w = resident_waves_per_simd(n, groups_per_cu);
     if (w <= 2)
       return launch_coop<2, MC, K2>(d_descs, d_order, n, d_src, d_dst, d_ws, d_results, stride,
                                     groups_per_cu, max_groups, d_queue, stream);
@@ -408,7 +420,7 @@ static int launch_class(const LzmaGpuStreamDesc* d_descs, const uint32_t* d_orde
   if (lds_mask == (LZGPU_LDS_MASK_ALL | kCoopBit)) {
     // the whole table in LDS, plus the history window where the launch has room
     constexpr uint32_t MC = LZGPU_LDS_MASK_ALL | kCoopBit;
-    const uint32_t w = (groups_per_cu + 3) / 4;
+    const uint32_t w = resident_waves_per_simd(n, groups_per_cu);
     if (w <= 2)
       return launch_coop<2, MC, K2, MC | kWinBit>(d_descs, d_order, n, d_src, d_dst, d_ws,
                                                   d_results, stride, groups_per_cu, max_groups,
@@ -419,7 +431,11 @@ static int launch_class(const LzmaGpuStreamDesc* d_descs, const uint32_t* d_orde
   }
   if (lds_mask == LZGPU_LDS_MASK_LAT)
     return launch_lds_w<LZGPU_LDS_MASK_LAT, K2>(d_descs, d_order, n, d_src, d_dst, d_ws,
-                                                d_results, lanes, stride, waves_per_simd,
+                                                d_results, lanes, stride,
+                                                lanes == 1 ? std::min(waves_per_simd,
+                                                                      resident_waves_per_simd(
+                                                                          n, groups_per_cu))
+                                                           : waves_per_simd,
                                                 groups_per_cu, max_groups, d_queue, sl, stream);
   return -1;  // no kernel built for this placement
 }
