@@ -154,13 +154,29 @@ struct Coalescer {
   std::vector<OneCall*> pending;
   BatchSet sets[kMaxInFlight];
   uint32_t in_flight = 0;  // calls in running batches
+  std::atomic<uint32_t> callers{0};  // threads inside a call (ActiveCall)
   std::atomic<uint64_t> batches{0}, items{0}, max_items{0};
+};
+
+// Counts a thread as inside a drop-in call for its whole duration, host work
+// before and after its launch included (the concurrency gate of free_set).
+struct ActiveCall {
+  std::atomic<uint32_t>* n;
+  explicit ActiveCall(std::atomic<uint32_t>* c) : n(c) {
+    if (n) ++*n;
+  }
+  ~ActiveCall() {
+    if (n) --*n;
+  }
+  ActiveCall(const ActiveCall&) = delete;
+  ActiveCall& operator=(const ActiveCall&) = delete;
 };
 
 // Group commit, shared by the one-call and the session coalescers (C: mu,
 // pending, sets[], in_flight and the counters; Call: taken, done, cv).  A
-// pending call leads when a batch set is free and no batch runs, or the
-// running ones hold fewer than budget / 2 calls (budget: one call per CU; a
+// pending call leads when a batch set is free and no batch runs, or fewer
+// than budget / 2 calls are active -- threads inside a call, whether pending,
+// running or in their own host work around it (budget: one call per CU; a
 // lone call's stream is one wave, so small batches leave the chip idle and
 // run side by side, while a large one already fills it); it takes the
 // pending calls in arrival order, up to budget minus those in flight, runs them
@@ -173,11 +189,14 @@ bool coalesce_on();
 
 template <class Set, class Coal>
 Set* free_set(Coal& C, uint32_t budget) {
-  // a second batch only while the running ones fill less than half the
-  // budget: 256 callers ran 124 MB/s one batch at a time and 86 MB/s with
-  // concurrent batches (each a fraction of the callers), 16 callers 12.9 vs
-  // 17.2 MB/s the other way round (profiles/r05_coalesce/)
-  if (C.in_flight != 0 && C.in_flight >= budget / 2) return nullptr;
+  // a second batch only while the active calls (running + pending) are fewer
+  // than half the budget: with many callers one batch at a time holds them
+  // all, while concurrent sets split them into small batches -- 256 callers
+  // 124 vs 86 MB/s, DecodeToBuf loops 21 vs 12 MB/s; with few callers the
+  // sets run side by side -- 16 callers 12.9 vs 19.3 MB/s
+  // (profiles/r05_coalesce/)
+  const size_t active = std::max<size_t>(C.in_flight + C.pending.size(), C.callers.load());
+  if (C.in_flight != 0 && active >= budget / 2) return nullptr;
   for (int i = 0; i < in_flight_limit(); ++i)
     if (!C.sets[i].busy) return &C.sets[i];
   return nullptr;
@@ -475,6 +494,8 @@ SRes gpu_one_call(uint8_t kind, Byte* dest, SizeT* destLen, const Byte* src, Siz
   int dev = 0;
   if (!hip_ok(hipGetDevice(&dev), "current device")) return SZ_ERROR_FAIL;
   ++g_calls;
+  Coalescer* Cp = coalescer(dev);
+  ActiveCall active(Cp ? &Cp->callers : nullptr);
   const uint64_t t_call = now_ns();
   OneCall c;
   c.kind = kind;
@@ -726,6 +747,7 @@ struct SessCoalescer {
   std::vector<SessCall*> pending;
   SessSet sets[kMaxInFlight];  // up to in_flight_limit() launches at once
   uint32_t in_flight = 0;      // calls in running launches
+  std::atomic<uint32_t> callers{0};  // threads inside a session call (ActiveCall)
   std::atomic<uint64_t> batches{0}, items{0}, max_items{0};
 };
 
@@ -805,6 +827,8 @@ SRes gpu_session_call(CLzmaDec* p, int mode, SizeT dicLimit, const Byte* src, Si
   int dev = 0;
   if (!hip_ok(hipGetDevice(&dev), "current device")) return SZ_ERROR_FAIL;
   ++g_calls;
+  SessCoalescer* SCp = sess_coalescer(dev);
+  ActiveCall active(SCp ? &SCp->callers : nullptr);
   const uint32_t cells = lzgpu::table_cells(p->prop.lc, p->prop.lp, p->prop.pb);
   if (p->probs == nullptr || cells > p->numProbs) {
     set_error("LzmaDec: probabilities not allocated for the current props");
