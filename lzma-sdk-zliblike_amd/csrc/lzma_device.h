@@ -713,20 +713,53 @@ struct LocalReader {
 
 // ------------------------------------------------------------------ range decoder
 
-template <class Rd>
+// The cooperative kernels' lanes all hold the same decoder state, so the
+// decoder's branch conditions are wave-uniform there.
+template <uint32_t M>
+__host__ __device__ constexpr bool uni_on() {
+  return (M & kCoopBit) != 0u;
+}
+// A wave-uniform branch condition tested as a ballot: the compiler branches on
+// the compare's mask (VCC) instead of saving, narrowing and restoring EXEC
+// around the body.  Measured (profiles/r05_uni/): the cooperative kernel,
+// one wave per SIMD, +2.2 % on config 4 and +2.5 % on the xz leg; the 32-lane
+// one-stream kernel, four waves per SIMD and issue-bound, lost 3.5 % on
+// config 2 (the compiler materialises the conditions and adds phi copies), so
+// it keeps EXEC-masked branches.
+#ifndef LZGPU_UNI_IF
+#define LZGPU_UNI_IF 2  // 0: plain (EXEC-masked) branches everywhere; 1: NORMALIZE only (A/B)
+#endif
+template <bool U>
+__device__ __forceinline__ bool lz_if(bool c) {
+#ifndef LZGPU_HOST_EMU
+  if constexpr (U && LZGPU_UNI_IF != 0) return __builtin_amdgcn_ballot_w64(c) != 0;
+#endif
+  return c;
+}
+// the same for the symbol loop's own branches (symbol kind, rep kind, length
+// choice, distance slot class); LZGPU_UNI_IF=1 keeps them EXEC-masked
+template <bool U>
+__device__ __forceinline__ bool lz_br(bool c) {
+#ifndef LZGPU_HOST_EMU
+  if constexpr (U && LZGPU_UNI_IF >= 2) return __builtin_amdgcn_ballot_w64(c) != 0;
+#endif
+  return c;
+}
+
+template <class Rd, bool U = false>
 struct Rc {
   uint32_t range, code;
   Rd* rd;
   // NORMALIZE (LzmaDec.c:17): shift in one input byte when range < 2^24
   __device__ __forceinline__ void norm() {
-    if (range < kTop) {
+    if (lz_if<U>(range < kTop)) {
       range <<= 8;
       code = (code << 8) | rd->next();
     }
   }
   // NORMALIZE after a reader checkpoint: the byte is known to be in the window
   __device__ __forceinline__ void norm_u() {
-    if (range < kTop) {
+    if (lz_if<U>(range < kTop)) {
       range <<= 8;
       code = (code << 8) | rd_take_u(*rd);
     }
@@ -920,8 +953,8 @@ __device__ __forceinline__ uint32_t lz_lane_id() { return __lane_id(); }
 // (code >= 2^31 + (R >> k): only a corrupt stream) takes the chunk bit by
 // bit.  Returns with range >= 2^24 not guaranteed (the caller's next decision
 // normalises first, as the reference does).
-template <class Rd>
-__device__ __forceinline__ void direct_coop(Rc<Rd>& rc, uint32_t& dist, uint32_t left) {
+template <class Rd, bool U>
+__device__ __forceinline__ void direct_coop(Rc<Rd, U>& rc, uint32_t& dist, uint32_t left) {
 #ifndef LZGPU_HOST_EMU
   const uint32_t j = lz_lane_id() & 31u;
 #endif
@@ -1238,8 +1271,8 @@ __device__ __forceinline__ void lz_emit(gbyte* dic, uint64_t pos, uint32_t v, Lz
 // Literal-tree cell for reference literal offset `rel` (0..0x2FF) of context ctx:
 // plain part for rel < 0x100, matched part above.  Both parts in LDS (or both
 // global) -> a branch-free offset select; split placement -> a real branch.
-template <uint32_t M, class Lo, class Rd>
-__device__ __forceinline__ uint32_t lit_bit(Rc<Rd>& rc, const Tab<M, Lo>& T, uint32_t ctx,
+template <uint32_t M, class Lo, class Rd, bool U>
+__device__ __forceinline__ uint32_t lit_bit(Rc<Rd, U>& rc, const Tab<M, Lo>& T, uint32_t ctx,
                                             uint32_t offs_mbit, uint32_t sym) {
   constexpr bool p_lds = ((M >> S_LITP) & 1u) != 0u, m_lds = ((M >> S_LITM) & 1u) != 0u;
   if constexpr (p_lds == m_lds) {
@@ -1257,8 +1290,8 @@ __device__ __forceinline__ uint32_t lit_bit(Rc<Rd>& rc, const Tab<M, Lo>& T, uin
 
 // One literal (LzmaDec.c:161-196): plain tree for state < 7, matched tree
 // against the byte at rep0 otherwise; writes the byte, updates state.
-template <uint32_t M, class Lo, class Rd>
-__device__ __forceinline__ void lz_literal(Rc<Rd>& rc, const Tab<M, Lo>& T, uint32_t& st,
+template <uint32_t M, class Lo, class Rd, bool U>
+__device__ __forceinline__ void lz_literal(Rc<Rd, U>& rc, const Tab<M, Lo>& T, uint32_t& st,
                                            uint32_t& prev, uint32_t& total, uint32_t full,
                                            uint32_t lc, uint32_t lp_mask, gbyte* dic,
                                            uint64_t& pos, uint64_t cap, uint32_t r0,
@@ -1266,7 +1299,7 @@ __device__ __forceinline__ void lz_literal(Rc<Rd>& rc, const Tab<M, Lo>& T, uint
   uint32_t sym = 1;
   uint32_t ctx = 0;
   if (full != 0 || total != 0) ctx = ((total & lp_mask) << lc) + (prev >> (8 - lc));
-  if (st < 7) {
+  if (lz_br<U>(st < 7)) {
     st = (st < 4) ? 0 : st - 3;
     auto lp = T.template at<S_LITP>(ctx << 8);
     const uint32_t m = rc.template tree_u<4>(lp, 1);
@@ -1367,7 +1400,8 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
   uint32_t total = s.total;
   const uint32_t full = s.full;
   uint32_t len = 0;
-  Rc<Rd> rc{s.range, s.code, &rd};
+  constexpr bool kU = uni_on<M>();  // wave-uniform decoder state (lz_br)
+  Rc<Rd, kU> rc{s.range, s.code, &rd};
   // previous byte (literal context), kept in a register
   uint32_t prev = 0;
   if (full != 0 || total != 0) prev = dic[(pos == 0 ? cap : pos) - 1];
@@ -1411,11 +1445,11 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
       uint64_t tB = 0, tC = 0;
       bool did_lit = false;
 #endif
-      if (lit_on) {
+      if (lz_br<kU>(lit_on)) {
         ps = total & pb_mask;
         rd_topup(rd);
         const uint32_t ism = rc.bit_u(T.template at<S_MATCH>((st << pb) + ps));
-        if (ism) {
+        if (lz_br<kU>(ism != 0)) {
           is_match = true;
           lit_on = false;
         } else {
@@ -1428,7 +1462,7 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
 #if LZGPU_PROF && !defined(LZGPU_HOST_EMU)
           tC = lz_clock();
 #endif
-          if (!(pos < limit && rd.used() < in_limit)) {
+          if (lz_br<kU>(!(pos < limit && rd.used() < in_limit))) {
             stop = true;
             lit_on = false;
           }
@@ -1474,13 +1508,13 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
 #endif
     const uint64_t tm0 = lz_clock();
 #endif
-    if (!rc.bit(T.template at<S_REP>(st))) {
+    if (lz_br<kU>(!rc.bit(T.template at<S_REP>(st)))) {
       st += 12;
       lcoder_is_rep = 0;
     } else {
       if (full == 0 && total == 0) return kErrData;
-      if (!rc.bit(T.template at<S_REP>(12 + st))) {
-        if (!rc.bit(T.template at<S_REP0L>((st << pb) + ps))) {
+      if (lz_br<kU>(!rc.bit(T.template at<S_REP>(12 + st)))) {
+        if (lz_br<kU>(!rc.bit(T.template at<S_REP0L>((st << pb) + ps)))) {
           if constexpr ((M & kCoopBit) != 0u) {
             // short rep = a one-byte copy: the byte and the next matched byte
             // in one load batch
@@ -1498,10 +1532,10 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
         }
       } else {
         uint32_t dist;
-        if (!rc.bit(T.template at<S_REP>(24 + st))) {
+        if (lz_br<kU>(!rc.bit(T.template at<S_REP>(24 + st)))) {
           dist = r1;
         } else {
-          if (!rc.bit(T.template at<S_REP>(36 + st))) {
+          if (lz_br<kU>(!rc.bit(T.template at<S_REP>(36 + st)))) {
             dist = r2;
           } else {
             dist = r3;
@@ -1556,9 +1590,9 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
           len = 16 + rc.template tree<8>(T.template at<S_LENHI>(lcoder_is_rep << 8));
         }
       } else {
-        if (!rc.bit(lbase))
+        if (lz_br<kU>(!rc.bit(lbase)))
           len = rc.template tree<3>(lbase + 2 + (ps << 3));
-        else if (!rc.bit(lbase + 1))
+        else if (lz_br<kU>(!rc.bit(lbase + 1)))
           len = 8 + rc.template tree<3>(lbase + 2 + (8u << pb) + (ps << 3));
         else
           len = 16 + rc.template tree<8>(T.template at<S_LENHI>(lcoder_is_rep << 8));
@@ -1569,7 +1603,7 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
     const uint64_t tm2 = lz_clock();
     s.prof[9] += tm2 - tm1;
 #endif
-    if (st >= 12) {
+    if (lz_br<kU>(st >= 12)) {
       const uint32_t lstate = len < 4 ? len : 3;
       uint32_t dist;
       if constexpr (((M >> S_SLOT) & 1u) == 0u) {
@@ -1598,11 +1632,11 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
 #if LZGPU_PROF == 1 && !defined(LZGPU_HOST_EMU)
       const uint64_t t_tail = lz_clock();
 #endif
-      if (dist >= 4) {
+      if (lz_br<kU>(dist >= 4)) {
         const uint32_t slot = dist;
         uint32_t nbits = (slot >> 1) - 1;
         dist = 2 | (slot & 1);
-        if (slot < 14) {
+        if (lz_br<kU>(slot < 14)) {
           dist <<= nbits;
           uint32_t mask = 1, node = 1;
           const uint32_t sp = dist - slot - 1;
@@ -1621,7 +1655,7 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
               nbits = 0;
             }
           }
-          while (nbits != 0) {
+          while (lz_br<kU>(nbits != 0)) {
             uint32_t b = rc.bit(T.template at<S_SPEC>(sp + node));
             node = (node << 1) | b;
             dist |= b ? mask : 0u;
