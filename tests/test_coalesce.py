@@ -114,3 +114,32 @@ def test_gpu_c_threads_caller_matches_reference_build(tmp_path):
         if os.path.exists(TC.THREADS_REF):
             d = TC.run_c_threads(TC.THREADS_REF, 16, f, mode=mode)
             assert d["fails"] == 0 and d["crc_xor"] == "%08x" % want, d
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("inflight,coalesce", [("1", "1"), ("8", "1"), ("4", "0")])
+def test_gpu_c_threads_every_in_flight_setting(tmp_path, inflight, coalesce):
+    """The group-commit variants (dropin_capi.hip group_commit): one batch set,
+    the most sets, and coalescing off (one launch per call), for both one-call
+    and DecodeToBuf callers: every stream's CRC equals the plain data's, and
+    with coalescing on concurrent callers share launches."""
+    if not os.path.exists(TC.THREADS_BIN):
+        TC.build_c_threads()
+    plain, comp, lens, props = W.uniform_batch(300, 4096, 0, 0, 0, 4096, first=5000)
+    offs = [0]
+    for ln in lens:
+        offs.append(offs[-1] + int(ln))
+    comps = [comp[offs[i]:offs[i + 1]].tobytes() for i in range(300)]
+    f = TC.write_stream_set(str(tmp_path), comps, [props] * 300, [4096] * 300)
+    want = 0
+    for i in range(300):
+        want ^= zlib.crc32(plain[i * 4096:(i + 1) * 4096].tobytes(), i)
+    env = dict(os.environ, LZGPU_COALESCE_INFLIGHT=inflight, LZGPU_COALESCE=coalesce)
+    for mode in ("one", "buf"):
+        for threads in (5, 48):
+            d = TC.run_c_threads(TC.THREADS_BIN, threads, f, env=env, mode=mode)
+            assert d["fails"] == 0 and d["crc_xor"] == "%08x" % want, (mode, threads, d)
+            if coalesce == "1" and threads == 48:
+                assert d["max_batch"] > 1, d
+            if coalesce == "0":
+                assert d["max_batch"] == 1, d
