@@ -8,6 +8,9 @@ cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/r05_fuzz
 mkdir -p $O
 sha256sum lzma-sdk-zliblike_amd/lib/liblzmagpu.so > $O/binary.sha256
+timeout -k 10 300 python -u -m pytest tests/test_coalesce.py -v --timeout 240 --timeout-method thread -m gpu \
+  -k oversized > $O/pytest_oversized.log 2>&1
+s=$?; echo "oversized exit $s: $(tail -1 $O/pytest_oversized.log)"; [ $s -eq 0 ] || exit $s
 LZGPU_FUZZ_CASES=50000 LZGPU_FUZZ_SEED=20261019 timeout -k 10 600 python -u -m pytest \
   tests/test_gpu_kernels.py -m gpu -v --timeout 500 --timeout-method thread -k "test_fuzz_vs_oracle_each_kernel" \
   > $O/fuzz_50k_seed20261019.log 2>&1

@@ -143,3 +143,29 @@ def test_gpu_c_threads_every_in_flight_setting(tmp_path, inflight, coalesce):
                 assert d["max_batch"] > 1, d
             if coalesce == "0":
                 assert d["max_batch"] == 1, d
+
+
+@pytest.mark.gpu
+def test_gpu_oversized_call_runs_beside_small_ones():
+    """a call whose input + capacity exceed the coalescer's item
+    limit (dropin_capi.hip kCoalesceItemMax, 256 MiB) runs in a batch of its
+    own, so its footprint neither sets nor fails the small calls' batch; every
+    call still returns exactly what the oracle does."""
+    import lzmagpu as L
+    orc = native.oracle()
+    rng = random.Random(515)
+    cases = []
+    for i in range(40):
+        data = native.gen("text", 97_000 + i, rng.choice([100, 4096, 20000]))
+        comp = lzma.compress(data, format=lzma.FORMAT_RAW, filters=[
+            {"id": lzma.FILTER_LZMA1, "dict_size": 1 << 16, "lc": 3, "lp": 0, "pb": 2}])
+        cap = len(data) if i != 17 else (256 << 20) + 4096  # one oversized capacity
+        cases.append((comp, W.props_bytes(3, 0, 2, 1 << 16), cap, 0 if i == 17 else 1))
+    want = [native.decode(orc, "orc", c, p, cap, fin) for c, p, cap, fin in cases]
+    L.coalesce_stats(reset=True)
+    with ThreadPoolExecutor(16) as ex:
+        got = list(ex.map(lambda k: L.LzmaDecode(*cases[k]), range(len(cases))))
+    for k, (g, w) in enumerate(zip(got, want)):
+        assert g[0] == w[0] and g[2:] == w[2:] and (g[0] != 0 or g[1] == w[1]), (k, g[:4], w[:4])
+    batches, calls, _ = L.coalesce_stats()
+    assert calls == len(cases) and batches >= 2, (batches, calls)
