@@ -48,6 +48,12 @@
 namespace lzgpu {
 
 enum : int { kOk = 0, kErrData = 1, kErrMem = 2, kErrUnsupported = 4, kErrParam = 5, kErrInputEof = 6 };
+// internal (never returned to a caller): the fast tail of a one-shot decode
+// met a symbol that needs input past the stream's end; decode it again exactly
+constexpr int kRetryExact = 99;
+#ifndef LZGPU_FAST_TAIL
+#define LZGPU_FAST_TAIL 1  // 0: probe every symbol of the last 20 bytes (A/B)
+#endif
 enum : int { kStNone = 0, kStDoneMark = 1, kStNotDone = 2, kStMoreInput = 3, kStMaybeDone = 4 };
 enum : int { kFinAny = 0, kFinEnd = 1 };
 
@@ -2019,10 +2025,18 @@ __device__ __forceinline__ void lz_init_dic_state(LzStateT<Lo>& s, bool init_dic
 // LzmaDec_DecodeToDic for one lane.  src is global memory.  WithTemp = false
 // drops the tempBuf continuation path, which a one-call decode (all input
 // present) never takes: its first need is a NEEDS_MORE_INPUT return.
+// fast_tail (one-shot decodes only): the last < 20 input bytes are decoded in
+// one bulk pass, checked afterwards, instead of one symbol per pass behind the
+// reference's look-ahead probe (LzmaDec.c:775-800, LzmaDec_TryDummy).  A
+// symbol the probe lets through is one whose reads, plus the byte a following
+// NORMALIZE would take, stay inside the input; reads only grow, so checking
+// the pass's last symbol checks them all.  If that fails, or the pass stops on
+// a data error (which may sit in a symbol the probe would have refused), it
+// returns kRetryExact and the caller decodes the item again on the exact path.
 template <bool WithTemp, uint32_t M, class Lo>
 __device__ __forceinline__ int lz_decode_to_dic(LzStateT<Lo>& s, uint64_t dic_limit,
                                                 const gbyte* src, uint64_t& src_len, int fin,
-                                                int& status) {
+                                                int& status, bool fast_tail = false) {
   uint64_t avail = src_len;
   src_len = 0;
   lz_flush_pending<M>(s, dic_limit);
@@ -2063,7 +2077,10 @@ __device__ __forceinline__ int lz_decode_to_dic(LzStateT<Lo>& s, uint64_t dic_li
       const uint64_t t_tail = lz_clock();
       const bool tail = avail < kLookahead || at_end_check;
 #endif
-      if (avail < kLookahead || at_end_check) {
+      const bool fast = !WithTemp && fast_tail && avail < kLookahead && avail != 0 && !at_end_check;
+      if (fast) {
+        in_limit = uint32_t(avail);  // through the last byte, checked below
+      } else if (avail < kLookahead || at_end_check) {
         int k = lz_probe<M>(s, src, avail);
         if (k == PROBE_SHORT) {
           for (uint32_t i = 0; i < uint32_t(avail); ++i) s.tmp.set(i, src[i]);
@@ -2080,17 +2097,20 @@ __device__ __forceinline__ int lz_decode_to_dic(LzStateT<Lo>& s, uint64_t dic_li
       }
       typename BulkReaderFor<M>::type rd;
       rd.init(src, avail);
-#if LZGPU_PROF && !defined(LZGPU_HOST_EMU)
       const int rr = lz_run_split<M>(s, dic_limit, rd, in_limit);
+#if LZGPU_PROF && !defined(LZGPU_HOST_EMU)
       s.prof[4] += rd.prof;
       if (tail) {
         s.prof[18] += lz_clock() - t_tail;
         s.prof[19] += 1;
       }
-      if (rr != kOk) return kErrData;
-#else
-      if (lz_run_split<M>(s, dic_limit, rd, in_limit) != kOk) return kErrData;
 #endif
+      // the probe also wants the byte the next NORMALIZE would take
+      // (LzmaDec_TryDummy ends in NORMALIZE_CHECK); a data error may sit in a
+      // symbol the probe would have refused: both go exact
+      if (fast && (rr != kOk || uint64_t(rd.used()) + (s.range < kTop ? 1u : 0u) > avail))
+        return kRetryExact;
+      if (rr != kOk) return kErrData;
       const uint32_t used = rd.used();
       src_len += used;
       src += used;

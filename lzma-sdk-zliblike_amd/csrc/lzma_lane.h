@@ -168,25 +168,40 @@ __device__ __forceinline__ LzmaGpuResult lane_decode_lds(const LzmaGpuStreamDesc
     r.res = kErrMem;
     return r;
   }
-  s.lo = lo;
-  s.gl = gtab();
-  s.win = w0;
-  s.dic = (gbyte*)(dst + d.dst_off);
-  s.cap = d.dst_cap;
-  s.pos = 0;
-  s.range = s.code = 0;
-  s.st = 0;
-  s.rep0 = s.rep1 = s.rep2 = s.rep3 = 1;
-  s.need_state_init = 0;
-  lz_init_dic_state(s, true, true);
+  auto start = [&]() {
+    s.lo = lo;
+    s.gl = gtab();
+    s.win = w0;
+    s.dic = (gbyte*)(dst + d.dst_off);
+    s.cap = d.dst_cap;
+    s.pos = 0;
+    s.range = s.code = 0;
+    s.st = 0;
+    s.rep0 = s.rep1 = s.rep2 = s.rep3 = 1;
+    s.need_state_init = 0;
+    lz_init_dic_state(s, true, true);
+  };
+  start();
   uint64_t sl = d.src_len;
   int status = kStNone;
 #if LZGPU_PROF && !defined(LZGPU_HOST_EMU)
   for (int k = 0; k < 21; ++k) s.prof[k] = 0;
   const uint64_t t0 = lz_clock();
 #endif
-  int res = lz_decode_to_dic<false, M>(s, d.dst_cap, (const gbyte*)(src + d.src_off), sl,
-                                    d.finish_mode, status);
+  // the fast tail first; a truncated or corrupt end (kRetryExact) again, with
+  // the reference's probe on every symbol of the tail (one instantiation of the
+  // decoder for both passes)
+  bool fast = LZGPU_FAST_TAIL != 0;
+  int res;
+  for (;;) {
+    res = lz_decode_to_dic<false, M>(s, d.dst_cap, (const gbyte*)(src + d.src_off), sl,
+                                     d.finish_mode, status, fast);
+    if (res != kRetryExact) break;
+    fast = false;
+    start();
+    sl = d.src_len;
+    status = kStNone;
+  }
 #if LZGPU_PROF && !defined(LZGPU_HOST_EMU)
   s.prof[3] = lz_clock() - t0;
   s.prof[12] = s.total;  // literals + match bytes: decoded bytes
