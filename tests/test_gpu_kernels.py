@@ -176,6 +176,54 @@ def test_goldens_through_each_kernel(L, kernel):
     assert not bad, (kernel, len(bad), bad[:8])
 
 
+# ---------------------------------------------------------------- the stream's last bytes
+
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_tail_truncations_through_each_kernel(L, kernel):
+    """The fast tail of one-shot decodes (lzma_device.h lz_decode_to_dic): the
+    last < 20 input bytes in one bulk pass, checked afterwards against the
+    reference's probe rule, a truncated end decoded again exactly.  Streams cut
+    at every length in their last 26 bytes, with and without an end marker,
+    exact / short / long capacities and both finish modes, against the oracle
+    (LzmaDec.c:775-800: the probe decides where a truncated stream stops)."""
+    import lzma
+    orc = native.oracle()
+    rng = random.Random(2605)
+    items, srcs, exp, off, doff = [], [], [], 0, 0
+    have_ref = os.path.exists(native.REF_SO)
+    for it in range(12):
+        n = rng.choice([300, 4096, 9000])
+        data = native.gen(rng.choice(["text", "runs"]), 61_000 + it, n)
+        if have_ref and it % 2:
+            props, comp = native.ref_encode(data, level=5, dict_size=1 << 16, lc=3, lp=0, pb=2,
+                                            end_mark=bool(it % 4 == 1))
+        else:
+            comp = lzma.compress(data, format=lzma.FORMAT_RAW, filters=[
+                {"id": lzma.FILTER_LZMA1, "dict_size": 1 << 16, "lc": 3, "lp": 0, "pb": 2}])
+            props = W.props_bytes(3, 0, 2, 1 << 16)
+        for cut in range(0, 26):
+            c = comp[:max(5, len(comp) - cut)]
+            cap = n + rng.choice([0, 0, 7, -3])
+            fin = rng.randrange(2)
+            items.append(dict(src_off=off, src_len=len(c), dst_off=doff, dst_cap=cap, props=props,
+                              finish=fin))
+            srcs.append(c)
+            exp.append(native.decode(orc, "orc", c, props, cap, fin))
+            off += len(c)
+            doff += cap
+    descs = L.make_descs(items)
+    plan = L.Plan()
+    r, res, dst = L.decode_batch_host(descs, b"".join(srcs), doff, _opts(L, kernel), plan)
+    assert r == 0, L.last_error()
+    bad = []
+    for k, e in enumerate(exp):
+        got = (res[k].res, res[k].status, res[k].dest_len, res[k].src_len)
+        out = dst[items[k]["dst_off"]:items[k]["dst_off"] + res[k].dest_len]
+        if got != tuple(e[:4]) or out != e[4]:
+            bad.append((k, got, e[:4]))
+    assert not bad, (kernel, len(bad), bad[:6])
+
+
 # ---------------------------------------------------------------- fuzz, every kernel
 
 _FUZZ = {}
