@@ -189,8 +189,10 @@ bool coalesce_on();
 
 template <class Set, class Coal>
 Set* free_set(Coal& C, uint32_t budget) {
-  // a second batch only while the active calls (running + pending) are fewer
-  // than half the budget: with many callers one batch at a time holds them
+  // a second batch only while the active calls (threads inside a call, or
+  // running + pending if more) are fewer than half the budget (a finished
+  // batch wakes the oldest pending call, so a call refused here is retried
+  // when the running batches end): with many callers one batch at a time holds them
   // all, while concurrent sets split them into small batches -- 256 callers
   // 124 vs 86 MB/s, DecodeToBuf loops 21 vs 12 MB/s; with few callers the
   // sets run side by side -- 16 callers 12.9 vs 19.3 MB/s
