@@ -169,3 +169,31 @@ def test_gpu_oversized_call_runs_beside_small_ones():
         assert g[0] == w[0] and g[2:] == w[2:] and (g[0] != 0 or g[1] == w[1]), (k, g[:4], w[:4])
     batches, calls, _ = L.coalesce_stats()
     assert calls == len(cases) and batches >= 2, (batches, calls)
+
+
+@pytest.mark.gpu
+def test_gpu_concurrent_decode_to_buf_loops_fuzz():
+    """Seeded zlib-like DecodeToBuf loops (LZGPU_DROPIN_FUZZ, default 120) run
+    from 24 threads at once through the drop-in (dropin_capi.hip: mirrors with
+    pooled device buffers, pinned staging, coalesced session launches): every
+    call's {res, status, srcLen, destLen}, the output and the input used equal
+    the oracle's loop (the restatement pinned to the reference's streaming
+    traces)."""
+    import lzmagpu as L
+    from test_sessions import _fuzz_sessions
+    cases = _fuzz_sessions(int(os.environ.get("LZGPU_DROPIN_FUZZ", "120")),
+                           int(os.environ.get("LZGPU_DROPIN_SEED", "919")))
+
+    def run(c):
+        return L.stream_decode(c["src"], c["props"], c["out_total"], c["in_chunk"],
+                               c["out_chunk"], c["finish"])
+
+    with ThreadPoolExecutor(24) as ex:
+        got = list(ex.map(run, cases))
+    bad = []
+    for k, (c, g) in enumerate(zip(cases, got)):
+        calls, trace, out, used = g
+        if list(map(tuple, trace)) != list(map(tuple, c["trace"])) or out != c["out"] or \
+                used != c["used"]:
+            bad.append((k, calls, trace[:2], c["trace"][:2]))
+    assert not bad, (len(bad), bad[:4])
