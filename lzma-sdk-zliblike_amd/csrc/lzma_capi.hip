@@ -243,11 +243,15 @@ static LzmaGpuLdsClass plan_lds_class(uint32_t stride, uint64_t count, uint32_t 
     lanes = std::max<uint32_t>(1, std::min<uint32_t>(32, pow2floor(std::max<uint32_t>(1, per_cu / 8))));
     groups = pow2floor(std::max<uint32_t>(1, std::min<uint32_t>(per_cu / lanes, 16)));
   } else {
-    // one lane per wave: as many waves as LDS allows, up to the 16 the
-    // register budget keeps resident; a power of two unless the caller
-    // (a merged class, persistent lanes drawing from one queue) takes any
-    groups = std::min<uint32_t>(per_cu, 16);
-    if (!any_groups) groups = pow2floor(groups);
+    // one lane per wave: as many waves as LDS allows -- counted in the CU's
+    // 1,280-byte LDS blocks (lzgpu_host::lds_groups_fit) -- up to the 16 the
+    // register budget keeps resident.  Round 1's "a power of two, 6 / 10 / 12
+    // per CU run 10-30 % slower" was this count taken in bytes: the padded
+    // slices of 6, 10, 12 or 15 workgroups do not all fit, the last one waits
+    // for the queue to drain (config 5: 15 planned, 14 resident, 5.6 GB/s;
+    // 14 planned 7.2, profiles/r05_cfg5groups/)
+    groups = std::min<uint32_t>(lzgpu_host::lds_groups_fit(size_t(stride) * 2), 16);
+    (void)any_groups;
     // Fitted latency shape (strong-scaling shares, profiles/r03_shares/): a
     // batch of 17-63 streams per CU would run one-stream waves in two or more
     // rounds; widen the waves instead so that every stream is resident at
@@ -271,8 +275,11 @@ static LzmaGpuLdsClass plan_lds_class(uint32_t stride, uint64_t count, uint32_t 
     groups = pow2floor(std::max<uint32_t>(1, std::min<uint32_t>(per_cu / lanes, 16)));
   }
   if (occ_over) groups = std::min<uint32_t>(groups, 4 * occ);
+  // every planned workgroup resident at once, in whole LDS blocks
+  const uint32_t fit = lzgpu_host::lds_groups_fit(size_t(lanes) * stride * 2);
+  while (groups > 1 && groups > fit) groups = lanes == 1 ? groups - 1 : pow2floor(groups - 1);
   const uint32_t g_over = o.groups_per_cu;
-  if (g_over > 0 && g_over * lanes <= per_cu) groups = g_over;
+  if (g_over > 0 && g_over <= fit) groups = g_over;
   c.n = count;
   c.lanes_per_group = lanes;
   c.lds_cells_per_lane = stride;

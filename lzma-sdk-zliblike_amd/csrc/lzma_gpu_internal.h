@@ -67,6 +67,27 @@ extern "C" int lzgpu_launch_delta(uint8_t* d_data, const uint64_t* d_off, const 
 
 // host-side helpers shared by the C-ABI translation units (lzma_capi.hip)
 namespace lzgpu_host {
+
+// LDS is given to a workgroup in whole blocks: 128 blocks of 1,280 bytes make a
+// CU's 160 KiB (measured, profiles/r05_cfg5groups/: a launch padded to 160 KiB
+// / 15 = 10,752 bytes per workgroup fitted 14 per CU, not 15 -- 9 blocks
+// each).  Workgroup counts and the LDS padding that forces them are computed in
+// blocks.
+constexpr uint32_t kLdsBytesPerCu = 160u * 1024u;
+constexpr uint32_t kLdsGrain = 1280u;
+constexpr uint32_t kLdsBlocksPerCu = kLdsBytesPerCu / kLdsGrain;
+inline uint32_t lds_blocks(size_t bytes) {
+  return uint32_t((bytes + kLdsGrain - 1) / kLdsGrain);
+}
+// workgroups of `bytes` of LDS that fit a CU at once
+inline uint32_t lds_groups_fit(size_t bytes) {
+  const uint32_t b = lds_blocks(bytes);
+  return b ? kLdsBlocksPerCu / b : 0xFFFFu;
+}
+// the most LDS each of `groups` workgroups can take with all of them resident
+inline size_t lds_share(uint32_t groups) {
+  return size_t(kLdsBlocksPerCu / (groups ? groups : 1u)) * kLdsGrain;
+}
 bool ensure_device();
 void set_error(const char* what);
 bool hip_ok(hipError_t e, const char* what);

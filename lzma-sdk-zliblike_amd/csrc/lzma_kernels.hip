@@ -248,7 +248,7 @@ static uint32_t window_bytes(uint64_t grid, size_t table_bytes, uint32_t groups_
   uint64_t per_cu = (grid + cus - 1) / cus;
   if (groups_per_cu && per_cu > groups_per_cu) per_cu = groups_per_cu;
   if (per_cu == 0) per_cu = 1;
-  const size_t share = (size_t(160 * 1024) / per_cu) & ~size_t(511);
+  const size_t share = lzgpu_host::lds_share(per_cu);
   const size_t tb = (table_bytes + 15) & ~size_t(15);
   if (share <= tb + 4096) return 0;
   uint32_t w = 1u << 17;
@@ -302,7 +302,7 @@ static int launch_lds(const LzmaGpuStreamDesc* d_descs, const uint32_t* d_order,
   // interleaved slices take whole 32-lane rows
   size_t lds = size_t(lds_ilv<M>() ? (lanes + kIlv - 1) / kIlv * kIlv : lanes) * stride * 2;
   if (groups_per_cu) {
-    const size_t share = (size_t(160 * 1024) / groups_per_cu) & ~size_t(511);
+    const size_t share = lzgpu_host::lds_share(groups_per_cu);
     if (share > lds) lds = share;
   }
   uint32_t grid = (n + lanes - 1) / lanes;
@@ -355,7 +355,7 @@ static int launch_coop(const LzmaGpuStreamDesc* d_descs, const uint32_t* d_order
   if (win) {
     lds = ((lds + 15) & ~size_t(15)) + win;
   } else if (groups_per_cu) {
-    const size_t share = (size_t(160 * 1024) / groups_per_cu) & ~size_t(511);
+    const size_t share = lzgpu_host::lds_share(groups_per_cu);
     if (share > lds) lds = share;
   }
   hipLaunchKernelGGL(kfn, dim3(grid), dim3(32), lds, stream, d_descs, d_order, n, d_src, d_dst,

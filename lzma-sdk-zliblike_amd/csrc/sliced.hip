@@ -318,7 +318,7 @@ size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 
 // workgroups of `cells` staged cells (+ the lane kernel's flag word) per CU, <= 16
 uint32_t lds_fit(uint32_t cells) {
-  return uint32_t(std::min<size_t>(16, (160 * 1024) / align_up(size_t(cells) * 2 + 16, 512)));
+  return std::min<uint32_t>(16, lzgpu_host::lds_groups_fit(size_t(cells) * 2 + 16));
 }
 
 SRes plan_sliced(LzmaGpuStreamDesc* descs, size_t n, uint64_t slice, unsigned kernel,
@@ -460,8 +460,7 @@ SRes decode_sliced(const LzmaGpuSlicedPlan* p, const LzmaGpuStreamDesc* d_descs,
   const uint32_t lds_words = sliced_vec(stage_cells) * 4u;
   const size_t lds = size_t(lds_words) * 4 + 16;
   // pad every workgroup's LDS so that exactly groups_per_cu fit on a CU
-  const size_t lds_pad =
-      std::max(lds, (size_t(160 * 1024) / std::max<uint32_t>(p->groups_per_cu, 1)) & ~size_t(511));
+  const size_t lds_pad = std::max(lds, lzgpu_host::lds_share(std::max<uint32_t>(p->groups_per_cu, 1)));
   auto round_args = [&](unsigned r, uint32_t c) {
     SlicedRound a;
     a.sess = sess;
