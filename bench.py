@@ -298,7 +298,7 @@ def plan_kernels(plan):
         dup = int(os.environ.get("LZGPU_DUP", "32") or 0)  # lzma_kernels.hip kLaneDup
         if m & 0x80000000:
             k = "lzgpu_decode_coop_kernel"
-        elif m == 0x1BF and int(c.lanes_per_group) == 1 and 1 < dup <= 64:
+        elif m in (0x1BF, 0x19F) and int(c.lanes_per_group) == 1 and 1 < dup <= 64:
             k = "lzgpu_decode_dup_kernel"  # one-stream waves on all 32 lanes
         else:
             k = "lzgpu_decode_lds_kernel"

@@ -374,6 +374,12 @@ typedef struct LzmaGpuPlanOptions {
  * (LZGPU_THR_FIT=0). */
 #define LZMA_GPU_PLAN_NO_THR_FIT 64u
 
+/* Default: a one-lane latency class with more streams per CU than its widest
+ * slice lets resident (lc + lp = 4 at pb = 4 takes 9 of a CU's 128 LDS blocks:
+ * 14 workgroups) keeps its slot trees in the global rows instead, 8 blocks and
+ * 16 workgroups per CU.  This flag keeps them in LDS (LZGPU_SLOTG=0). */
+#define LZMA_GPU_PLAN_NO_SLOTG 128u
+
 /* LzmaGpu_PlanBatchEx with explicit options (opt == NULL: as PlanBatchEx,
  * whose defaults take the LZGPU_* experiment variables of the environment,
  * read per call).  SZ_ERROR_PARAM on an unknown kernel value. */

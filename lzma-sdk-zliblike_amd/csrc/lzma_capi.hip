@@ -127,6 +127,16 @@ static uint64_t plan_workspace(LzmaGpuStreamDesc* descs, size_t n, std::vector<u
   return off * 2;
 }
 
+// LDS cells of an item's slice under the slot-global latency placement
+// (lzgpu::kLdsMaskLatSlotG); 0 = bad props
+static uint32_t lat_slotg_cells(const LzmaGpuStreamDesc& d) {
+  if (d.kind == LZMA_GPU_KIND_LZMA2)
+    return d.props[0] <= 40 ? lzgpu::lzma2_lds_cells(lzgpu::kLdsMaskLatSlotG) : 0u;
+  uint32_t lc, lp, pb, dict;
+  if (lzgpu::lz_props_parse(d.props, d.props_size, lc, lp, pb, dict) != SZ_OK) return 0;
+  return lzgpu::make_layout(lc, lp, pb, lzgpu::kLdsMaskLatSlotG).lds_cells;
+}
+
 static size_t plan_simple(LzmaGpuStreamDesc* descs, size_t n, uint32_t* order) {
   std::vector<uint32_t> w;
   const uint64_t bytes = plan_workspace(descs, n, &w);
@@ -155,7 +165,8 @@ size_t LzmaGpu_PlanBatch(LzmaGpuStreamDesc* descs, size_t n, uint32_t* order) {
 // call time (LZGPU_KERNEL=global|throughput|latency|coop, LZGPU_MASK=1|2,
 // LZGPU_COOP=0|1, LZGPU_CUS, LZGPU_LANES, LZGPU_GROUPS, LZGPU_OCC,
 // LZGPU_PERSIST=0, LZGPU_CLASSES=1, LZGPU_SLICE_ALIGN8=1, LZGPU_KERNEL_LZMA2=1,
-// LZGPU_COOP_LAT=1, LZGPU_MERGE_LAT=0, LZGPU_ILV=0, LZGPU_ILV_ANY=1, LZGPU_THR_FIT=0).  Only LzmaGpu_PlanBatchEx reads them;
+// LZGPU_COOP_LAT=1, LZGPU_MERGE_LAT=0, LZGPU_ILV=0, LZGPU_ILV_ANY=1, LZGPU_THR_FIT=0,
+// LZGPU_SLOTG=0).  Only LzmaGpu_PlanBatchEx reads them;
 // LzmaGpu_PlanBatchOpt takes its options from the caller alone.
 static LzmaGpuPlanOptions env_options() {
   LzmaGpuPlanOptions o;
@@ -187,7 +198,8 @@ static LzmaGpuPlanOptions env_options() {
             (env_int("LZGPU_MERGE_LAT", 1) ? 0u : LZMA_GPU_PLAN_NO_MERGE_LAT) |
             (env_int("LZGPU_ILV", 1) ? 0u : LZMA_GPU_PLAN_NO_ILV) |
             (env_int("LZGPU_ILV_ANY", 0) ? LZMA_GPU_PLAN_ILV_ANY : 0u) |
-            (env_int("LZGPU_THR_FIT", 1) ? 0u : LZMA_GPU_PLAN_NO_THR_FIT);
+            (env_int("LZGPU_THR_FIT", 1) ? 0u : LZMA_GPU_PLAN_NO_THR_FIT) |
+            (env_int("LZGPU_SLOTG", 1) ? 0u : LZMA_GPU_PLAN_NO_SLOTG);
   return o;
 }
 
@@ -229,8 +241,8 @@ static LzmaGpuLdsClass plan_lds_class(uint32_t stride, uint64_t count, uint32_t 
   //  * latency -- few streams per CU (small batches, or wide lc+lp tables):
   //    one stream per wave, 16 waves per CU (config 2: 5.8 GB/s vs 2.5 GB/s
   //    with 4 lanes x 4 waves; config 5: 2.6 GB/s vs 2.2 GB/s with 2 lanes).
-  // Workgroups per CU stay a power of two so the four SIMDs carry equal
-  // loads (6, 10 or 12 ran 10-30 % slower).
+  // Throughput shapes keep lanes and workgroups per CU powers of two; every
+  // count is checked in LDS blocks below (lds_groups_fit).
   auto pow2floor = [](uint32_t v) {
     while (v & (v - 1)) v &= v - 1;
     return v;
@@ -383,6 +395,20 @@ static SRes plan_batch(LzmaGpuStreamDesc* descs, size_t n, uint32_t* order, Lzma
         }
       }
     }
+    // more streams per CU than the widest slice lets resident: the slot trees
+    // to the global rows where that fits more one-stream workgroups per CU
+    // (config 5: 14 -> 16)
+    if (c.lds_mask == LZGPU_LDS_MASK_LAT && c.lanes_per_group == 1 && c.groups_per_cu < 16 &&
+        per_cu_batch > c.groups_per_cu && !(o.flags & LZMA_GPU_PLAN_NO_SLOTG)) {
+      uint32_t stride_sg = 0;
+      for (uint32_t i : idx) stride_sg = std::max(stride_sg, lat_slotg_cells(descs[i]));
+      if (stride_sg != 0 && stride_sg <= kMaxLdsCells) {
+        const LzmaGpuLdsClass cs =
+            plan_lds_class(stride_sg, idx.size(), lzgpu::kLdsMaskLatSlotG, cus,
+                           o.kernel == LZMA_GPU_KERNEL_AUTO ? 0 : 2, o, nullptr, any_groups);
+        if (cs.lanes_per_group == 1 && cs.groups_per_cu > c.groups_per_cu) c = cs;
+      }
+    }
     return c;
   };
   // Several buckets in the one-lane latency regime (mixed-props batches,
@@ -398,7 +424,9 @@ static SRes plan_batch(LzmaGpuStreamDesc* descs, size_t n, uint32_t* order, Lzma
     for (int b = 0; b < LZMA_GPU_MAX_CLASSES; ++b) {
       if (bucket_idx[b].empty()) continue;
       const LzmaGpuLdsClass c = plan_bucket(bucket_idx[b], bucket_stride[b], false);
-      if (c.lds_mask == LZGPU_LDS_MASK_LAT && c.lanes_per_group == 1) lat_b[n_lat++] = b;
+      if ((c.lds_mask == LZGPU_LDS_MASK_LAT || c.lds_mask == lzgpu::kLdsMaskLatSlotG) &&
+          c.lanes_per_group == 1)
+        lat_b[n_lat++] = b;
     }
     if (n_lat >= 2) {
       const int t = lat_b[0];

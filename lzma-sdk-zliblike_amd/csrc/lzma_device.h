@@ -172,6 +172,11 @@ __host__ __device__ inline uint32_t num_probs(uint32_t lc, uint32_t lp) {
 #ifndef LZGPU_LDS_MASK_LAT
 #define LZGPU_LDS_MASK_LAT 0x1BFu
 #endif
+// The latency placement with the slot trees in the global rows: a merged
+// latency class whose widest slice (lc + lp = 4 at pb = 4: 5,316 cells) would
+// take 9 of a CU's 128 LDS blocks runs 16 workgroups per CU at 8 blocks
+// instead of 14 (the planner picks it only where it raises residency).
+constexpr uint32_t kLdsMaskLatSlotG = LZGPU_LDS_MASK_LAT & ~(1u << S_SLOT);
 
 // Explicit address spaces: LDS (3) for the lo table of the fast kernel, global
 // (1) for everything else.  Generic pointers would compile to flat_* memory

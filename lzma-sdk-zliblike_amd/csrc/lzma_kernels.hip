@@ -288,6 +288,34 @@ extern "C" int lzgpu_launch_decode_batch(const LzmaGpuStreamDesc* d_descs, const
   return hipGetLastError() == hipSuccess ? 0 : -1;
 }
 
+// One-stream waves on kLaneDup lanes (lzgpu_decode_dup_kernel): `groups_per_cu`
+// one-wave workgroups per CU, each padded to its share of the CU's LDS blocks.
+template <int W, uint32_t M, bool K2>
+static int launch_dup(const LzmaGpuStreamDesc* d_descs, const uint32_t* d_order, uint32_t n,
+                      const uint8_t* d_src, uint8_t* d_dst, uint16_t* d_ws,
+                      LzmaGpuResult* d_results, uint32_t stride, uint32_t groups_per_cu,
+                      uint32_t max_groups, uint32_t* d_queue, uint32_t dup, hipStream_t stream) {
+  auto kd = lzgpu_decode_dup_kernel<W, M, K2>;
+  if (allow_full_lds(reinterpret_cast<const void*>(kd)) != 0) return -1;
+  if (hipMemsetAsync(d_queue, 0, sizeof(uint32_t), stream) != hipSuccess) return -1;
+  size_t lds = size_t(stride) * 2;
+  if (groups_per_cu) lds = std::max(lds, lzgpu_host::lds_share(groups_per_cu));
+  uint32_t grid = n;
+  if (max_groups && grid > max_groups) grid = max_groups;
+  hipLaunchKernelGGL(kd, dim3(grid), dim3(dup), lds, stream, d_descs, d_order, n, d_src, d_dst,
+                     d_ws, d_results, stride, d_queue);
+  return hipGetLastError() == hipSuccess ? 0 : -1;
+}
+
+// kLaneDup, or LZGPU_DUP=D for A/B (D = 1 launches the one-lane kernel)
+static int lane_dup() {
+  static const int dup = [] {
+    const char* e = getenv("LZGPU_DUP");
+    return e ? atoi(e) : kLaneDup;
+  }();
+  return dup;
+}
+
 template <int W, uint32_t M, bool K2>
 static int launch_lds(const LzmaGpuStreamDesc* d_descs, const uint32_t* d_order, uint32_t n,
                       const uint8_t* d_src, uint8_t* d_dst, uint16_t* d_ws,
@@ -318,12 +346,8 @@ static int launch_lds(const LzmaGpuStreamDesc* d_descs, const uint32_t* d_order,
   }
   const uint32_t lanes_total = grid * lanes;
   if constexpr (M == LZGPU_LDS_MASK_LAT) {
-    // one-stream waves: kLaneDup lanes per stream (LZGPU_DUP=D overrides for
-    // A/B; D = 1 launches the one-lane kernel)
-    static const int dup = [] {
-      const char* e = getenv("LZGPU_DUP");
-      return e ? atoi(e) : kLaneDup;
-    }();
+    // one-stream waves: kLaneDup lanes per stream
+    const int dup = lane_dup();
     if (lanes == 1 && dup > 1 && dup <= 64) {
       auto kd = lzgpu_decode_dup_kernel<W, M, K2>;
       if (allow_full_lds(reinterpret_cast<const void*>(kd)) != 0) return -1;
@@ -428,6 +452,23 @@ static int launch_class(const LzmaGpuStreamDesc* d_descs, const uint32_t* d_orde
     return launch_coop<4, MC, K2, MC | kWinBit>(d_descs, d_order, n, d_src, d_dst, d_ws, d_results,
                                                 stride, groups_per_cu, max_groups, d_queue,
                                                 stream);
+  }
+  if (lds_mask == kLdsMaskLatSlotG) {
+    // planned for one-stream workgroups only (lzma_capi.hip plan_bucket)
+    const int dup = lane_dup();
+    if (lanes != 1 || dup <= 1 || dup > 64) return -1;
+    const uint32_t w = std::min(waves_per_simd, resident_waves_per_simd(n, groups_per_cu));
+    if (w <= 1)
+      return launch_dup<1, kLdsMaskLatSlotG, K2>(d_descs, d_order, n, d_src, d_dst, d_ws,
+                                                 d_results, stride, groups_per_cu, max_groups,
+                                                 d_queue, uint32_t(dup), stream);
+    if (w == 2)
+      return launch_dup<2, kLdsMaskLatSlotG, K2>(d_descs, d_order, n, d_src, d_dst, d_ws,
+                                                 d_results, stride, groups_per_cu, max_groups,
+                                                 d_queue, uint32_t(dup), stream);
+    return launch_dup<4, kLdsMaskLatSlotG, K2>(d_descs, d_order, n, d_src, d_dst, d_ws, d_results,
+                                               stride, groups_per_cu, max_groups, d_queue,
+                                               uint32_t(dup), stream);
   }
   if (lds_mask == LZGPU_LDS_MASK_LAT)
     return launch_lds_w<LZGPU_LDS_MASK_LAT, K2>(d_descs, d_order, n, d_src, d_dst, d_ws,

@@ -35,6 +35,9 @@ EMU_VARIANTS = {
     "lit_batch_32": "-DLZGPU_LIT_BATCH=32",
     "match_fat_global_len": "-DLZGPU_LDS_MASK_LAT=0x105 -DLZGPU_LDS_MASK=0x107 -DEMU_LAT_MASK",
     "latency_instantiation": "-DEMU_LAT_MASK",
+    # round 5: the latency placement with the slot trees global (the planner's
+    # choice for classes whose widest slice would cost workgroups per CU)
+    "latency_slot_global": "-DLZGPU_LDS_MASK_LAT=0x19F -DEMU_LAT_MASK",
     "interleaved_global_instantiation": "-DEMU_ILV",
     "coop_instantiation": "-DEMU_COOP",
     "coop_all_lds_instantiation": "-DEMU_COOP_ALL",

@@ -34,6 +34,7 @@ pytestmark = pytest.mark.gpu
 
 COOP = 0x80000000
 M_THR, M_LAT, M_ALL = 0x105, 0x1BF, 0x7FF
+M_LAT_SG = 0x19F  # the latency placement with the slot trees global (kLdsMaskLatSlotG)
 RES_DT = np.dtype([("res", "<i4"), ("status", "<i4"), ("dest_len", "<u8"), ("src_len", "<u8")])
 # coop: the cooperative kernel, every table section in LDS where the table fits
 # (placement 0x7FF); coop_lat: the same kernel on the latency placement 0x1BF
@@ -85,7 +86,8 @@ def _check_plan(plan, kernel):
             if ilv:
                 assert c.slot_cells > 0 and c.slot_groups > 0 and c.slot_off % 64 == 0
         elif kernel == "latency":
-            assert c.lds_mask == M_LAT and c.lanes_per_group == 1, hex(c.lds_mask)
+            # the slot trees go global where that fits more workgroups per CU
+            assert c.lds_mask in (M_LAT, M_LAT_SG) and c.lanes_per_group == 1, hex(c.lds_mask)
         elif kernel == "coop":
             # all sections in LDS where the whole table fits the class's
             # streams per CU, else the latency placement
@@ -474,17 +476,19 @@ def test_cfg5_full_count_mixed_props(L, torch):
     comp = np.frombuffer(b"".join(p[1] for p in parts), dtype=np.uint8)
     plain = b"".join(p[0] for p in parts)
     # the planner's default: the four width buckets all land in the one-lane
-    # latency regime and are merged into one class (one launch, 14 workgroups
-    # per CU for the widest slice: 10,636 bytes = 9 of the CU's 128 LDS blocks
-    # of 1,280 bytes); LZMA_GPU_PLAN_NO_MERGE_LAT: four classes
+    # latency regime and are merged into one class (one launch; its widest
+    # slice, 10,636 bytes = 9 of the CU's 128 LDS blocks of 1,280 bytes, would
+    # allow 14 workgroups per CU, so the slot trees go global: 8 blocks, 16
+    # per CU); LZMA_GPU_PLAN_NO_MERGE_LAT: four classes
     # launched concurrently on forked streams
     for opts, n_classes in ((None, 1), (L.plan_options("auto", flags=8), 4)):
         plan, res, d_dst = _device_decode(L, torch, descs, comp, int(nout.sum()), opts)
         masks = sorted(plan.classes[k].lds_mask for k in range(plan.n_classes))
-        assert plan.n_classes == n_classes and plan.n_lds == count and set(masks) == {M_LAT}, \
-            masks
+        assert plan.n_classes == n_classes and plan.n_lds == count and \
+            set(masks) <= {M_LAT, M_LAT_SG}, masks
         if n_classes == 1:
-            assert plan.classes[0].groups_per_cu == 14 and plan.classes[0].lanes_per_group == 1
+            assert plan.classes[0].groups_per_cu == 16 and plan.classes[0].lanes_per_group == 1
+            assert plan.classes[0].lds_mask == M_LAT_SG
         # FINISH_END reads the end mark (FINISHED_WITH_MARK); FINISH_ANY stops
         # at destLen in front of it (NOT_FINISHED)
         want_status = np.where(fin == 1, 1, 2)
