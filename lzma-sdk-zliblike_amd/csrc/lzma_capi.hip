@@ -1027,7 +1027,7 @@ CallScratch* scratch_acquire() {
 uint8_t* scratch_pinned(CallScratch* s, size_t n) {
   if (!s || n > kPinnedStageMax) return nullptr;
   if (s->pin_cap >= n) return s->pin;
-  const size_t want = std::min(kPinnedStageMax, std::max({n, s->pin_cap * 2, size_t(1) << 20}));
+  const size_t want = std::min(kPinnedStageMax, std::max({n, s->pin_cap * 2, size_t(256) << 10}));
   if (s->pin) (void)hipHostFree(s->pin);
   s->pin = nullptr;
   s->pin_cap = 0;

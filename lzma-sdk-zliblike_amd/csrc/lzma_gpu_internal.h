@@ -161,7 +161,7 @@ struct CallScratch {
 CallScratch* scratch_acquire();  // current device; nullptr (error set) on failure
 void scratch_release(CallScratch* s);
 // The scratch's pinned host staging, at least n bytes (grown geometrically from
-// 1 MiB, at most kPinnedStageMax); nullptr when n is larger or the allocation
+// 256 KiB, at most kPinnedStageMax); nullptr when n is larger or the allocation
 // fails -- the caller then copies from / to pageable memory directly.  A
 // pageable hipMemcpyAsync goes through the runtime's own staging buffer, one
 // per device, so concurrent callers' small copies queue behind each other.
