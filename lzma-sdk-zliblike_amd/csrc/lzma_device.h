@@ -51,6 +51,9 @@ enum : int { kOk = 0, kErrData = 1, kErrMem = 2, kErrUnsupported = 4, kErrParam 
 // internal (never returned to a caller): the fast tail of a one-shot decode
 // met a symbol that needs input past the stream's end; decode it again exactly
 constexpr int kRetryExact = 99;
+#ifndef LZGPU_LEN_PF
+#define LZGPU_LEN_PF 0  // 1: length coders preloaded ahead of the literal batch (unmeasured A/B)
+#endif
 #ifndef LZGPU_FAST_TAIL
 #define LZGPU_FAST_TAIL 1  // 0: probe every symbol of the last 20 bytes (A/B)
 #endif
@@ -1431,6 +1434,24 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
     // that sit in literal runs keep decoding together instead of idling
     // behind a neighbour's match path on every symbol.
     bool is_match = false, stop = false;
+    // Throughput placement with pb = 0 (every symbol in posState 0): both
+    // length coders' choice bit and low tree (lengths 2..9) are loaded here,
+    // ahead of the literal batch's byte stores.  On gfx950 loads and stores
+    // share one in-order vmcnt queue, so the match path's first global load
+    // otherwise waits for every store of the batch to drain.
+    constexpr bool kLenPf = LZGPU_LEN_PF != 0 && (M & ~kIlvBit) == LZGPU_LDS_MASK;
+    // plain scalars, not arrays: a select between two array elements becomes
+    // a load through a selected pointer and puts the array in scratch
+    uint32_t ca = 0, cb = 0, a1 = 0, a2 = 0, a3 = 0, a4 = 0, a5 = 0, a6 = 0, a7 = 0;
+    uint32_t b1 = 0, b2 = 0, b3 = 0, b4 = 0, b5 = 0, b6 = 0, b7 = 0;
+    if constexpr (kLenPf) {
+      if (pb == 0) {
+        auto l0 = T.g(T.L.o[S_LEN]);
+        auto l1 = T.g(T.L.o[S_REPLEN]);
+        ca = l0[0]; a1 = l0[3]; a2 = l0[4]; a3 = l0[5]; a4 = l0[6]; a5 = l0[7]; a6 = l0[8]; a7 = l0[9];
+        cb = l1[0]; b1 = l1[3]; b2 = l1[4]; b3 = l1[5]; b4 = l1[6]; b5 = l1[7]; b6 = l1[8]; b7 = l1[9];
+      }
+    }
     // lanes leave the batch by clearing lit_on, the loop itself exits only
     // when the whole wave is done: no divergent exit, so no per-iteration
     // copies of the lane state into exit registers
@@ -1590,6 +1611,21 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
           len = rc.dec3(mid_t, 1, cmid);
         else
           len = 16 + rc.tree8_g(T.template at<S_LENHI>(lcoder_is_rep << 8)) - 256;
+        } else if (kLenPf && pb == 0) {
+        const bool r = lcoder_is_rep != 0;
+        if (!rc.bit_v(r ? cb : ca, lbase)) {
+          // the low tree (lbase + 2, root 1) from the preloaded cells
+          auto lt = lbase + 2;
+          const uint32_t d0 = rc.bit_v(r ? b1 : a1, lt + 1);
+          const uint32_t d1 = rc.bit_v(d0 ? (r ? b3 : a3) : (r ? b2 : a2), lt + 2 + d0);
+          const uint32_t p2 = d0 ? (d1 ? (r ? b7 : a7) : (r ? b6 : a6)) : (d1 ? (r ? b5 : a5) : (r ? b4 : a4));
+          const uint32_t d2 = rc.bit_v(p2, lt + 4 + 2 * d0 + d1);
+          len = 4 * d0 + 2 * d1 + d2;
+        }
+        else if (!rc.bit(lbase + 1))
+          len = 8 + rc.sub3(lbase + 10, 1) - 8;
+        else
+          len = 16 + rc.template tree<8>(T.template at<S_LENHI>(lcoder_is_rep << 8));
         } else {
         const uint32_t ch = lbase[0];
         auto lo_t = lbase + 2 + (ps << 3);

@@ -38,6 +38,10 @@ EMU_VARIANTS = {
     # round 5: the latency placement with the slot trees global (the planner's
     # choice for classes whose widest slice would cost workgroups per CU)
     "latency_slot_global": "-DLZGPU_LDS_MASK_LAT=0x19F -DEMU_LAT_MASK",
+    # round 5 (opt-in, GPU A/B pending): length coders preloaded ahead of the
+    # literal batch in the throughput placement (pb = 0 streams)
+    "length_preload": "-DLZGPU_LEN_PF=1",
+    "length_preload_interleaved": "-DLZGPU_LEN_PF=1 -DEMU_ILV",
     "interleaved_global_instantiation": "-DEMU_ILV",
     "coop_instantiation": "-DEMU_COOP",
     "coop_all_lds_instantiation": "-DEMU_COOP_ALL",
