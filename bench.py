@@ -612,9 +612,20 @@ def build_cfg4_unique(workers):
 def print_prof(L):
     """Region cycles and counters of a profiling build (LZGPU_PROF), else nothing."""
     if hasattr(L.lib, "LzmaGpu_ProfileRead"):  # profiling variant builds only
-        buf = (ctypes.c_ulonglong * 24)()
+        buf = (ctypes.c_ulonglong * 40)()
         L.lib.LzmaGpu_ProfileRead(buf, 0)
         lanes = max(1, buf[23])
+        if buf[22] == 3:
+            # wait attribution (lzma_device.h LZGPU_PROF=3): cycles per stream the
+            # wave spent in forced vmcnt(0) waits, by class, and the stream's total
+            w = ("drain_stores", "matched_literal", "rep", "length", "slot", "specpos", "align",
+                 "lenhigh", "copy_region", "matched_byte", "input", "prev_probe")
+            prof = {k: buf[24 + i] / lanes for i, k in enumerate(w)}
+            prof["stream_total"] = buf[3] / lanes
+            prof["bytes"] = buf[12] / lanes
+            log("PROF3 per stream (cycles, wave time per lane): " + json.dumps(
+                {k: round(v) for k, v in prof.items()}))
+            return
         # "a|b|c": the counter's meaning in the per-lane (PROF=2) / global-slot /
         # LDS-slot (cooperative, round 4) builds
         names = ("literal_batches", "match_decode", "copy_tail", "decode_to_dic_total",

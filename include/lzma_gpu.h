@@ -32,9 +32,14 @@
  *     fork's LzmaDec.c:945 debug printf); Lzma2Decode initialises its state
  *     (the reference one-call omits Lzma2Dec_Init, which is undefined
  *     behaviour); a dicLimit beyond dicBufSize returns SZ_ERROR_PARAM instead
- *     of writing out of bounds; without a usable HIP device every decode entry
- *     returns SZ_ERROR_FAIL and LzmaGpu_LastError() says why (there is no CPU
- *     fallback).
+ *     of writing out of bounds; after an LzmaDec_DecodeToDic / DecodeToBuf call
+ *     that returns SZ_ERROR_DATA, dic[dicPos, ...) keeps its previous contents
+ *     (the reference leaves the failed pass's partly decoded bytes there:
+ *     LzmaDec.c:366-379 returns before the dicPos write-back at :413-423; the
+ *     drop-in downloads only dic[old dicPos, new dicPos) -- both are bytes past
+ *     dicPos, which the reference's contract never defines); without a usable
+ *     HIP device every decode entry returns SZ_ERROR_FAIL and LzmaGpu_LastError()
+ *     says why (there is no CPU fallback).
  *
  *  2. The batch extension (new): many independent streams per launch, all
  *     buffers caller-owned device memory, no allocation inside the call.
@@ -378,11 +383,16 @@ typedef struct LzmaGpuPlanOptions {
  * slice lets resident (lc + lp = 4 at pb = 4 takes 9 of a CU's 128 LDS blocks:
  * 14 workgroups) keeps its slot trees in the global rows instead, 8 blocks and
  * 16 workgroups per CU.  This flag keeps them in LDS (LZGPU_SLOTG=0). */
-#define LZMA_GPU_PLAN_NO_SLOTG 128u
+#define LZMA_GPU_PLAN_NO_SLOTG 256u
+/* 128u was LZMA_GPU_PLAN_STEP (round 4's decision-level kernel, removed in
+ * round 5): reserved, rejected with SZ_ERROR_PARAM so that a caller built
+ * against the old header is told rather than silently given another flag. */
+#define LZMA_GPU_PLAN_KNOWN_FLAGS 0x17Fu
 
 /* LzmaGpu_PlanBatchEx with explicit options (opt == NULL: as PlanBatchEx,
  * whose defaults take the LZGPU_* experiment variables of the environment,
- * read per call).  SZ_ERROR_PARAM on an unknown kernel value. */
+ * read per call).  SZ_ERROR_PARAM on an unknown kernel value or a flag bit
+ * outside LZMA_GPU_PLAN_KNOWN_FLAGS. */
 SRes LzmaGpu_PlanBatchOpt(LzmaGpuStreamDesc *descs, size_t n, uint32_t *order, LzmaGpuPlan *plan,
                           const LzmaGpuPlanOptions *opt);
 

@@ -131,6 +131,7 @@ struct BatchSet {
   DevBuf io, ws, meta;
   hipStream_t stream = nullptr;
   bool busy = false;
+  bool broken = false;  // its stream could not be created: not picked (group_commit)
 };
 
 // Batches in flight per device at once (LZGPU_COALESCE_INFLIGHT=1..8, default
@@ -200,8 +201,29 @@ Set* free_set(Coal& C, uint32_t budget) {
   const size_t active = std::max<size_t>(C.in_flight + C.pending.size(), C.callers.load());
   if (C.in_flight != 0 && active >= budget / 2) return nullptr;
   for (int i = 0; i < in_flight_limit(); ++i)
-    if (!C.sets[i].busy) return &C.sets[i];
+    if (!C.sets[i].busy && !C.sets[i].broken) return &C.sets[i];
   return nullptr;
+}
+template <class Coal>
+bool all_sets_broken(const Coal& C) {
+  for (int i = 0; i < in_flight_limit(); ++i)
+    if (!C.sets[i].broken) return false;
+  return true;
+}
+// A batch set's stream.  LZGPU_FAULT_STREAM_CREATE=N (fault injection for
+// tests/test_coalesce.py only) makes the first N creations in the process fail.
+bool create_set_stream(hipStream_t* st) {
+  static std::atomic<int> fail_left{[] {
+    const char* e = getenv("LZGPU_FAULT_STREAM_CREATE");
+    return e ? atoi(e) : 0;
+  }()};
+  if (fail_left.load() > 0 && fail_left.fetch_sub(1) > 0) return false;
+  if (hipStreamCreateWithFlags(st, hipStreamNonBlocking) != hipSuccess) {
+    (void)hipGetLastError();
+    *st = nullptr;
+    return false;
+  }
+  return true;
 }
 template <class Coal, class Set>
 void wake_next(Coal& C, uint32_t budget) {
@@ -215,16 +237,28 @@ void group_commit(Coal& C, Call& me, uint32_t budget, Run run, Fail stream_faile
   while (!me.done) {
     Set* R = me.taken ? nullptr : free_set<Set>(C, budget);
     if (!R) {
+      if (!me.taken && C.in_flight == 0 && all_sets_broken(C)) {
+        // no set has a stream and no batch runs: fail this call
+        // and wake every pending one, which fails the same way -- nobody
+        // waits for a batch that cannot come; the last one clears the marks,
+        // so later calls try to create the streams again
+        C.pending.erase(std::find(C.pending.begin(), C.pending.end(), &me));
+        stream_failed(me);
+        me.taken = me.done = true;
+        for (Call* c : C.pending) c->cv.notify_one();
+        if (C.pending.empty())
+          for (auto& x : C.sets) x.broken = false;
+        return;
+      }
       me.cv.wait(lk);
       continue;
     }
-    if (!R->stream && hipStreamCreateWithFlags(&R->stream, hipStreamNonBlocking) != hipSuccess) {
-      (void)hipGetLastError();
-      R->stream = nullptr;
-      C.pending.erase(std::find(C.pending.begin(), C.pending.end(), &me));
-      stream_failed(me);
-      me.taken = me.done = true;
-      return;
+    if (!R->stream && !create_set_stream(&R->stream)) {
+      // this set cannot run batches: leave it out and try again -- another
+      // set, the end of a running batch (which wakes the next pending call),
+      // or the failure above when no set is left
+      R->broken = true;
+      continue;
     }
     std::vector<Call*> batch;
     if (!coalesce_on()) {  // one launch per call: this one now
@@ -313,6 +347,11 @@ constexpr size_t kBulkOutMax = size_t(64) << 20;
 // workspace and metadata take a quarter): 256 coalesced 4 KiB calls need
 // ~1.6 MB, so steady traffic never regrows them.
 constexpr size_t kSetFloor = size_t(4) << 20;
+// Largest pinned staging a batch set keeps: the doubling stops
+// here, and a batch that would need more -- an oversized call run alone, up to
+// 256 MiB of input -- stages through pageable memory instead of leaving every
+// set holding that much pinned memory for the life of the process.
+constexpr size_t kSetPinMax = kBulkOutMax + (size_t(32) << 20);
 
 // One batch of calls on the current device (the leader, C.mu not held).
 void run_batch(BatchSet& C, const std::vector<OneCall*>& b) {
@@ -355,13 +394,21 @@ void run_batch(BatchSet& C, const std::vector<OneCall*>& b) {
   pc.mark(kTPlan);
   const size_t meta_bytes = align16(k * sizeof(LzmaGpuStreamDesc)) + align16(k * sizeof(uint32_t));
   const size_t res_bytes = align16(k * sizeof(LzmaGpuResult));
-  const bool bulk_out = out_total <= kBulkOutMax;
-  const size_t pin_need = in_total + meta_bytes + res_bytes + (bulk_out ? out_total : 0) + 64;
-  if (C.pin_cap < pin_need) {
-    // grow geometrically from 4 MiB: a run of slightly larger batches
-    // reallocates (and synchronises the device, hipHostFree / hipHostMalloc,
-    // stalling the other sets' batches) O(log) times
-    const size_t want = std::max({pin_need, C.pin_cap * 2, kSetFloor});
+  bool bulk_out = out_total <= kBulkOutMax;
+  size_t pin_need = in_total + meta_bytes + res_bytes + (bulk_out ? out_total : 0) + 64;
+  // over kSetPinMax: inputs uploaded and outputs downloaded per call from the
+  // callers' own (pageable) buffers, descriptors and results in host memory
+  const bool pageable = pin_need > kSetPinMax;
+  std::vector<uint8_t> host_meta;
+  if (pageable) {
+    bulk_out = false;
+    host_meta.resize(meta_bytes + res_bytes + 64);
+  }
+  if (!pageable && C.pin_cap < pin_need) {
+    // grow geometrically from 4 MiB up to kSetPinMax: a run of slightly
+    // larger batches reallocates (and synchronises the device, hipHostFree /
+    // hipHostMalloc, stalling the other sets' batches) O(log) times
+    const size_t want = std::max({pin_need, std::min(C.pin_cap * 2, kSetPinMax), kSetFloor});
     if (C.pin) (void)hipHostFree(C.pin);
     C.pin = nullptr;
     C.pin_cap = 0;
@@ -377,17 +424,25 @@ void run_batch(BatchSet& C, const std::vector<OneCall*>& b) {
   uint8_t* d_meta = static_cast<uint8_t*>(C.meta.get(std::max(meta_bytes + res_bytes + 16, kSetFloor / 4)));
   if (!d_io || !d_ws || !d_meta) return fail_all(SZ_ERROR_MEM, "LzmaDecode: device allocation failed");
   // pack inputs and metadata, one upload each
-  uint8_t* pin_meta = C.pin + in_total;
-  for (size_t i = 0; i < k; ++i)
-    if (b[i]->in_size) memcpy(C.pin + d[i].src_off, b[i]->src, b[i]->in_size);
+  uint8_t* pin_meta = pageable ? host_meta.data() : C.pin + in_total;
+  if (!pageable)
+    for (size_t i = 0; i < k; ++i)
+      if (b[i]->in_size) memcpy(C.pin + d[i].src_off, b[i]->src, b[i]->in_size);
   memcpy(pin_meta, d.data(), k * sizeof(LzmaGpuStreamDesc));
   memcpy(pin_meta + align16(k * sizeof(LzmaGpuStreamDesc)), order.data(), k * sizeof(uint32_t));
   const hipStream_t st = C.stream;
   LzmaGpuResult* pin_res = reinterpret_cast<LzmaGpuResult*>(pin_meta + meta_bytes);
   LzmaGpuResult* d_res = reinterpret_cast<LzmaGpuResult*>(d_meta + meta_bytes);
   pc.mark(kTStage);
-  if ((in_total && xfer(d_io, C.pin, in_total, hipMemcpyHostToDevice, st) != hipSuccess) ||
-      xfer(d_meta, pin_meta, meta_bytes, hipMemcpyHostToDevice, st) != hipSuccess)
+  bool up_ok = true;
+  if (pageable) {
+    for (size_t i = 0; i < k && up_ok; ++i)
+      up_ok = !b[i]->in_size || xfer(d_io + d[i].src_off, b[i]->src, b[i]->in_size,
+                                     hipMemcpyHostToDevice, st) == hipSuccess;
+  } else {
+    up_ok = !in_total || xfer(d_io, C.pin, in_total, hipMemcpyHostToDevice, st) == hipSuccess;
+  }
+  if (!up_ok || xfer(d_meta, pin_meta, meta_bytes, hipMemcpyHostToDevice, st) != hipSuccess)
     return fail_all(SZ_ERROR_FAIL, "LzmaDecode: upload failed");
   pc.mark(kTUpload);
   if (LzmaGpu_DecodeBatchEx(&plan, reinterpret_cast<LzmaGpuStreamDesc*>(d_meta),
@@ -742,6 +797,7 @@ struct SessSet {
   std::vector<LzgpuSession> h;  // its host copy
   hipStream_t stream = nullptr;
   bool busy = false;
+  bool broken = false;  // its stream could not be created: not picked (group_commit)
 };
 
 struct SessCoalescer {
@@ -897,7 +953,10 @@ SRes gpu_session_call(CLzmaDec* p, int mode, SizeT dicLimit, const Byte* src, Si
   // small transfers go through the scratch's pinned staging (layout: input |
   // table up; after the launch: table down | decoded bytes)
   const size_t tab_bytes = size_t(cells) * 2, tab_pad = (tab_bytes + 15) & ~size_t(15);
-  const size_t down_max = tab_pad + (mode == 1 ? out_room : size_t(p->dicBufSize));
+  // (DecodeToDic downloads at most dic[dicPos, dicLimit), not the whole ring:
+  // ADVICE r05, many callers on multi-MiB dictionaries)
+  const size_t dic_room = dicLimit > p->dicPos ? size_t(dicLimit - p->dicPos) : 0;
+  const size_t down_max = tab_pad + (mode == 1 ? out_room : dic_room);
   uint8_t* pin = lzgpu_host::scratch_pinned(L.s, std::max(in_pad + tab_pad, down_max));
   // the table: the device copy is current after every successful call
   if (!m->probs_dev) {
@@ -964,7 +1023,8 @@ SRes gpu_session_call(CLzmaDec* p, int mode, SizeT dicLimit, const Byte* src, Si
   // decoded bytes (DecodeToDic's new dictionary bytes, DecodeToBuf's output),
   // in one synchronisation, into the pinned staging when there is one
   if (mode == 0) {
-    if (q.dic_pos < pos0 || q.dic_pos > p->dicBufSize) return fail("LzmaDec: bad session state");
+    if (q.dic_pos < pos0 || q.dic_pos > p->dicBufSize || q.dic_pos > std::max<SizeT>(dicLimit, pos0))
+      return fail("LzmaDec: bad session state");
   } else if (q.out_len > out_room || q.dic_pos > p->dicBufSize) {
     return fail("LzmaDec: bad session state");
   }

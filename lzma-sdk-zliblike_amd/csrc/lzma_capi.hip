@@ -531,6 +531,7 @@ SRes LzmaGpu_PlanBatchEx(LzmaGpuStreamDesc* descs, size_t n, uint32_t* order,
 
 SRes LzmaGpu_PlanBatchOpt(LzmaGpuStreamDesc* descs, size_t n, uint32_t* order, LzmaGpuPlan* plan,
                           const LzmaGpuPlanOptions* opt) {
+  if (opt && (opt->flags & ~LZMA_GPU_PLAN_KNOWN_FLAGS)) return SZ_ERROR_PARAM;
   return plan_batch_nothrow(descs, n, order, plan, opt ? *opt : env_options());
 }
 

@@ -51,9 +51,6 @@ enum : int { kOk = 0, kErrData = 1, kErrMem = 2, kErrUnsupported = 4, kErrParam 
 // internal (never returned to a caller): the fast tail of a one-shot decode
 // met a symbol that needs input past the stream's end; decode it again exactly
 constexpr int kRetryExact = 99;
-#ifndef LZGPU_LEN_PF
-#define LZGPU_LEN_PF 0  // 1: length coders preloaded ahead of the literal batch (unmeasured A/B)
-#endif
 #ifndef LZGPU_FAST_TAIL
 #define LZGPU_FAST_TAIL 1  // 0: probe every symbol of the last 20 bytes (A/B)
 #endif
@@ -253,8 +250,50 @@ struct LS {
 #ifndef LZGPU_LIT_BATCH
 #define LZGPU_LIT_BATCH 8
 #endif
+// The decision's instruction form (Rc::decide): form 1 where the one-stream
+// kernel runs (LZGPU_BIT_FORM=1, default: config 2 +2.6 %, config 5 +1 %),
+// form 0 elsewhere (form 1 in the cooperative kernel: config 4 -4 %; in the
+// throughput kernel: config 3 -0.4 %); 0 = form 0 everywhere, 2 = form 1
+// everywhere (A/B; round 6).
+#ifndef LZGPU_BIT_FORM
+#define LZGPU_BIT_FORM 1
+#endif
 #ifndef LZGPU_PROF
 #define LZGPU_PROF 0
+#endif
+// LZGPU_PROF=3 (profiling build, never the default; round 6, VERDICT r05 items
+// 3-4): global-memory wait attribution.  At each class of global access the
+// wave waits for all of its outstanding vector-memory operations (vmcnt(0))
+// and the cycles of that wait go to the class: the stores queued before the
+// match path (W_DRAIN), then each class's own loads.  The waits are taken one
+// after another instead of overlapping, so the split says which class holds
+// the wave, not the exact share of the default build's time.
+#if LZGPU_PROF == 3 && !defined(LZGPU_HOST_EMU)
+enum : uint32_t {
+  W_DRAIN,   // stores still queued at the match path's entry (literal bytes, table updates)
+  W_MLIT,    // matched-literal cells (global placements)
+  W_REP,     // IsRep0Long / rep-choice cells in global memory
+  W_LEN,     // length coder
+  W_SLOT,    // distance slot tree
+  W_SPEC,    // SpecPos reverse trees
+  W_ALIGN,   // Align reverse tree
+  W_LENHI,   // LenHigh trees (lengths >= 18)
+  W_COPY,    // match copies and short reps (dictionary reads + their stores)
+  W_MB,      // the matched byte at rep0, loaded at match end
+  W_INPUT,   // input blocks (reader refills)
+  W_PREV,    // the previous byte at a pass's start, the look-ahead probe
+  W_N
+};
+__device__ __forceinline__ void lz_wait_into(uint64_t& acc) {
+  const uint64_t t0 = __builtin_amdgcn_s_memtime();
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+  acc += __builtin_amdgcn_s_memtime() - t0;
+}
+#define LZ_WAIT(arr, k) lz_wait_into((arr)[k])
+#define LZ_WCLS(rc, k) ((rc).wcls = (k))
+#else
+#define LZ_WAIT(arr, k) ((void)0)
+#define LZ_WCLS(rc, k) ((void)0)
 #endif
 
 // LDS history window (round 4, placement bit kWinBit, the wave-cooperative
@@ -399,6 +438,9 @@ struct LzStateT {
   // passes, LzmaDec.c:487-675 / :766-812), [19] tail passes, [20] table init
   uint64_t prof[21];
 #endif
+#if LZGPU_PROF == 3 && !defined(LZGPU_HOST_EMU)
+  uint64_t wprof[W_N];  // wait attribution (cycles per class)
+#endif
 };
 
 template <uint32_t M>
@@ -473,6 +515,11 @@ __device__ __attribute__((aligned(16))) uint32_t g_lz_zero_word[4] = {0, 0, 0, 0
 // next 16-byte aligned block (its low half is taken when win empties, the high
 // half 8 bytes later, and only then is the following block requested), so one
 // load and one drain per 16 input bytes.
+// (Round 6 measured keeping the prefetched block in the load's own registers
+// with wave-uniform refills on the one-stream and cooperative kernels -- the
+// EXEC-masked refill copies the block at once, which waits for the load: config
+// 4 -3.5 %, config 5 -0.9 %, config 2 +-0; the extra branches cost more than the
+// waits.  DESIGN.md §4, round 6.)
 struct GlobalReader16 {
   const gu32* wp;  // next 16-byte block to prefetch (as words)
   uint32_t left;   // 16-byte blocks with a valid byte still to prefetch
@@ -538,6 +585,9 @@ struct GlobalReader16 {
     nb = 8;
     taken += 8;
 #if LZGPU_PROF && !defined(LZGPU_HOST_EMU)
+#if LZGPU_PROF == 3
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // the refill's load (W_INPUT)
+#endif
     prof += __builtin_amdgcn_s_memtime() - t0;
 #endif
   }
@@ -600,6 +650,9 @@ struct GlobalReaderQ {
     blo = (blo >> 32) | (bhi << 32);
     bhi >>= 32;
     if (--bw == 0) {
+#if LZGPU_PROF == 3 && !defined(LZGPU_HOST_EMU)
+      lz_wait_into(prof);  // the prefetched block (wait attribution: W_INPUT)
+#endif
       blo = uint64_t(nx.x) | (uint64_t(nx.y) << 32);
       bhi = uint64_t(nx.z) | (uint64_t(nx.w) << 32);
       bw = 4;
@@ -665,6 +718,15 @@ typedef GlobalReader16 PlainReader;
 // Bit 31 of a placement mask marks the wave-cooperative kernel (kCoopBit: one
 // stream per wave, every lane holding the same state).
 constexpr uint32_t kCoopBit = 0x80000000u;
+// Bit 26 of a placement mask marks the one-stream 32-lane kernel
+// (lzgpu_decode_dup_kernel): every lane of the wave holds the same decoder
+// state, as in the cooperative kernels, but the loads, stores and copies stay
+// those of one lane.
+constexpr uint32_t kDupBit = 0x04000000u;
+template <uint32_t M>
+__host__ __device__ constexpr bool bit_form() {
+  return LZGPU_BIT_FORM >= 2 || (LZGPU_BIT_FORM == 1 && (M & kDupBit) != 0u);
+}
 template <uint32_t M>
 __host__ __device__ constexpr bool def_on() {
   return LZGPU_WIN_DEFER != 0 && win_on<M>() && (M & kCoopBit) != 0u;
@@ -743,6 +805,31 @@ __host__ __device__ constexpr bool uni_on() {
 #ifndef LZGPU_UNI_IF
 #define LZGPU_UNI_IF 2  // 0: plain (EXEC-masked) branches everywhere; 1: NORMALIZE only (A/B)
 #endif
+// Uniform symbol loop (round 6): where every lane holds the same state, the
+// symbol loop decodes one symbol per pass and tests the symbol kind (IsMatch)
+// and its exit as wave-uniform branches.  The literal batch (LZGPU_LIT_BATCH)
+// exists to keep the independent streams of a wave together; on a uniform
+// decoder it only costs lane-mask bookkeeping: its flags (literal run on,
+// match found, stop) are loop-carried lane masks, ~40 scalar mask instructions
+// per literal in the ISA of the one-stream kernel.
+//   0: batch loop everywhere; 1: uniform loop in the one-stream kernel;
+//   2: ... and in the cooperative kernels.
+#ifndef LZGPU_UNI_LOOP
+#define LZGPU_UNI_LOOP 2
+#endif
+template <uint32_t M>
+__host__ __device__ constexpr bool uloop_on() {
+  return (LZGPU_UNI_LOOP >= 1 && (M & kDupBit) != 0u) ||
+         (LZGPU_UNI_LOOP >= 2 && (M & kCoopBit) != 0u);
+}
+// a condition every lane of the wave agrees on, as a uniform branch
+__device__ __forceinline__ bool lz_uni(bool c) {
+#ifndef LZGPU_HOST_EMU
+  return __builtin_amdgcn_ballot_w64(c) != 0;
+#else
+  return c;
+#endif
+}
 template <bool U>
 __device__ __forceinline__ bool lz_if(bool c) {
 #ifndef LZGPU_HOST_EMU
@@ -760,10 +847,22 @@ __device__ __forceinline__ bool lz_br(bool c) {
   return c;
 }
 
-template <class Rd, bool U = false>
+// F: the decision's instruction form (Rc::decide; bit_form<M>())
+template <class P>
+constexpr bool kGlobP = __is_same(P, gu16*) || __is_same(P, GS);
+template <class Rd, bool U = false, bool F = false>
 struct Rc {
   uint32_t range, code;
   Rd* rd;
+#if LZGPU_PROF == 3 && !defined(LZGPU_HOST_EMU)
+  uint64_t* wacc = nullptr;  // wait attribution: accumulators, current class
+  uint32_t wcls = 0;
+  __device__ __forceinline__ void wstamp() {
+    if (wacc) lz_wait_into(wacc[wcls]);
+  }
+#else
+  __device__ __forceinline__ void wstamp() {}
+#endif
   // NORMALIZE (LzmaDec.c:17): shift in one input byte when range < 2^24
   __device__ __forceinline__ void norm() {
     if (lz_if<U>(range < kTop)) {
@@ -778,30 +877,49 @@ struct Rc {
       code = (code << 8) | rd_take_u(*rd);
     }
   }
-  // decision with norm_u (the shared-form update, see bit())
+  // The decision and its probability update on a loaded value p (after
+  // NORMALIZE), IF_BIT_0 / UPDATE_0 / UPDATE_1 of LzmaDec.c:8-16.
+  // Form 0 (rounds 1-5): selects only -- b = (code >= bound), p -= (p - m) >> 5
+  // (arithmetic) with m = 2017 for bit 0 and 0 for bit 1 (UPDATE_0:
+  // p + ((2048 - p) >> 5) == p - ((p - 2017) >> 5); UPDATE_1: p - (p >> 5)).
+  // Form 1 (round 6, LZGPU_BIT_FORM): the subtraction's borrow is the bit
+  // (v_sub_co: code - bound and code < bound in one instruction, the compare
+  // gone) and the update is one multiply-add, p' = (31 p + c) >> 5 with
+  // c = 31 for bit 1 and 2048 for bit 0: p - floor(p / 32) = floor((31 p + 31)
+  // / 32) and p + floor((2048 - p) / 32) = floor((31 p + 2048) / 32) for every
+  // 0 <= p <= 2048 (checked for all p by tests/test_emu.py).
   template <class P>
-  __device__ __forceinline__ uint32_t bit_u(P prob) {
-    const uint32_t p = *prob;
-    norm_u();
+  __device__ __forceinline__ uint32_t decide(uint32_t p, P prob) {
     const uint32_t bound = (range >> 11) * p;
+    if constexpr (F) {
+    uint32_t t;
+    const bool borrow = __builtin_sub_overflow(code, bound, &t);
+    code = borrow ? code : t;
+    range = borrow ? bound : range - bound;
+    *prob = uint16_t((p * 31u + (borrow ? 2048u : 31u)) >> 5);
+    return borrow ? 0u : 1u;
+    } else {
     const bool b = code >= bound;
     const int32_t m = b ? 0 : int32_t(kProbOne - 31);
     *prob = uint16_t(int32_t(p) - ((int32_t(p) - m) >> 5));
     range = b ? range - bound : bound;
     code = b ? code - bound : code;
     return b ? 1u : 0u;
+    }
+  }
+  // decision with norm_u
+  template <class P>
+  __device__ __forceinline__ uint32_t bit_u(P prob) {
+    const uint32_t p = *prob;
+    if constexpr (kGlobP<P>) wstamp();
+    norm_u();
+    return decide(p, prob);
   }
   // decision on a preloaded value p with norm_u
   template <class P>
   __device__ __forceinline__ uint32_t bit_vu(uint32_t p, P prob) {
     norm_u();
-    const uint32_t bound = (range >> 11) * p;
-    const bool b = code >= bound;
-    const int32_t m = b ? 0 : int32_t(kProbOne - 31);
-    *prob = uint16_t(int32_t(p) - ((int32_t(p) - m) >> 5));
-    range = b ? range - bound : bound;
-    code = b ? code - bound : code;
-    return b ? 1u : 0u;
+    return decide(p, prob);
   }
   // BITS levels of an MSB-first tree from node m (no refill checks: at most
   // 5 levels after a checkpoint); returns the node reached
@@ -815,29 +933,15 @@ struct Rc {
   template <class P>
   __device__ __forceinline__ uint32_t bit(P prob) {
     const uint32_t p = *prob;
+    if constexpr (kGlobP<P>) wstamp();
     norm();
-    const uint32_t bound = (range >> 11) * p;
-    // selects only: with b = (code >= bound),
-    //   UPDATE_0: p + ((2048 - p) >> 5) == p - ((p - 2017) >> 5)  (arithmetic >>)
-    //   UPDATE_1: p - (p >> 5)          == p - ((p - 0) >> 5)
-    const bool b = code >= bound;
-    const int32_t m = b ? 0 : int32_t(kProbOne - 31);
-    *prob = uint16_t(int32_t(p) - ((int32_t(p) - m) >> 5));
-    range = b ? range - bound : bound;
-    code = b ? code - bound : code;
-    return b ? 1u : 0u;
+    return decide(p, prob);
   }
   // decision on an already-loaded probability value p, update stored to *prob
   template <class P>
   __device__ __forceinline__ uint32_t bit_v(uint32_t p, P prob) {
     norm();
-    const uint32_t bound = (range >> 11) * p;
-    const bool b = code >= bound;
-    const int32_t m = b ? 0 : int32_t(kProbOne - 31);
-    *prob = uint16_t(int32_t(p) - ((int32_t(p) - m) >> 5));
-    range = b ? range - bound : bound;
-    code = b ? code - bound : code;
-    return b ? 1u : 0u;
+    return decide(p, prob);
   }
   // MSB-first bit tree of BITS levels (TREE_DECODE); returns [0, 1 << BITS)
   template <int BITS, class P>
@@ -857,6 +961,7 @@ struct Rc {
     const uint32_t c0 = probs[root], c10 = probs[r2], c11 = probs[r2 + 1];
     const uint32_t c20 = probs[r4], c21 = probs[r4 + 1], c22 = probs[r4 + 2],
                    c23 = probs[r4 + 3];
+    if constexpr (kGlobP<P>) wstamp();
     const uint32_t b0 = bit_v(c0, probs + root);
     uint32_t m = r2 + b0;
     const uint32_t b1 = bit_v(b0 ? c11 : c10, probs + m);
@@ -870,6 +975,7 @@ struct Rc {
   template <class P>
   __device__ __forceinline__ uint32_t sub2(P probs, uint32_t root) {
     const uint32_t c0 = probs[root], c10 = probs[2 * root], c11 = probs[2 * root + 1];
+    if constexpr (kGlobP<P>) wstamp();
     const uint32_t b0 = bit_v(c0, probs + root);
     const uint32_t m = 2 * root + b0;
     const uint32_t b1 = bit_v(b0 ? c11 : c10, probs + m);
@@ -891,6 +997,7 @@ struct Rc {
     for (int k = 0; k < 4; ++k) c4[k] = probs[r4 + k];
 #pragma unroll
     for (int k = 0; k < 8; ++k) c8[k] = probs[r8 + k];
+    if constexpr (kGlobP<P>) wstamp();
     const uint32_t b0 = dec(c1, probs + root);
     uint32_t m = r2 + b0;
     const uint32_t p1 = b0 ? c2[1] : c2[0];
@@ -919,6 +1026,7 @@ struct Rc {
   }
   template <class P>
   __device__ __forceinline__ uint32_t dec3(P probs, uint32_t root, const uint32_t* c) {
+    if constexpr (kGlobP<P>) wstamp();
     const uint32_t b0 = bit_v(c[0], probs + root);
     uint32_t m = 2 * root + b0;
     const uint32_t b1 = bit_v(b0 ? c[2] : c[1], probs + m);
@@ -967,8 +1075,8 @@ __device__ __forceinline__ uint32_t lz_lane_id() { return __lane_id(); }
 // (code >= 2^31 + (R >> k): only a corrupt stream) takes the chunk bit by
 // bit.  Returns with range >= 2^24 not guaranteed (the caller's next decision
 // normalises first, as the reference does).
-template <class Rd, bool U>
-__device__ __forceinline__ void direct_coop(Rc<Rd, U>& rc, uint32_t& dist, uint32_t left) {
+template <class Rd, bool U, bool F>
+__device__ __forceinline__ void direct_coop(Rc<Rd, U, F>& rc, uint32_t& dist, uint32_t left) {
 #ifndef LZGPU_HOST_EMU
   const uint32_t j = lz_lane_id() & 31u;
 #endif
@@ -1285,8 +1393,8 @@ __device__ __forceinline__ void lz_emit(gbyte* dic, uint64_t pos, uint32_t v, Lz
 // Literal-tree cell for reference literal offset `rel` (0..0x2FF) of context ctx:
 // plain part for rel < 0x100, matched part above.  Both parts in LDS (or both
 // global) -> a branch-free offset select; split placement -> a real branch.
-template <uint32_t M, class Lo, class Rd, bool U>
-__device__ __forceinline__ uint32_t lit_bit(Rc<Rd, U>& rc, const Tab<M, Lo>& T, uint32_t ctx,
+template <uint32_t M, class Lo, class Rd, bool U, bool F>
+__device__ __forceinline__ uint32_t lit_bit(Rc<Rd, U, F>& rc, const Tab<M, Lo>& T, uint32_t ctx,
                                             uint32_t offs_mbit, uint32_t sym) {
   constexpr bool p_lds = ((M >> S_LITP) & 1u) != 0u, m_lds = ((M >> S_LITM) & 1u) != 0u;
   if constexpr (p_lds == m_lds) {
@@ -1304,8 +1412,8 @@ __device__ __forceinline__ uint32_t lit_bit(Rc<Rd, U>& rc, const Tab<M, Lo>& T, 
 
 // One literal (LzmaDec.c:161-196): plain tree for state < 7, matched tree
 // against the byte at rep0 otherwise; writes the byte, updates state.
-template <uint32_t M, class Lo, class Rd, bool U>
-__device__ __forceinline__ void lz_literal(Rc<Rd, U>& rc, const Tab<M, Lo>& T, uint32_t& st,
+template <uint32_t M, class Lo, class Rd, bool U, bool F>
+__device__ __forceinline__ void lz_literal(Rc<Rd, U, F>& rc, const Tab<M, Lo>& T, uint32_t& st,
                                            uint32_t& prev, uint32_t& total, uint32_t full,
                                            uint32_t lc, uint32_t lp_mask, gbyte* dic,
                                            uint64_t& pos, uint64_t cap, uint32_t r0,
@@ -1336,6 +1444,8 @@ __device__ __forceinline__ void lz_literal(Rc<Rd, U>& rc, const Tab<M, Lo>& T, u
 #pragma unroll
       for (int k = 0; k < 8; ++k)
         pk[k] = lm[(((mb >> (7 - k)) & 1u) << 8) + ((1u << k) | (mb >> (8 - k)))];
+      LZ_WCLS(rc, W_MLIT);
+      rc.wstamp();
       bool matched = true;
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
@@ -1351,6 +1461,7 @@ __device__ __forceinline__ void lz_literal(Rc<Rd, U>& rc, const Tab<M, Lo>& T, u
       }
     } else {
       uint32_t offs = 0x100;
+      LZ_WCLS(rc, W_MLIT);
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         mbyte <<= 1;
@@ -1414,14 +1525,22 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
   uint32_t total = s.total;
   const uint32_t full = s.full;
   uint32_t len = 0;
-  constexpr bool kU = uni_on<M>();  // wave-uniform decoder state (lz_br)
-  Rc<Rd, kU> rc{s.range, s.code, &rd};
+  // wave-uniform decoder state: NORMALIZE as a uniform branch (Rc), symbol
+  // kinds (lz_br), the uniform symbol loop (kUL)
+  constexpr bool kUN = uni_on<M>();
+  constexpr bool kU = uni_on<M>();
+  constexpr bool kUL = uloop_on<M>();
+  Rc<Rd, kUN, bit_form<M>()> rc{s.range, s.code, &rd};
+#if LZGPU_PROF == 3 && !defined(LZGPU_HOST_EMU)
+  rc.wacc = s.wprof;
+#endif
   // previous byte (literal context), kept in a register
   uint32_t prev = 0;
   if (full != 0 || total != 0) prev = dic[(pos == 0 ? cap : pos) - 1];
   // byte at distance rep0, needed by a matched literal (state >= 7)
   uint32_t mb_pf = 0;
   if constexpr (mb_pf_on<M>()) mb_pf = (st >= 7) ? uint32_t(dic[ring_back(pos, r0, cap)]) : 0u;
+  LZ_WAIT(s.wprof, W_PREV);
 
   uint32_t ps = 0;
 #if LZGPU_PROF && !defined(LZGPU_HOST_EMU)
@@ -1429,29 +1548,24 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
 #endif
   do {
     uint32_t lcoder_is_rep;
+    if constexpr (kUL) {
+      // one symbol per pass, kind and loop exit as uniform branches
+      ps = total & pb_mask;
+      rd_topup(rd);
+      const uint32_t ism = rc.bit_u(T.template at<S_MATCH>((st << pb) + ps));
+      if (!lz_uni(ism != 0)) {
+        lz_literal<M>(rc, T, st, prev, total, full, lc, lp_mask, dic, pos, cap, r0, mb_pf,
+                      &s.win);
+        LZ_PROF_MARK(s, 0, t_prof);
+        continue;
+      }
+      LZ_PROF_MARK(s, 0, t_prof);
+    } else {
     // Up to LZGPU_LIT_BATCH symbols per pass of this loop while they are
     // literals: a lane's symbol sequence is unchanged, but lanes of a wave
     // that sit in literal runs keep decoding together instead of idling
     // behind a neighbour's match path on every symbol.
     bool is_match = false, stop = false;
-    // Throughput placement with pb = 0 (every symbol in posState 0): both
-    // length coders' choice bit and low tree (lengths 2..9) are loaded here,
-    // ahead of the literal batch's byte stores.  On gfx950 loads and stores
-    // share one in-order vmcnt queue, so the match path's first global load
-    // otherwise waits for every store of the batch to drain.
-    constexpr bool kLenPf = LZGPU_LEN_PF != 0 && (M & ~kIlvBit) == LZGPU_LDS_MASK;
-    // plain scalars, not arrays: a select between two array elements becomes
-    // a load through a selected pointer and puts the array in scratch
-    uint32_t ca = 0, cb = 0, a1 = 0, a2 = 0, a3 = 0, a4 = 0, a5 = 0, a6 = 0, a7 = 0;
-    uint32_t b1 = 0, b2 = 0, b3 = 0, b4 = 0, b5 = 0, b6 = 0, b7 = 0;
-    if constexpr (kLenPf) {
-      if (pb == 0) {
-        auto l0 = T.g(T.L.o[S_LEN]);
-        auto l1 = T.g(T.L.o[S_REPLEN]);
-        ca = l0[0]; a1 = l0[3]; a2 = l0[4]; a3 = l0[5]; a4 = l0[6]; a5 = l0[7]; a6 = l0[8]; a7 = l0[9];
-        cb = l1[0]; b1 = l1[3]; b2 = l1[4]; b3 = l1[5]; b4 = l1[6]; b5 = l1[7]; b6 = l1[8]; b7 = l1[9];
-      }
-    }
     // lanes leave the batch by clearing lit_on, the loop itself exits only
     // when the whole wave is done: no divergent exit, so no per-iteration
     // copies of the lane state into exit registers
@@ -1461,7 +1575,7 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
 #if LZGPU_PROF && !defined(LZGPU_HOST_EMU)
       const uint64_t t_it = lz_clock();
 #endif
-#if LZGPU_PROF >= 2 && !defined(LZGPU_HOST_EMU)
+#if LZGPU_PROF == 2 && !defined(LZGPU_HOST_EMU)
       {
         const uint64_t on = __builtin_amdgcn_ballot_w64(lit_on);
         const uint64_t ml = __builtin_amdgcn_ballot_w64(lit_on && st >= 7);
@@ -1519,7 +1633,7 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
 #endif
     }
     LZ_PROF_MARK(s, 0, t_prof);
-#if LZGPU_PROF >= 2 && !defined(LZGPU_HOST_EMU)
+#if LZGPU_PROF == 2 && !defined(LZGPU_HOST_EMU)
     {
       const uint64_t mm = __builtin_amdgcn_ballot_w64(is_match && !stop);
       s.prof[9] += mm ? 1 : 0;
@@ -1529,6 +1643,9 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
 #endif
     if (stop) break;
     if (!is_match) continue;
+    }
+    LZ_WAIT(s.wprof, W_DRAIN);  // wait attribution: the stores queued so far
+    LZ_WCLS(rc, W_REP);
 #if LZGPU_PROF == 1 && !defined(LZGPU_HOST_EMU)
 #if LZGPU_PROF_DRAIN
     {
@@ -1547,6 +1664,10 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
       if (full == 0 && total == 0) return kErrData;
       if (lz_br<kU>(!rc.bit(T.template at<S_REP>(12 + st)))) {
         if (lz_br<kU>(!rc.bit(T.template at<S_REP0L>((st << pb) + ps)))) {
+#if LZGPU_PROF == 3 && !defined(LZGPU_HOST_EMU)
+          LZ_WAIT(s.wprof, W_DRAIN);
+          const uint64_t tc0 = lz_clock();
+#endif
           if constexpr ((M & kCoopBit) != 0u) {
             // short rep = a one-byte copy: the byte and the next matched byte
             // in one load batch
@@ -1558,6 +1679,10 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
             lz_put(dic + pos++, prev);
             if constexpr (mb_pf_on<M>()) mb_pf = dic[ring_back(pos, r0, cap)];
           }
+#if LZGPU_PROF == 3 && !defined(LZGPU_HOST_EMU)
+          __builtin_amdgcn_s_waitcnt(0x0F70);
+          s.wprof[W_COPY] += lz_clock() - tc0;
+#endif
           total++;
           st = (st < 7) ? 9 : 11;
           continue;
@@ -1587,6 +1712,7 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
 #endif
     {
       // length coder of this match kind (LzmaDec.c:261-292)
+      LZ_WCLS(rc, W_LEN);
       const uint32_t lsec_o = lcoder_is_rep ? T.L.o[S_REPLEN] : T.L.o[S_LEN];
       static_assert(((M >> S_LEN) & 1u) == ((M >> S_REPLEN) & 1u), "Len/RepLen placement");
       constexpr bool len_lds = ((M >> S_LEN) & 1u) != 0u;
@@ -1605,44 +1731,37 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
         uint32_t clo[7], cmid[7];
         rc.load7(lo_t, 1, clo);
         rc.load7(mid_t, 1, cmid);
+        rc.wstamp();
         if (!rc.bit_v(ch, lbase))
           len = rc.dec3(lo_t, 1, clo) - 8;
         else if (!rc.bit_v(ch2, lbase + 1))
           len = rc.dec3(mid_t, 1, cmid);
-        else
+        else {
+          LZ_WCLS(rc, W_LENHI);
           len = 16 + rc.tree8_g(T.template at<S_LENHI>(lcoder_is_rep << 8)) - 256;
-        } else if (kLenPf && pb == 0) {
-        const bool r = lcoder_is_rep != 0;
-        if (!rc.bit_v(r ? cb : ca, lbase)) {
-          // the low tree (lbase + 2, root 1) from the preloaded cells
-          auto lt = lbase + 2;
-          const uint32_t d0 = rc.bit_v(r ? b1 : a1, lt + 1);
-          const uint32_t d1 = rc.bit_v(d0 ? (r ? b3 : a3) : (r ? b2 : a2), lt + 2 + d0);
-          const uint32_t p2 = d0 ? (d1 ? (r ? b7 : a7) : (r ? b6 : a6)) : (d1 ? (r ? b5 : a5) : (r ? b4 : a4));
-          const uint32_t d2 = rc.bit_v(p2, lt + 4 + 2 * d0 + d1);
-          len = 4 * d0 + 2 * d1 + d2;
         }
-        else if (!rc.bit(lbase + 1))
-          len = 8 + rc.sub3(lbase + 10, 1) - 8;
-        else
-          len = 16 + rc.template tree<8>(T.template at<S_LENHI>(lcoder_is_rep << 8));
         } else {
         const uint32_t ch = lbase[0];
         auto lo_t = lbase + 2 + (ps << 3);
+        rc.wstamp();
         if (!rc.bit_v(ch, lbase))
           len = rc.sub3(lo_t, 1) - 8;
         else if (!rc.bit(lbase + 1))
           len = 8 + rc.sub3(lbase + 2 + (8u << pb) + (ps << 3), 1) - 8;
-        else
+        else {
+          LZ_WCLS(rc, W_LENHI);
           len = 16 + rc.template tree<8>(T.template at<S_LENHI>(lcoder_is_rep << 8));
+        }
         }
       } else {
         if (lz_br<kU>(!rc.bit(lbase)))
           len = rc.template tree<3>(lbase + 2 + (ps << 3));
         else if (lz_br<kU>(!rc.bit(lbase + 1)))
           len = 8 + rc.template tree<3>(lbase + 2 + (8u << pb) + (ps << 3));
-        else
+        else {
+          LZ_WCLS(rc, W_LENHI);
           len = 16 + rc.template tree<8>(T.template at<S_LENHI>(lcoder_is_rep << 8));
+        }
       }
     }
 
@@ -1653,6 +1772,7 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
     if (lz_br<kU>(st >= 12)) {
       const uint32_t lstate = len < 4 ? len : 3;
       uint32_t dist;
+      LZ_WCLS(rc, W_SLOT);
       if constexpr (((M >> S_SLOT) & 1u) == 0u) {
         auto sl_t = T.template at<S_SLOT>(lstate << 6);
 #if LZGPU_PROF == 1 && !defined(LZGPU_HOST_EMU)
@@ -1687,6 +1807,7 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
           dist <<= nbits;
           uint32_t mask = 1, node = 1;
           const uint32_t sp = dist - slot - 1;
+          LZ_WCLS(rc, W_SPEC);
           if constexpr (((M >> S_SPEC) & 1u) == 0u) {
             if (nbits >= 3) {
               // first three reverse-tree bits in one load batch
@@ -1724,6 +1845,7 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
 #endif
           dist <<= 4;
           uint32_t node = 1;
+          LZ_WCLS(rc, W_ALIGN);
           if constexpr (((M >> S_ALIGN) & 1u) == 0u) {
             if constexpr ((M & ~kIlvBit) != LZGPU_LDS_MASK) {
               // all four reverse bits from one batch of the 15 cells
@@ -1774,17 +1896,32 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
       const uint64_t from = ring_back(pos, r0, cap);
       total += n;
       len -= n;
+#if LZGPU_PROF == 3 && !defined(LZGPU_HOST_EMU)
+      LZ_WAIT(s.wprof, W_DRAIN);  // the match path's table updates
+      const uint64_t tc0 = lz_clock();
+#endif
       if constexpr ((M & kCoopBit) != 0u) {
         prev = lz_copy_coop<win_on<M>(), def_on<M>()>(dic, pos, from, n, r0, cap, mb_pf, &s.win);
         pos += n;
       } else {
         prev = lz_copy(dic, pos, from, n, r0, cap);
         pos += n;
+#if LZGPU_PROF == 3 && !defined(LZGPU_HOST_EMU)
+        __builtin_amdgcn_s_waitcnt(0x0F70);
+        s.wprof[W_COPY] += lz_clock() - tc0;
+#endif
         if constexpr (mb_pf_on<M>()) mb_pf = dic[ring_back(pos, r0, cap)];
+        LZ_WAIT(s.wprof, W_MB);
       }
+#if LZGPU_PROF == 3 && !defined(LZGPU_HOST_EMU)
+      if constexpr ((M & kCoopBit) != 0u) {
+        __builtin_amdgcn_s_waitcnt(0x0F70);
+        s.wprof[W_COPY] += lz_clock() - tc0;
+      }
+#endif
     }
     LZ_PROF_MARK(s, 2, t_prof);
-  } while (pos < limit && rd.used() < in_limit);
+  } while (kUL ? lz_uni(pos < limit && rd.used() < in_limit) : (pos < limit && rd.used() < in_limit));
 
   if constexpr (def_on<M>()) win_flush(s.win, dic, pos);  // the dictionary complete again
   rc.norm();
@@ -2140,7 +2277,11 @@ __device__ __forceinline__ int lz_decode_to_dic(LzStateT<Lo>& s, uint64_t dic_li
       rd.init(src, avail);
       const int rr = lz_run_split<M>(s, dic_limit, rd, in_limit);
 #if LZGPU_PROF && !defined(LZGPU_HOST_EMU)
+#if LZGPU_PROF == 3
+      s.wprof[W_INPUT] += rd.prof;
+#else
       s.prof[4] += rd.prof;
+#endif
       if (tail) {
         s.prof[18] += lz_clock() - t_tail;
         s.prof[19] += 1;

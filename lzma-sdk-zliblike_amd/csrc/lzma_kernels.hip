@@ -133,7 +133,7 @@ __global__ void __launch_bounds__(64, W) lzgpu_decode_dup_kernel(
     const uint32_t z = lz_vzero();
     d.src_off += z;
     d.dst_off += z;
-    const LzmaGpuResult r = lane_decode_lds<M, K2>(d, src, dst, ws, lo, stride, nullptr);
+    const LzmaGpuResult r = lane_decode_lds<M | kDupBit, K2>(d, src, dst, ws, lo, stride, nullptr);
     uint32_t next = 0;
     if (threadIdx.x == 0) {
       results[id] = r;
@@ -508,13 +508,15 @@ extern "C" int lzgpu_launch_session(LzgpuSession* d_sess, uint32_t n, hipStream_
 }
 
 #if LZGPU_PROF
-// profiling builds: read (and optionally clear) the region cycle sums
+// profiling builds: read (and optionally clear) the region cycle sums -- 40
+// counters, out[22] = the build's LZGPU_PROF level
 extern "C" int LzmaGpu_ProfileRead(unsigned long long* out, int reset) {
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(lzgpu::g_lz_prof), 24 * sizeof(unsigned long long)) !=
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(lzgpu::g_lz_prof), 40 * sizeof(unsigned long long)) !=
       hipSuccess)
     return -1;
+  out[22] = LZGPU_PROF;
   if (reset) {
-    unsigned long long z[24] = {};
+    unsigned long long z[40] = {};
     if (hipMemcpyToSymbol(HIP_SYMBOL(lzgpu::g_lz_prof), z, sizeof z) != hipSuccess) return -1;
   }
   return 0;

@@ -19,8 +19,9 @@ typedef LzmaGpuSession LzgpuSession;
 namespace lzgpu {
 
 #if LZGPU_PROF && !defined(LZGPU_HOST_EMU)
-// per-region cycle sums over lanes (profiling builds only)
-__device__ unsigned long long g_lz_prof[24];
+// per-region cycle sums over lanes (profiling builds only); [24, 24 + W_N):
+// the wait attribution of LZGPU_PROF=3
+__device__ unsigned long long g_lz_prof[40];
 #endif
 
 // One batch item with the whole probability table in global memory (the
@@ -140,6 +141,9 @@ __device__ __forceinline__ LzmaGpuResult lane_decode_lds(const LzmaGpuStreamDesc
     int status = kStNone;
 #if LZGPU_PROF && !defined(LZGPU_HOST_EMU)
     for (int k = 0; k < 21; ++k) p.dec.prof[k] = 0;
+#if LZGPU_PROF == 3
+    for (uint32_t k = 0; k < W_N; ++k) p.dec.wprof[k] = 0;
+#endif
     const uint64_t t0 = lz_clock();
 #endif
     r.res = lz2_decode_to_dic<M>(p, d.dst_cap, (const gbyte*)(src + d.src_off), sl,
@@ -148,6 +152,9 @@ __device__ __forceinline__ LzmaGpuResult lane_decode_lds(const LzmaGpuStreamDesc
     p.dec.prof[3] = lz_clock() - t0;
     p.dec.prof[12] = p.dec.total;
     for (int k = 0; k < 21; ++k) atomicAdd(&g_lz_prof[k], (unsigned long long)p.dec.prof[k]);
+#if LZGPU_PROF == 3
+    for (uint32_t k = 0; k < W_N; ++k) atomicAdd(&g_lz_prof[24 + k], (unsigned long long)p.dec.wprof[k]);
+#endif
     atomicAdd(&g_lz_prof[23], 1ull);
 #endif
     r.status = status;
@@ -186,6 +193,9 @@ __device__ __forceinline__ LzmaGpuResult lane_decode_lds(const LzmaGpuStreamDesc
   int status = kStNone;
 #if LZGPU_PROF && !defined(LZGPU_HOST_EMU)
   for (int k = 0; k < 21; ++k) s.prof[k] = 0;
+#if LZGPU_PROF == 3
+  for (uint32_t k = 0; k < W_N; ++k) s.wprof[k] = 0;
+#endif
   const uint64_t t0 = lz_clock();
 #endif
   // the fast tail first; a truncated or corrupt end (kRetryExact) again, with
@@ -206,6 +216,9 @@ __device__ __forceinline__ LzmaGpuResult lane_decode_lds(const LzmaGpuStreamDesc
   s.prof[3] = lz_clock() - t0;
   s.prof[12] = s.total;  // literals + match bytes: decoded bytes
   for (int k = 0; k < 21; ++k) atomicAdd(&g_lz_prof[k], (unsigned long long)s.prof[k]);
+#if LZGPU_PROF == 3
+  for (uint32_t k = 0; k < W_N; ++k) atomicAdd(&g_lz_prof[24 + k], (unsigned long long)s.wprof[k]);
+#endif
   atomicAdd(&g_lz_prof[23], 1ull);
 #endif
   if (res == kOk && status == kStMoreInput) res = kErrInputEof;

@@ -1,6 +1,6 @@
 """Write N config-3 streams (bench.py's workload) as the stream-set files of
 tests/c_host/lzma_c_threads.c into DIR (for profiling the drop-in callers).
-  python scripts/r05/stream_set.py DIR [N]"""
+  python scripts/analysis/stream_set.py DIR [N]"""
 import os
 import sys
 

@@ -5,12 +5,13 @@
 # (counters are collected in runs of their own, never with other tracing).
 set -o pipefail
 TAG=${1:-r01}; shift
-R="$GRAFT_REPO_ROOT"
-OUT="$R/gpurun_out/prof_$TAG"
+R="${GRAFT_REPO_ROOT:-$PWD}"
+# TAG with a slash: an output directory relative to the repo (scripts/gpu.sh)
+case $TAG in */*) OUT="$R/$TAG" ;; *) OUT="$R/gpurun_out/prof_$TAG" ;; esac
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-BARGS="--no-cpu-baseline --no-e2e --no-crc $*"
-sha256sum "$R/lzma-sdk-zliblike_amd/lib/liblzmagpu.so" > "$OUT/binary.sha256"
+BARGS="--no-cpu-baseline --no-e2e --no-crc --no-secondary $*"
+sha256sum "${LZGPU_LIB:-$R/lzma-sdk-zliblike_amd/lib/liblzmagpu.so}" > "$OUT/binary.sha256"
 rocprofv3 -L > "$OUT/counters_list.txt" 2>&1 || true
 echo "== kernel trace"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o kt --output-format csv -- \

@@ -67,6 +67,9 @@ void emu_decode_batch_lds(const LzmaGpuStreamDesc* descs, size_t n, const uint8_
     // the wave-cooperative kernel's instantiation on the latency placement
     results[i] = lane_decode_lds<LZGPU_LDS_MASK_LAT | kCoopBit>(descs[i], src, dst, ws, slab,
                                                                 stride);
+#elif defined(EMU_DUP)
+    // the one-stream 32-lane kernel's instantiation (latency placement)
+    results[i] = lane_decode_lds<LZGPU_LDS_MASK_LAT | kDupBit>(descs[i], src, dst, ws, slab, stride);
 #elif defined(EMU_LAT_MASK)
     // the latency-placement instantiation (the kernels' second LDS variant)
     results[i] = lane_decode_lds<LZGPU_LDS_MASK_LAT>(descs[i], src, dst, ws, slab, stride);

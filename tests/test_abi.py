@@ -175,6 +175,14 @@ def test_plan_batch_workspace_and_order():
     # LZMA_GPU_PLAN_SLICE_ALIGN8: the round-1 8-byte aligned slices (158 dwords)
     pa, _ = L.plan_ex(big, L.plan_options("auto", flags=1))
     assert pa.classes[0].lds_cells_per_lane == 316
+    # 0x80 was LZMA_GPU_PLAN_STEP (removed); a caller still setting
+    # it is refused, not silently given LZMA_GPU_PLAN_NO_SLOTG (now 0x100)
+    order = (ctypes.c_uint32 * len(big))()
+    for bad in (0x80, 0x200, 0x80000000):
+        assert L.lib.LzmaGpu_PlanBatchOpt(big, len(big), order, ctypes.byref(L.Plan()),
+                                          ctypes.byref(L.plan_options("auto", flags=bad))) == 5
+    pn, _ = L.plan_ex(big, L.plan_options("auto", flags=0x100))  # NO_SLOTG: accepted
+    assert pn.n_classes == 1
     assert plan.queue_offset % 64 == 0 and plan.workspace_bytes >= plan.queue_offset + 256
 
 

@@ -146,6 +146,39 @@ def test_gpu_c_threads_every_in_flight_setting(tmp_path, inflight, coalesce):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("inflight,faults", [("1", "1"), ("4", "2"), ("2", "5")])
+def test_gpu_stream_creation_failures_never_hang(tmp_path, inflight, faults):
+    """ADVICE r05 (dropin_capi.hip group_commit): a batch set whose stream
+    cannot be created is left out and the call tries another set; when no set
+    is left and no batch runs, the call and every pending one fail at once
+    (SZ_ERROR_FAIL), and later calls create the streams again.  Fault
+    injection: LZGPU_FAULT_STREAM_CREATE=N fails the process's first N stream
+    creations.  48 threads, one-call and DecodeToBuf callers: the program
+    ends (no caller sleeps forever), every stream that decoded has the plain
+    data's CRC, and with a set left over nothing fails at all."""
+    if not os.path.exists(TC.THREADS_BIN):
+        TC.build_c_threads()
+    n = 240
+    plain, comp, lens, props = W.uniform_batch(n, 4096, 0, 0, 0, 4096, first=9000)
+    offs = [0]
+    for ln in lens:
+        offs.append(offs[-1] + int(ln))
+    comps = [comp[offs[i]:offs[i + 1]].tobytes() for i in range(n)]
+    f = TC.write_stream_set(str(tmp_path), comps, [props] * n, [4096] * n)
+    want = 0
+    for i in range(n):
+        want ^= zlib.crc32(plain[i * 4096:(i + 1) * 4096].tobytes(), i)
+    env = dict(os.environ, LZGPU_COALESCE_INFLIGHT=inflight, LZGPU_FAULT_STREAM_CREATE=faults)
+    for mode in ("one", "buf"):
+        d = TC.run_c_threads(TC.THREADS_BIN, 48, f, env=env, mode=mode, timeout=120)
+        if int(faults) < int(inflight):
+            assert d["fails"] == 0 and d["crc_xor"] == "%08x" % want, (mode, d)
+        else:
+            # every set failed once: the calls of that moment fail, the rest decode
+            assert 0 < d["fails"] < n, (mode, d)
+
+
+@pytest.mark.gpu
 def test_gpu_oversized_call_runs_beside_small_ones():
     """a call whose input + capacity exceed the coalescer's item
     limit (dropin_capi.hip kCoalesceItemMax, 256 MiB) runs in a batch of its

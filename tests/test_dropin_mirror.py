@@ -192,7 +192,8 @@ def test_host_edits_between_calls_match_the_reference(L):
         # the dictionary up to the final dicPos (after SZ_ERROR_DATA the
         # reference also leaves the failed pass's bytes beyond dicPos in dic,
         # LzmaDec.c:366-379 returning before the write-back; the drop-in
-        # returns dic[0, dicPos) -- DESIGN.md §2)
+        # returns dic[0, dicPos) -- the documented difference in
+        # include/lzma_gpu.h's header comment, INTEGRATION.md and DESIGN.md §2)
         end = want[0][-1][3]
         assert got[1][:end] == want[1][:end], edit
         if edit is None:

@@ -38,10 +38,6 @@ EMU_VARIANTS = {
     # round 5: the latency placement with the slot trees global (the planner's
     # choice for classes whose widest slice would cost workgroups per CU)
     "latency_slot_global": "-DLZGPU_LDS_MASK_LAT=0x19F -DEMU_LAT_MASK",
-    # round 5 (opt-in, GPU A/B pending): length coders preloaded ahead of the
-    # literal batch in the throughput placement (pb = 0 streams)
-    "length_preload": "-DLZGPU_LEN_PF=1",
-    "length_preload_interleaved": "-DLZGPU_LEN_PF=1 -DEMU_ILV",
     "interleaved_global_instantiation": "-DEMU_ILV",
     "coop_instantiation": "-DEMU_COOP",
     "coop_all_lds_instantiation": "-DEMU_COOP_ALL",
@@ -52,6 +48,22 @@ EMU_VARIANTS = {
     "coop_window_64k": "-DEMU_COOP_ALL_WIN -DEMU_WIN_BYTES=65536",
     "session_coop_window_4k": "-DEMU_SESS_COOP_WIN -DEMU_WIN_BYTES=4096",
     "session_coop_window_64k": "-DEMU_SESS_COOP_WIN -DEMU_WIN_BYTES=65536",
+    # round 6: the one-stream 32-lane kernel's instantiation, and the uniform
+    # symbol loop (one symbol per pass, uniform kind / exit branches) in it and
+    # in the cooperative kernels, with and without uniform symbol-kind branches
+    "dup_instantiation": "-DEMU_DUP",
+    "dup_uniform_loop": "-DLZGPU_UNI_LOOP=1 -DEMU_DUP",
+    "dup_uniform_loop_slot_global": "-DLZGPU_UNI_LOOP=1 -DLZGPU_LDS_MASK_LAT=0x19F -DEMU_DUP",
+    "coop_uniform_loop": "-DLZGPU_UNI_LOOP=2 -DEMU_COOP",
+    "coop_window_uniform_loop": "-DLZGPU_UNI_LOOP=2 -DEMU_COOP_ALL_WIN -DEMU_WIN_BYTES=4096",
+    "session_coop_window_uniform_loop": "-DLZGPU_UNI_LOOP=2 -DEMU_SESS_COOP_WIN -DEMU_WIN_BYTES=4096",
+    # round 6: the decision as borrow + one multiply-add update (Rc::decide form 1)
+    # (defaults since round 6: uniform loop 2, decision form 1; the A/B forms)
+    "bit_form_0_dup": "-DLZGPU_BIT_FORM=0 -DEMU_DUP",
+    "bit_form_2": "-DLZGPU_BIT_FORM=2",
+    "bit_form_2_coop_window": "-DLZGPU_BIT_FORM=2 -DEMU_COOP_ALL_WIN -DEMU_WIN_BYTES=4096",
+    "dup_batch_loop": "-DLZGPU_UNI_LOOP=0 -DEMU_DUP",
+    "coop_window_batch_loop": "-DLZGPU_UNI_LOOP=0 -DEMU_COOP_ALL_WIN -DEMU_WIN_BYTES=4096",
 }
 
 
@@ -230,6 +242,15 @@ def test_emu_fuzz_vs_oracle(emu, lds):
         got = (res[k].res, res[k].status, res[k].dest_len, res[k].src_len)
         out = dst[items[k]["dst_off"]:items[k]["dst_off"] + res[k].dest_len]
         assert got == exp[k][:4] and out == exp[k][4], (k, got, exp[k][:4])
+
+
+def test_update_forms_agree_for_every_probability():
+    """Rc::decide's two update forms equal the reference's UPDATE_0 / UPDATE_1
+    (LzmaDec.c:12-16) for every probability a cell can hold (0..2048)."""
+    for p in range(0, 2049):
+        up0, up1 = p + ((2048 - p) >> 5), p - (p >> 5)
+        assert p - ((p - 2017) >> 5) == up0 and p - (p >> 5) == up1  # form 0 (Python >> is arithmetic)
+        assert (31 * p + 2048) >> 5 == up0 and (31 * p + 31) >> 5 == up1  # form 1
 
 
 def test_direct_chunks_match_serial_direct_bits(tmp_path):
