@@ -813,7 +813,8 @@ def run_cfg4(args):
                                     "gather": gather}},
             "roofline": {"bound": "issue", "priced_against": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
-                         "traffic": None, "kernel": plan_kernels(plan),
+                         "traffic": pmc_traffic("cfg4"), "traffic_source": "profiles/pmc_cfg4.json",
+                         "binary": lib_sha256(), "kernel": plan_kernels(plan),
                          "kernel_avg_ms": round(dec_ms, 4), "alg_bytes_per_launch": alg,
                          "kernel_ms_steps": [round(x, 3) for x in dec_steps]},
             "cpu_baseline": cpu, "verified": ok}), flush=True)
@@ -978,7 +979,8 @@ def run_cfg5(args):
                        "kernel_plan": {"lds_streams": int(plan.n_lds), "classes": cls}},
             "roofline": {"bound": "issue", "priced_against": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
-                         "traffic": None, "kernel": plan_kernels(plan),
+                         "traffic": pmc_traffic("cfg5"), "traffic_source": "profiles/pmc_cfg5.json",
+                         "binary": lib_sha256(), "kernel": plan_kernels(plan),
                          "kernel_avg_ms": round(dec_ms, 4), "alg_bytes_per_launch": alg},
             "sliced": sliced, "cpu_baseline": cpu, "verified": ok}), flush=True)
     if world > 1:
@@ -1683,6 +1685,27 @@ def run_secondary(cfgs, steps=5, warmup=1, timeout=420):
 ISSUE_PEAKS = os.path.join(ROOT, "profiles", "r05_issue", "issue_peaks.json")
 
 
+def pmc_traffic(cfg):
+    """L2<->fabric bytes per launch from the committed PMC summary of `cfg`."""
+    try:
+        return json.load(open(os.path.join(ROOT, "profiles", f"pmc_{cfg}.json"))).get(
+            "hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def lib_sha256():
+    """sha256 of the decode library this process loads (LZGPU_LIB or the
+    in-tree build): the binary the bench line measured, to match against the
+    profiles' binary.sha256."""
+    import hashlib
+    import lzmagpu as L
+    try:
+        return hashlib.sha256(open(L.LIB_PATH, "rb").read()).hexdigest()
+    except OSError:
+        return None
+
+
 def issue_peaks():
     """Measured SIMD issue ceilings (scripts/ubench/simd_issue_ubench.hip, run
     on the box; summarized in profiles/r05_issue/issue_peaks.json): wave-
@@ -1944,14 +1967,11 @@ def main():
             vp, dtp, mp_, _ = cpu_baseline(comp, lens, offs, n, props, thr, count, "port")
             cpu_base["port_MBps"] = round(vp, 2)
 
-    traffic = None
-    tpath = os.path.join(ROOT, "profiles", f"traffic_{args.config}.json")
-    if os.path.exists(tpath):
-        try:
-            traffic = json.load(open(tpath)).get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
+    # traffic and the issue figures from the same committed PMC summary
+    # (profiles/pmc_<cfg>.json: scripts/profile.sh + scripts/pmc_summary.py on
+    # the binary it names; `binary` below is the library this run loaded)
     issue = issue_roofline(args.config, avg_kern_ms, int(plan.waves_per_simd))
+    traffic = issue.get("hbm_bytes_per_launch") if issue else None
     secondary = None
     if rank == 0 and world == 1 and args.config == "cfg3" and not args.no_secondary:
         # reported with their own `verified`; the headline's stands on config 3 alone
@@ -1983,14 +2003,18 @@ def main():
                          "achieved": round(achieved, 3), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 6),
                          "traffic": traffic,
+                         "traffic_source": issue.get("source") if issue else None,
+                         "binary": lib_sha256(),
                          "kernel": plan_kernels(plan),
                          "kernel_avg_ms": round(avg_kern_ms, 4),
                          "kernel_ms_steps": [round(x, 4) for x in kern_ms],
                          "alg_bytes_per_launch": alg_bytes,
                          "issue": issue,
                          "why": "each output byte needs ~5 serially dependent range-coder "
-                                "decisions per stream: the kernel is bound by issue latency "
-                                "(waves parked on s_waitcnt), not by HBM bytes"},
+                                "decisions per stream: the kernel is bound by the latency of "
+                                "that chain at 2 waves per SIMD (forced-wait attribution, "
+                                "LZGPU_PROF=3: global-memory waits ~10 % of wave time), "
+                                "not by HBM bytes"},
             "e2e": e2e,
             "sliced": sliced,
             "cpu_baseline": cpu_base,

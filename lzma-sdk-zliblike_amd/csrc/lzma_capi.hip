@@ -357,6 +357,15 @@ static SRes plan_batch(LzmaGpuStreamDesc* descs, size_t n, uint32_t* order, Lzma
   // One class per width bucket: the throughput placement first; a class that
   // lands in the latency regime is re-planned with the latency placement (more
   // tables in LDS, few streams per CU); few streams per CU go cooperative.
+  // The cooperative kernel is for few streams per CU -- counted over every
+  // LDS-eligible stream of the batch, since the classes run side by side and
+  // share the CUs (round 6: config 5's 4,096-stream share -- 16 per CU -- was
+  // four classes of ~4 per CU, each planned cooperative with the whole CU's
+  // LDS to itself and then starved of it when launched together: 246 ms,
+  // against 132 ms for 16,384 streams of the same mix)
+  size_t lds_total = 0;
+  for (int b = 0; b < LZMA_GPU_MAX_CLASSES; ++b) lds_total += bucket_idx[b].size();
+  const uint64_t per_cu_lds = (lds_total + cus - 1) / cus;
   auto plan_bucket = [&](const std::vector<uint32_t>& idx, uint32_t stride_lo,
                          bool any_groups, bool allow_fit = false) -> LzmaGpuLdsClass {
     bool lat = false;
@@ -378,7 +387,7 @@ static SRes plan_batch(LzmaGpuStreamDesc* descs, size_t n, uint32_t* order, Lzma
     const uint64_t per_cu_batch = (idx.size() + cus - 1) / cus;
     const bool coop = o.kernel == LZMA_GPU_KERNEL_COOP ||
                       (o.kernel == LZMA_GPU_KERNEL_AUTO &&
-                       (o.coop == 1 || (o.coop == 0 && per_cu_batch <= 8)));
+                       (o.coop == 1 || (o.coop == 0 && per_cu_lds <= 8)));
     if (c.lanes_per_group == 1 && coop) {
       c.lds_mask = LZGPU_LDS_MASK_LAT | lzgpu::kCoopBit;
       if (!(o.flags & LZMA_GPU_PLAN_COOP_LAT)) {

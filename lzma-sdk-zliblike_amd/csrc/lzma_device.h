@@ -1646,6 +1646,15 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
     }
     LZ_WAIT(s.wprof, W_DRAIN);  // wait attribution: the stores queued so far
     LZ_WCLS(rc, W_REP);
+    // Under the uniform loop the match path has no exit of its own: a short
+    // rep, the end marker and a data error set xc and skip the rest of the
+    // symbol, and the loop leaves at one uniform test after it.
+    // Exits from inside the symbol's EXEC-masked branches made the compiler
+    // keep a per-lane "which way out" value, its lane masks and copies of the
+    // decoder state on every pass (~17 vector + ~30 scalar instructions per
+    // literal in the one-stream kernel).  Elsewhere xc stays 0 and the exits
+    // are the reference's own returns.
+    uint32_t xc = 0;  // 1: short rep done, 2: end marker, 3: data error
 #if LZGPU_PROF == 1 && !defined(LZGPU_HOST_EMU)
 #if LZGPU_PROF_DRAIN
     {
@@ -1661,7 +1670,12 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
       st += 12;
       lcoder_is_rep = 0;
     } else {
-      if (full == 0 && total == 0) return kErrData;
+      if constexpr (kUL) {
+        xc = (full == 0 && total == 0) ? 3u : 0u;
+      } else {
+        if (full == 0 && total == 0) return kErrData;
+      }
+      if (!kUL || xc == 0) {
       if (lz_br<kU>(!rc.bit(T.template at<S_REP>(12 + st)))) {
         if (lz_br<kU>(!rc.bit(T.template at<S_REP0L>((st << pb) + ps)))) {
 #if LZGPU_PROF == 3 && !defined(LZGPU_HOST_EMU)
@@ -1685,7 +1699,10 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
 #endif
           total++;
           st = (st < 7) ? 9 : 11;
-          continue;
+          if constexpr (kUL)
+            xc = 1;
+          else
+            continue;
         }
       } else {
         uint32_t dist;
@@ -1703,9 +1720,13 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
         r1 = r0;
         r0 = dist;
       }
-      st = (st < 7) ? 8 : 11;
-      lcoder_is_rep = 1;
+      if (!kUL || xc == 0) {
+        st = (st < 7) ? 8 : 11;
+        lcoder_is_rep = 1;
+      }
+      }
     }
+    if (!kUL || xc == 0) {
 #if LZGPU_PROF == 1 && !defined(LZGPU_HOST_EMU)
     const uint64_t tm1 = lz_clock();
     s.prof[8] += tm1 - tm0;
@@ -1872,25 +1893,42 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
           if (dist == 0xFFFFFFFFu) {
             len += kLenDone;
             st -= 12;
-            break;
+            if constexpr (kUL)
+              xc = 2;
+            else
+              break;
           }
         }
       }
+      if (!kUL || xc == 0) {
       r3 = r2;
       r2 = r1;
       r1 = r0;
       r0 = dist + 1;
-      if (full == 0 ? dist >= total : dist >= full) return kErrData;
+      if (full == 0 ? dist >= total : dist >= full) {
+        if constexpr (kUL)
+          xc = 3;
+        else
+          return kErrData;
+      }
       st = (st < 19) ? 7 : 10;
+      }
 #if LZGPU_PROF == 1 && !defined(LZGPU_HOST_EMU)
       s.prof[10] += lz_clock() - tm2;
       s.prof[11] += 1;
 #endif
     }
+    if (!kUL || xc == 0) {
     len += 2;
     LZ_PROF_MARK(s, 1, t_prof);
-    if (limit == pos) return kErrData;
-    {
+    if (limit == pos) {
+      if constexpr (kUL)
+        xc = 3;
+      else
+        return kErrData;
+    }
+    }
+    if (!kUL || xc == 0) {
       const uint64_t room = limit - pos;
       const uint32_t n = (room < len) ? uint32_t(room) : len;
       const uint64_t from = ring_back(pos, r0, cap);
@@ -1920,7 +1958,14 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
       }
 #endif
     }
+    }  // !kUL || xc == 0: length, distance, copy
     LZ_PROF_MARK(s, 2, t_prof);
+    if constexpr (kUL) {
+      if (lz_uni(xc >= 2u)) {
+        if (lz_uni(xc == 3u)) return kErrData;
+        break;  // the end marker
+      }
+    }
   } while (kUL ? lz_uni(pos < limit && rd.used() < in_limit) : (pos < limit && rd.used() < in_limit));
 
   if constexpr (def_on<M>()) win_flush(s.win, dic, pos);  // the dictionary complete again

@@ -15,8 +15,9 @@
 #                              extra bench.py arguments)
 #   profile:CFG[:VARIANT]      kernel trace + separate PMC passes of CFG
 #                              (scripts/profile.sh) -> TAG/prof_CFG
-#   shares:CFG:S1,S2,...       bench --streams S of CFG: one GPU's share of a
-#                              strong-scaling run
+#   shares:CFG:S1,S2,...[:ENV] bench --streams S of CFG: one GPU's share of a
+#                              strong-scaling run (ENV: K=V,K2=V2 planner
+#                              variables for every run of the step)
 #   pmci:CFG:VARIANTS          one PMC pass of instruction counters per
 #                              library (SQ_INSTS_*, waves) -> TAG/pmci_CFG_V
 #   pcs:CFG:VARIANT[:US]       host-trap PC sampling of CFG every US
@@ -72,9 +73,10 @@ for step in "$@"; do
       LZGPU_LIB=$(lib_abs "$b") bash scripts/profile.sh "$O/prof_$a" --config "$a" || exit $? ;;
     shares)
       for s in ${b//,/ }; do
-        f=$O/share_${a}_$s.json
-        timeout -k 10 300 python3 bench.py --config "$a" --streams "$s" $BA > "$f" 2>> "$O/shares.err" || exit $?
-        echo "$a share $s: $(summ "$f")"
+        f=$O/share_${a}_$s${c:+_${c//[=,]/_}}.json
+        env ${c//,/ } timeout -k 10 300 python3 bench.py --config "$a" --streams "$s" $BA > "$f" \
+          2>> "$O/shares.err" || exit $?
+        echo "$a share $s ${c}: $(summ "$f")"
       done ;;
     pmci)
       for v in ${b//,/ }; do

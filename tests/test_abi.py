@@ -221,6 +221,21 @@ def test_plan_options_force_each_instantiation():
     assert all(p.classes[c].lds_mask & COOP for c in range(p.n_classes))
     p, _ = L.plan_ex(descs, L.plan_options("auto", cus=256, coop=2))
     assert not any(p.classes[c].lds_mask & COOP for c in range(p.n_classes))
+    # round 6: the cooperative gate counts the whole batch per CU, not one
+    # width bucket -- four widths x 1,024 streams on 256 CUs (16 per CU in all,
+    # ~4 per bucket) run as one merged one-stream class, not four cooperative
+    # classes that would share the CUs' LDS
+    props4 = [b"\x00\x00\x00\x01\x00", b"\x5d\x00\x00\x01\x00", b"\x02\x00\x00\x01\x00",
+              b"\xb8\x00\x00\x01\x00"]  # lc0, lc3 pb2, lc2, lc4 pb4
+    mix = L.make_descs([dict(src_off=0, src_len=3000, dst_off=65536 * i, dst_cap=65536,
+                             props=props4[i % 4]) for i in range(4096)])
+    pm, _ = L.plan_ex(mix, L.plan_options("auto", cus=256))
+    assert pm.n_classes == 1 and not pm.classes[0].lds_mask & COOP and pm.classes[0].lanes_per_group == 1
+    # ... while few streams per CU in all still go cooperative
+    pf, _ = L.plan_ex(L.make_descs([dict(src_off=0, src_len=3000, dst_off=65536 * i, dst_cap=65536,
+                                         props=props4[i % 4]) for i in range(1024)]),
+                      L.plan_options("auto", cus=256))
+    assert all(pf.classes[c].lds_mask & COOP for c in range(pf.n_classes))
     bad = L.plan_options("auto")
     bad.kernel = 9
     order = (ctypes.c_uint32 * len(items))()
