@@ -889,7 +889,7 @@ struct Rc {
   // / 32) and p + floor((2048 - p) / 32) = floor((31 p + 2048) / 32) for every
   // 0 <= p <= 2048 (checked for all p by tests/test_emu.py).
   template <class P>
-  __device__ __forceinline__ uint32_t decide(uint32_t p, P prob) {
+  __device__ __forceinline__ bool decide_b(uint32_t p, P prob) {
     const uint32_t bound = (range >> 11) * p;
     if constexpr (F) {
     uint32_t t;
@@ -897,14 +897,36 @@ struct Rc {
     code = borrow ? code : t;
     range = borrow ? bound : range - bound;
     *prob = uint16_t((p * 31u + (borrow ? 2048u : 31u)) >> 5);
-    return borrow ? 0u : 1u;
+    return !borrow;
     } else {
     const bool b = code >= bound;
     const int32_t m = b ? 0 : int32_t(kProbOne - 31);
     *prob = uint16_t(int32_t(p) - ((int32_t(p) - m) >> 5));
     range = b ? range - bound : bound;
     code = b ? code - bound : code;
-    return b ? 1u : 0u;
+    return b;
+    }
+  }
+  template <class P>
+  __device__ __forceinline__ uint32_t decide(uint32_t p, P prob) {
+    return decide_b(p, prob) ? 1u : 0u;
+  }
+  // bit_u as a condition (a branch on it needs no 0 / 1 value: the uniform
+  // loop's IsMatch)
+  template <class P>
+  __device__ __forceinline__ bool bit_ub(P prob) {
+    const uint32_t p = *prob;
+    if constexpr (kGlobP<P>) wstamp();
+    norm_u();
+    if constexpr (F) {
+      // the bit as its own compare: a branch on a compare result needs no
+      // 0 / 1 value and mask rebuilt from it (the borrow of form 1 is one;
+      // config 2 +1.2 % with the two changes beside it, round 6)
+      const bool b = code >= (range >> 11) * p;
+      decide_b(p, prob);
+      return b;
+    } else {
+      return decide_b(p, prob);
     }
   }
   // decision with norm_u
@@ -1419,8 +1441,10 @@ __device__ __forceinline__ void lz_literal(Rc<Rd, U, F>& rc, const Tab<M, Lo>& T
                                            uint64_t& pos, uint64_t cap, uint32_t r0,
                                            uint32_t mb_pf, LzWin* w = nullptr) {
   uint32_t sym = 1;
-  uint32_t ctx = 0;
-  if (full != 0 || total != 0) ctx = ((total & lp_mask) << lc) + (prev >> (8 - lc));
+  // (LzmaDec.c:165-166 takes context 0 before the first byte of a dictionary;
+  // prev and total are 0 then, so the formula gives it without a test)
+  const uint32_t ctx = ((total & lp_mask) << lc) + (prev >> (8 - lc));
+  (void)full;
   if (lz_br<U>(st < 7)) {
     st = (st < 4) ? 0 : st - 3;
     auto lp = T.template at<S_LITP>(ctx << 8);
@@ -1541,6 +1565,14 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
   uint32_t mb_pf = 0;
   if constexpr (mb_pf_on<M>()) mb_pf = (st >= 7) ? uint32_t(dic[ring_back(pos, r0, cap)]) : 0u;
   LZ_WAIT(s.wprof, W_PREV);
+#ifndef LZGPU_HOST_EMU
+  // Both loads complete here, before the symbol loop (round 6): a value that
+  // enters the loop with its load outstanding is waited for at its use inside
+  // the loop -- with vmcnt(0), i.e. behind every store in flight -- on every
+  // pass, since the compiler's wait placement cannot tell the first pass from
+  // the others (the one-stream kernel drained its stores at each literal).
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+#endif
 
   uint32_t ps = 0;
 #if LZGPU_PROF && !defined(LZGPU_HOST_EMU)
@@ -1552,8 +1584,8 @@ __device__ __forceinline__ int lz_run(LzStateT<Lo>& s, uint64_t limit, Rd& rd,
       // one symbol per pass, kind and loop exit as uniform branches
       ps = total & pb_mask;
       rd_topup(rd);
-      const uint32_t ism = rc.bit_u(T.template at<S_MATCH>((st << pb) + ps));
-      if (!lz_uni(ism != 0)) {
+      const bool ism = rc.bit_ub(T.template at<S_MATCH>((st << pb) + ps));
+      if (!lz_uni(ism)) {
         lz_literal<M>(rc, T, st, prev, total, full, lc, lp_mask, dic, pos, cap, r0, mb_pf,
                       &s.win);
         LZ_PROF_MARK(s, 0, t_prof);
