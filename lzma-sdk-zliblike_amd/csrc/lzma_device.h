@@ -258,6 +258,9 @@ struct LS {
 #ifndef LZGPU_BIT_FORM
 #define LZGPU_BIT_FORM 1
 #endif
+#ifndef LZGPU_BIT16
+#define LZGPU_BIT16 1  // form 1's update in 16-bit arithmetic (Rc::decide_b)
+#endif
 #ifndef LZGPU_PROF
 #define LZGPU_PROF 0
 #endif
@@ -896,7 +899,19 @@ struct Rc {
     const bool borrow = __builtin_sub_overflow(code, bound, &t);
     code = borrow ? code : t;
     range = borrow ? bound : range - bound;
+#if LZGPU_BIT16
+    // 16-bit arithmetic: 31 p + c <= 31 * 2017 + 2048 < 2^16 -- a cell the
+    // decoder initialised (1024) stays within [31, 2017] under both updates,
+    // and form 1 runs only where the kernel initialises the table itself (the
+    // one-stream batch kernel) -- and a 16-bit multiply-add reads only the
+    // cell's low half (no mask of the loaded value: one VALU instruction per
+    // decision, round 6)
+    const uint16_t p16 = uint16_t(p);
+    const uint16_t c16 = borrow ? uint16_t(2048) : uint16_t(31);
+    *prob = uint16_t(uint16_t(p16 * uint16_t(31) + c16) >> 5);
+#else
     *prob = uint16_t((p * 31u + (borrow ? 2048u : 31u)) >> 5);
+#endif
     return !borrow;
     } else {
     const bool b = code >= bound;
