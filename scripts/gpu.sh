@@ -22,6 +22,7 @@
 #                              library (SQ_INSTS_*, waves) -> TAG/pmci_CFG_V
 #   pcs:CFG:VARIANT[:US]       host-trap PC sampling of CFG every US
 #                              microseconds (default 1) -> TAG/pcs_CFG
+#   smoke                      __graft_entry__.smoke()
 #   coalesce                   the drop-in's concurrent-caller bench
 #   fuzz:N[:VARIANT]           N LZMA (N/5 LZMA2) fuzz cases through every
 #                              instantiation against the oracle
@@ -94,6 +95,9 @@ for step in "$@"; do
           --pc-sampling-interval "${c:-1}" --kernel-trace -d "$d" -o pcs --output-format csv -- \
           python3 "$R0/bench.py" --config "$a" --steps 2 --warmup 0 $BA0 > "$d.json" 2> "$d.err" ) || exit $?
       echo "pcs $a: $(summ "$d.json"); $(find "$d" -name '*.csv' | head -5 | tr '\n' ' ')" ;;
+    smoke)
+      timeout -k 10 400 python3 -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1 || exit $?
+      echo "smoke: $(tail -1 "$O/smoke.log")" ;;
     coalesce)
       timeout -k 10 600 python3 bench.py --config coalesce > "$O/coalesce.json" 2> "$O/coalesce.err" || exit $?
       echo "coalesce: $(head -c 400 "$O/coalesce.json")" ;;
