@@ -20,8 +20,6 @@
 #                              variables for every run of the step)
 #   pmci:CFG:VARIANTS          one PMC pass of instruction counters per
 #                              library (SQ_INSTS_*, waves) -> TAG/pmci_CFG_V
-#   pcs:CFG:VARIANT[:US]       host-trap PC sampling of CFG every US
-#                              microseconds (default 1) -> TAG/pcs_CFG
 #   smoke                      __graft_entry__.smoke()
 #   coalesce                   the drop-in's concurrent-caller bench
 #   fuzz:N[:VARIANT]           N LZMA (N/5 LZMA2) fuzz cases through every
@@ -88,13 +86,6 @@ for step in "$@"; do
             python3 "$R0/bench.py" --config "$a" --steps 2 --warmup 0 $BA0 > "$d.json" 2> "$d.err" ) || exit $?
         echo "pmci $a $v: $(summ "$d.json")"
       done ;;
-    pcs)
-      d=$R0/$O/pcs_$a
-      ( cd /tmp && export TMPDIR=/tmp && LZGPU_LIB=$(lib_abs "$b") timeout -s KILL 300 rocprofv3 \
-          --pc-sampling-beta-enabled --pc-sampling-method host_trap --pc-sampling-unit time \
-          --pc-sampling-interval "${c:-1}" --kernel-trace -d "$d" -o pcs --output-format csv -- \
-          python3 "$R0/bench.py" --config "$a" --steps 2 --warmup 0 $BA0 > "$d.json" 2> "$d.err" ) || exit $?
-      echo "pcs $a: $(summ "$d.json"); $(find "$d" -name '*.csv' | head -5 | tr '\n' ' ')" ;;
     smoke)
       timeout -k 10 400 python3 -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1 || exit $?
       echo "smoke: $(tail -1 "$O/smoke.log")" ;;
