@@ -730,6 +730,56 @@ template <uint32_t M>
 __host__ __device__ constexpr bool bit_form() {
   return LZGPU_BIT_FORM >= 2 || (LZGPU_BIT_FORM == 1 && (M & kDupBit) != 0u);
 }
+// Plain literal tree walked by the cell's LDS address instead of the node
+// (Rc::tree8_a): a' = 2a + (bit ? step - base : -base) is one select and one
+// shift-add per level where the node form takes a shift, a 0 / 1 select, an
+// or and the address's shift-add (and form 1 its bit-mask xor) -- config 2
+// +1.9 %, config 3 +1.8 %, config 5 +0.6 %, config 4 +0.3 % (round 6,
+// DESIGN.md §4).  Bit mask of kernels: 1 one-stream, 2 cooperative, 4 the
+// others (throughput, one-lane latency); 7 = every kernel with the tree in LDS
+// (default).  The same walk in the match path's LDS trees (length, slot,
+// align) measured config 4 -1.3 %, config 2 -1 %, config 5 +0.9 % against it
+// and was removed.
+#ifndef LZGPU_LIT_ADDR
+#define LZGPU_LIT_ADDR 7
+#endif
+template <uint32_t M>
+__host__ __device__ constexpr bool lit_addr_on() {
+  constexpr uint32_t k = (M & kDupBit) != 0u ? 1u : (M & kCoopBit) != 0u ? 2u : 4u;
+  return ((M >> S_LITP) & 1u) != 0u && (LZGPU_LIT_ADDR & k) != 0u;
+}
+// LDS cell addresses as integers (32-bit on the device)
+#ifdef LZGPU_HOST_EMU
+typedef uintptr_t lds_addr_t;
+#else
+typedef uint32_t lds_addr_t;
+#endif
+__host__ __device__ __forceinline__ lds_addr_t lds_addr_of(lds_u16* p) {
+  return lds_addr_t(uintptr_t(p));
+}
+__host__ __device__ __forceinline__ lds_addr_t lds_addr_of(LS p) { return lds_addr_of(p.p); }
+template <class P>
+__host__ __device__ __forceinline__ P lds_at(lds_addr_t a);
+template <>
+__host__ __device__ __forceinline__ lds_u16* lds_at<lds_u16*>(lds_addr_t a) {
+  return (lds_u16*)uintptr_t(a);
+}
+template <>
+__host__ __device__ __forceinline__ LS lds_at<LS>(lds_addr_t a) {
+  return LS{(lds_u16*)uintptr_t(a)};
+}
+template <class P>
+constexpr lds_addr_t kLdsStep = __is_same(P, LS) ? lds_addr_t(2u * kIlv) : lds_addr_t(2u);
+// a value the compiler must not relate to the others (keeps a select of two
+// registers a select)
+template <class T>
+__host__ __device__ __forceinline__ void lz_opaque(T& x) {
+#ifndef LZGPU_HOST_EMU
+  asm("" : "+v"(x));
+#else
+  (void)x;
+#endif
+}
 template <uint32_t M>
 __host__ __device__ constexpr bool def_on() {
   return LZGPU_WIN_DEFER != 0 && win_on<M>() && (M & kCoopBit) != 0u;
@@ -965,6 +1015,24 @@ struct Rc {
 #pragma unroll
     for (int k = 0; k < BITS; ++k) m = (m << 1) | bit_u(probs + m);
     return m;
+  }
+  // The 8-level plain literal tree (as tree_u<4> + rd_topup + tree_u<4>)
+  // walked by the LDS address of the current cell (lit_addr_on); returns the
+  // node (256..511).
+  template <class P>
+  __device__ __forceinline__ uint32_t tree8_a(P probs) {
+    constexpr lds_addr_t st = kLdsStep<P>;
+    const lds_addr_t base = lds_addr_of(probs);
+    lds_addr_t k0 = lds_addr_t(0) - base, k1 = st - base;
+    lz_opaque(k1);
+    lds_addr_t a = base + st;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      if (k == 4) rd_topup(*rd);
+      const uint32_t b = bit_u(lds_at<P>(a));
+      a = (a << 1) + (b ? k1 : k0);
+    }
+    return uint32_t((a - base) / st);
   }
   // one adaptive decision on *prob (any address space), IF_BIT_0/UPDATE_0/1
   template <class P>
@@ -1463,9 +1531,13 @@ __device__ __forceinline__ void lz_literal(Rc<Rd, U, F>& rc, const Tab<M, Lo>& T
   if (lz_br<U>(st < 7)) {
     st = (st < 4) ? 0 : st - 3;
     auto lp = T.template at<S_LITP>(ctx << 8);
-    const uint32_t m = rc.template tree_u<4>(lp, 1);
-    rd_topup(*rc.rd);
-    sym = rc.template tree_u<4>(lp, m);
+    if constexpr (lit_addr_on<M>()) {
+      sym = rc.tree8_a(lp);
+    } else {
+      const uint32_t m = rc.template tree_u<4>(lp, 1);
+      rd_topup(*rc.rd);
+      sym = rc.template tree_u<4>(lp, m);
+    }
   } else {
     uint32_t mbyte = mb_pf_on<M>() ? mb_pf : uint32_t(dic[ring_back(pos, r0, cap)]);
     st = (st < 10) ? st - 3 : st - 6;

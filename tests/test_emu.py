@@ -64,6 +64,10 @@ EMU_VARIANTS = {
     "bit_form_2_coop_window": "-DLZGPU_BIT_FORM=2 -DEMU_COOP_ALL_WIN -DEMU_WIN_BYTES=4096",
     "dup_batch_loop": "-DLZGPU_UNI_LOOP=0 -DEMU_DUP",
     "coop_window_batch_loop": "-DLZGPU_UNI_LOOP=0 -DEMU_COOP_ALL_WIN -DEMU_WIN_BYTES=4096",
+    # the plain literal tree walked by node instead of cell address (LZGPU_LIT_ADDR)
+    "lit_node_walk": "-DLZGPU_LIT_ADDR=0",
+    "lit_node_walk_dup": "-DLZGPU_LIT_ADDR=0 -DEMU_DUP",
+    "lit_node_walk_coop_window": "-DLZGPU_LIT_ADDR=0 -DEMU_COOP_ALL_WIN -DEMU_WIN_BYTES=4096",
 }
 
 
