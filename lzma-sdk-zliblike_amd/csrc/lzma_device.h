@@ -250,13 +250,18 @@ struct LS {
 #ifndef LZGPU_LIT_BATCH
 #define LZGPU_LIT_BATCH 8
 #endif
-// The decision's instruction form (Rc::decide): form 1 where the one-stream
-// kernel runs (LZGPU_BIT_FORM=1, default: config 2 +2.6 %, config 5 +1 %),
-// form 0 elsewhere (form 1 in the cooperative kernel: config 4 -4 %; in the
-// throughput kernel: config 3 -0.4 %); 0 = form 0 everywhere, 2 = form 1
-// everywhere (A/B; round 6).
+// The decision's instruction form (Rc::decide), a bit mask of the kernels
+// that take form 1: 1 the one-stream kernel (config 2 +2.6 %, config 5 +1 %),
+// 4 the other batch kernels with an LDS placement -- throughput and one-lane
+// latency (config 3 +2.6 % once the literal tree walks by address; -0.4 %
+// before), 2 the cooperative kernels (config 4 -4 %, then -0.5 %: not taken).
+// Default 5.  Kernels with no LDS placement bits (the generic batch kernel, the
+// one-lane session kernel on a caller's CLzmaDec table) and the time-sliced
+// session rounds (kSessHybBit) keep form 0: form 1's
+// 16-bit update is exact only on cells the kernel initialised itself (round 6,
+// DESIGN.md §4).
 #ifndef LZGPU_BIT_FORM
-#define LZGPU_BIT_FORM 1
+#define LZGPU_BIT_FORM 5
 #endif
 #ifndef LZGPU_BIT16
 #define LZGPU_BIT16 1  // form 1's update in 16-bit arithmetic (Rc::decide_b)
@@ -728,7 +733,11 @@ constexpr uint32_t kCoopBit = 0x80000000u;
 constexpr uint32_t kDupBit = 0x04000000u;
 template <uint32_t M>
 __host__ __device__ constexpr bool bit_form() {
-  return LZGPU_BIT_FORM >= 2 || (LZGPU_BIT_FORM == 1 && (M & kDupBit) != 0u);
+  constexpr uint32_t k = (M & kDupBit) != 0u    ? 1u
+                         : (M & kCoopBit) != 0u ? 2u
+                         : ((M & 0x7FFu) != 0u && (M & kSessHybBit) == 0u) ? 4u
+                                                                           : 0u;
+  return (LZGPU_BIT_FORM & k) != 0u;
 }
 // Plain literal tree walked by the cell's LDS address instead of the node
 // (Rc::tree8_a): a' = 2a + (bit ? step - base : -base) is one select and one
@@ -953,7 +962,7 @@ struct Rc {
     // 16-bit arithmetic: 31 p + c <= 31 * 2017 + 2048 < 2^16 -- a cell the
     // decoder initialised (1024) stays within [31, 2017] under both updates,
     // and form 1 runs only where the kernel initialises the table itself (the
-    // one-stream batch kernel) -- and a 16-bit multiply-add reads only the
+    // batch kernels, bit_form) -- and a 16-bit multiply-add reads only the
     // cell's low half (no mask of the loaded value: one VALU instruction per
     // decision, round 6)
     const uint16_t p16 = uint16_t(p);

@@ -59,9 +59,11 @@ EMU_VARIANTS = {
     "session_coop_window_uniform_loop": "-DLZGPU_UNI_LOOP=2 -DEMU_SESS_COOP_WIN -DEMU_WIN_BYTES=4096",
     # round 6: the decision as borrow + one multiply-add update (Rc::decide form 1)
     # (defaults since round 6: uniform loop 2, decision form 1; the A/B forms)
-    "bit_form_0_dup": "-DLZGPU_BIT_FORM=0 -DEMU_DUP",
-    "bit_form_2": "-DLZGPU_BIT_FORM=2",
-    "bit_form_2_coop_window": "-DLZGPU_BIT_FORM=2 -DEMU_COOP_ALL_WIN -DEMU_WIN_BYTES=4096",
+    "bit_form_0_dup": "-DLZGPU_BIT_FORM=0",
+    "bit_form_0_dup_kernel": "-DLZGPU_BIT_FORM=0 -DEMU_DUP",
+    "bit_form_0_latency": "-DLZGPU_BIT_FORM=0 -DEMU_LAT_MASK",
+    "bit_form_all_coop_window": "-DLZGPU_BIT_FORM=7 -DEMU_COOP_ALL_WIN -DEMU_WIN_BYTES=4096",
+    "bit_form_all_coop": "-DLZGPU_BIT_FORM=7 -DEMU_COOP",
     "dup_batch_loop": "-DLZGPU_UNI_LOOP=0 -DEMU_DUP",
     "coop_window_batch_loop": "-DLZGPU_UNI_LOOP=0 -DEMU_COOP_ALL_WIN -DEMU_WIN_BYTES=4096",
     # the plain literal tree walked by node instead of cell address (LZGPU_LIT_ADDR)
